@@ -1,0 +1,95 @@
+"""ctypes binding of ``librescore.so`` (declared in ``include/rescore.h``).
+
+The library is built in-tree by ``__graft_entry__.build()`` (hipcc, gfx950).  ``torch`` is
+imported first so that the HIP runtime ``librescore.so`` links against is the one torch
+already loaded (both carry the soname ``libamdhip64.so.7``): device pointers and the
+``hipStream_t`` of ``torch.cuda.current_stream()`` are then valid inside the library.
+There is no CPU fallback: a missing library or GPU raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must load torch's HIP runtime before librescore.so)
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "librescore.so")
+
+RS_HEAD_MLM, RS_HEAD_CLS = 1, 2
+RS_FUSE = {"norm": 0, "legacy": 1, "am_norm": 2}
+KINDS = ["qkv", "oproj", "ffn1", "ffn2", "decoder", "attn", "other"]
+
+
+class RsBertCfg(ctypes.Structure):
+    _fields_ = [("vocab", ctypes.c_int32), ("hidden", ctypes.c_int32), ("layers", ctypes.c_int32),
+                ("heads", ctypes.c_int32), ("intermediate", ctypes.c_int32),
+                ("max_pos", ctypes.c_int32), ("type_vocab", ctypes.c_int32),
+                ("ln_eps", ctypes.c_float), ("mask_id", ctypes.c_int32),
+                ("heads_mask", ctypes.c_int32)]
+
+
+class RescoreError(RuntimeError):
+    pass
+
+
+_lib = None
+P = ctypes.c_void_p
+I32, I64 = ctypes.c_int32, ctypes.c_int64
+
+_SIGS = {
+    "rs_version": (ctypes.c_int, []),
+    "rs_last_error": (ctypes.c_char_p, []),
+    "rs_model_create": (ctypes.c_int, [ctypes.POINTER(RsBertCfg), ctypes.c_int, ctypes.POINTER(P)]),
+    "rs_model_set_tensor": (ctypes.c_int, [P, ctypes.c_char_p, P, ctypes.c_int, ctypes.POINTER(I64), ctypes.c_int]),
+    "rs_model_finalize": (ctypes.c_int, [P]),
+    "rs_model_reserve": (ctypes.c_int, [P, I64]),
+    "rs_pll_score": (ctypes.c_int, [P, P, P, I32, P, P, P]),
+    "rs_masked_logprob": (ctypes.c_int, [P, P, P, P, P, I32, P, P]),
+    "rs_cls_score": (ctypes.c_int, [P, P, P, I32, P, P]),
+    "rs_profile_enable": (ctypes.c_int, [P, ctypes.c_int]),
+    "rs_profile_read": (ctypes.c_int, [P, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(I64), ctypes.POINTER(ctypes.c_double)]),
+    "rs_model_destroy": (None, [P]),
+    "rs_pairwise_edit": (ctypes.c_int, [P, P, P, P, I32, I32, P, P]),
+    "rs_mbr_scores": (ctypes.c_int, [P, P, P, P, I32, I32, P, P, P]),
+    "rs_fuse_rerank": (ctypes.c_int, [P, P, P, P, I32, I32, P, I32, I32, P, P]),
+    "rs_corpus_edits": (ctypes.c_int, [P, P, P, I32, I32, P, P]),
+    "rs_ref_edit": (ctypes.c_int, [P, P, P, P, P, I32, P, P]),
+}
+
+EXPORTED = tuple(_SIGS)
+
+
+def load(path: str = LIB_PATH):
+    """Load and type the library; raises if it was not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"{path} not found: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc != 0:
+        raise RescoreError(f"librescore error {rc}: {load().rs_last_error().decode()}")
+
+
+def ptr(t) -> int:
+    """Device/host pointer of a tensor or numpy array (None -> NULL)."""
+    if t is None:
+        return None
+    if isinstance(t, torch.Tensor):
+        return t.data_ptr()
+    return t.ctypes.data
+
+
+def stream_ptr(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream

@@ -1,0 +1,87 @@
+// Shared definitions for the gfx950 kernels and the C-ABI host code.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef _Float16 f16;
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+#define RS_WAVE 64
+
+// GEMM epilogues (C = A[M,K] . W[N,K]^T, fp32 accumulate):
+enum EpiKind {
+    EPI_BIAS_F16 = 0,   // out16 = acc + bias                      (fused QKV projection)
+    EPI_GELU_F16 = 1,   // out16 = gelu(acc + bias)                (BertIntermediate)
+    EPI_GELU_F32 = 2,   // out32 = gelu(acc + bias)                (MLM transform, pre-LN)
+    EPI_RES_F32 = 3,    // out32 = acc + bias + res32              (BertSelfOutput / BertOutput, pre-LN)
+    EPI_LSE = 4,        // per-row partial (max, sum exp) over a 64-column slab + label logit
+};
+
+struct EpiArgs {
+    const float* bias;     // [N]
+    const float* res;      // [M, ldc] fp32 residual (EPI_RES_F32)
+    void* out;             // [M, ldc]
+    int ldc;
+    int m_valid;           // rows >= m_valid are not stored
+    int n_valid;           // columns >= n_valid are masked (EPI_LSE vocab padding)
+    float2* lse_part;      // [M, n_parts] (max, sum exp) (EPI_LSE)
+    int n_parts;
+    const int* label;      // [M] label column per row (EPI_LSE)
+    float* label_logit;    // [M]
+};
+
+// Per-sequence metadata of a scoring call (structure of arrays, device).  A "sequence"
+// is one BERT input: a masked copy of a hypothesis (MLM_PLL), a hypothesis
+// (RescoreBert) or a caller-provided row (masked_logprob).
+struct SeqMeta {
+    const int* tok_off;    // offset of the sequence's [CLS] in the token buffer
+    const int* len;        // T
+    const int* mask_pos;   // position replaced by [MASK] on device, -1 = none
+    const int* query;      // row whose last-layer state is scored
+    const int* label;      // label id at query, -1 = take tokens[tok_off + query]
+    const int* row;        // first token row of the sequence (global row index)
+};
+
+__device__ __forceinline__ float gelu_erf(float x) {
+    // transformers GELUActivation = nn.functional.gelu (exact erf form)
+    return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+
+// ---- launchers (defined in k_gemm.hip / k_bert.hip / k_rerank.hip) ---------------------
+hipError_t launch_gemm(int epi, const f16* A, const f16* W, int M_pad, int N_pad, int K,
+                       const EpiArgs& ep, hipStream_t st);
+int gemm_row_align();   // M padding granularity required by launch_gemm
+
+hipError_t launch_embed_ln(const int* tok, SeqMeta sm, int s0, int s1, int row0, int mask_id,
+                           int vocab, const float* word, const float* pos, const float* type0,
+                           const float* g, const float* b, float eps, int H, float* h32, f16* h16,
+                           hipStream_t st);
+hipError_t launch_ln_rows(const float* x, int rows, const float* g, const float* b, float eps,
+                          int H, float* y32, f16* y16, hipStream_t st);
+hipError_t launch_attention_full(const f16* qkv, SeqMeta sm, int s0, int s1, int row0, int H,
+                                 int heads, f16* ctx, hipStream_t st);
+hipError_t launch_attention_query(const f16* qkv, const float* h32, SeqMeta sm, int s0, int s1,
+                                  int row0, int H, int heads, f16* ctxq, float* resq,
+                                  hipStream_t st);
+hipError_t launch_gather_labels(const int* tok, SeqMeta sm, int s0, int s1, int* lab,
+                                hipStream_t st);
+hipError_t launch_lse_finalize(const float2* part, int n_parts, const float* label_logit,
+                               int rows, float* out, hipStream_t st);
+hipError_t launch_cls_linear(const float* h, int rows, int H, const float* w, const float* b,
+                             float* out, hipStream_t st);
+hipError_t launch_segsum_f64(const float* row_lp, const int* hyp_seq_off, int n_hyp, double* out,
+                             hipStream_t st);

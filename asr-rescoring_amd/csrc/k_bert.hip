@@ -1,0 +1,364 @@
+// BERT encoder kernels other than the GEMMs (gfx950, wave64).
+//
+//  embed_ln        K1+K2: on-device [MASK] expansion (MLM_PLL/preprocess.py:15-21) fused with
+//                  BertEmbeddings (modeling_bert.py:53-108): word + type[0] + position -> LN
+//  ln_rows         LayerNorm of BertSelfOutput / BertOutput / head transform (eps 1e-12)
+//  attention_full  eager_attention_forward (modeling_bert.py:111-136) over ragged sequences
+//                  (no padding rows: equal to the reference's additive pad mask)
+//  attention_query the same, last layer, only the scored row of each sequence (masked
+//                  position for MLM_PLL, [CLS] for RescoreBert) — the other rows' last-layer
+//                  states never reach a score
+//  lse_finalize    merges the decoder epilogue's (max, sum exp) slabs: log_softmax gather
+//                  (MLM_PLL/main.py:101-105)
+//  cls_linear      RescoreBert Linear(H, 1) on the CLS state (RescoreBert/model.py:19-20)
+//  segsum_f64      per-hypothesis PLL, float64, in row order (MLM_PLL/main.py:106-107)
+#include "common.h"
+
+namespace {
+
+template <int NV>
+__device__ __forceinline__ void ln_store(float4 (&x)[NV], const float* g, const float* b, float eps,
+                                         int lane, float* y32, f16* y16) {
+    constexpr int H = NV * 256;
+    float s = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) s += (x[v].x + x[v].y) + (x[v].z + x[v].w);
+    const float mean = wave_sum(s) * (1.0f / H);
+    float q = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        x[v].x -= mean; x[v].y -= mean; x[v].z -= mean; x[v].w -= mean;
+        q += (x[v].x * x[v].x + x[v].y * x[v].y) + (x[v].z * x[v].z + x[v].w * x[v].w);
+    }
+    const float inv = 1.0f / sqrtf(wave_sum(q) * (1.0f / H) + eps);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int c = v * 256 + lane * 4;
+        const float4 gg = *(const float4*)(g + c);
+        const float4 bb = *(const float4*)(b + c);
+        float4 y;
+        y.x = x[v].x * inv * gg.x + bb.x;
+        y.y = x[v].y * inv * gg.y + bb.y;
+        y.z = x[v].z * inv * gg.z + bb.z;
+        y.w = x[v].w * inv * gg.w + bb.w;
+        *(float4*)(y32 + c) = y;
+        half4 h = {(f16)y.x, (f16)y.y, (f16)y.z, (f16)y.w};
+        *(half4*)(y16 + c) = h;
+    }
+}
+
+template <int NV>
+__global__ void __launch_bounds__(256)
+embed_ln_kernel(const int* __restrict__ tok, SeqMeta sm, int s0, int row0, int mask_id, int vocab,
+                const float* __restrict__ word, const float* __restrict__ pos,
+                const float* __restrict__ type0, const float* __restrict__ g,
+                const float* __restrict__ b, float eps, float* __restrict__ h32,
+                f16* __restrict__ h16) {
+    constexpr int H = NV * 256;
+    const int s = s0 + blockIdx.x;
+    const int T = sm.len[s], toff = sm.tok_off[s], mp = sm.mask_pos[s];
+    const int rs = sm.row[s] - row0;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int t = wave; t < T; t += 4) {
+        int id = (t == mp) ? mask_id : tok[toff + t];
+        id = min(max(id, 0), vocab - 1);          // out-of-range ids are clamped, never read OOB
+        float4 x[NV];
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const int c = v * 256 + lane * 4;
+            const float4 w = *(const float4*)(word + (size_t)id * H + c);
+            const float4 ty = *(const float4*)(type0 + c);
+            const float4 p = *(const float4*)(pos + (size_t)t * H + c);
+            // transformers order: (inputs_embeds + token_type) + position
+            x[v] = make_float4((w.x + ty.x) + p.x, (w.y + ty.y) + p.y, (w.z + ty.z) + p.z, (w.w + ty.w) + p.w);
+        }
+        const size_t o = (size_t)(rs + t) * H;
+        ln_store<NV>(x, g, b, eps, lane, h32 + o, h16 + o);
+    }
+}
+
+template <int NV>
+__global__ void __launch_bounds__(256)
+ln_rows_kernel(const float* __restrict__ xin, int rows, const float* __restrict__ g,
+               const float* __restrict__ b, float eps, float* __restrict__ y32, f16* __restrict__ y16) {
+    constexpr int H = NV * 256;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    float4 x[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) x[v] = *(const float4*)(xin + (size_t)row * H + v * 256 + lane * 4);
+    ln_store<NV>(x, g, b, eps, lane, y32 + (size_t)row * H, y16 + (size_t)row * H);
+}
+
+// One wave per (sequence, head), one query row per lane, keys in blocks of 64 staged
+// in LDS as fp32; online softmax across key blocks (T > 64).
+__global__ void __launch_bounds__(64)
+attn_full_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
+                 f16* __restrict__ ctx) {
+    __shared__ __attribute__((aligned(16))) float sK[64][64];
+    __shared__ __attribute__((aligned(16))) float sV[64][64];
+    const int s = s0 + blockIdx.x, h = blockIdx.y;
+    const int T = sm.len[s], rs = sm.row[s] - row0;
+    const int lane = threadIdx.x;
+    const int ld = 3 * H;
+    const f16* base = qkv + (size_t)rs * ld + h * 64;
+    const float scale = 0.125f;   // head_dim ** -0.5 with head_dim = 64
+
+    for (int q0 = 0; q0 < T; q0 += 64) {
+        const int t = q0 + lane;
+        const bool qv = t < T;
+        float q[64];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+            half8 v = qv ? *(const half8*)(base + (size_t)t * ld + c * 8) : (half8){};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) q[c * 8 + e] = (float)v[e];
+        }
+        float acc[64];
+#pragma unroll
+        for (int d = 0; d < 64; ++d) acc[d] = 0.f;
+        float m = -INFINITY, l = 0.f;
+
+        for (int k0 = 0; k0 < T; k0 += 64) {
+            const int nk = min(64, T - k0);
+            __syncthreads();
+#pragma unroll
+            for (int it = 0; it < 8; ++it) {
+                const int kr = it * 8 + (lane >> 3), ch = lane & 7;
+                half8 kv = {}, vv = {};
+                if (kr < nk) {
+                    kv = *(const half8*)(base + (size_t)(k0 + kr) * ld + H + ch * 8);
+                    vv = *(const half8*)(base + (size_t)(k0 + kr) * ld + 2 * H + ch * 8);
+                }
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    sK[kr][ch * 8 + e] = (float)kv[e];
+                    sV[kr][ch * 8 + e] = (float)vv[e];
+                }
+            }
+            __syncthreads();
+            float sc[64];
+            float bm = -INFINITY;
+#pragma unroll
+            for (int j = 0; j < 64; ++j) {
+                float d0 = 0.f, d1 = 0.f;
+                if (j < nk) {
+#pragma unroll
+                    for (int c = 0; c < 16; c += 2) {
+                        const float4 ka = *(const float4*)&sK[j][c * 4];
+                        const float4 kb = *(const float4*)&sK[j][c * 4 + 4];
+                        d0 += q[c * 4] * ka.x + q[c * 4 + 1] * ka.y + q[c * 4 + 2] * ka.z + q[c * 4 + 3] * ka.w;
+                        d1 += q[c * 4 + 4] * kb.x + q[c * 4 + 5] * kb.y + q[c * 4 + 6] * kb.z + q[c * 4 + 7] * kb.w;
+                    }
+                    sc[j] = (d0 + d1) * scale;
+                    bm = fmaxf(bm, sc[j]);
+                } else {
+                    sc[j] = -INFINITY;
+                }
+            }
+            const float mn = fmaxf(m, bm);
+            const float alpha = __expf(m - mn);   // m = -inf on the first block -> 0
+            l *= alpha;
+#pragma unroll
+            for (int d = 0; d < 64; ++d) acc[d] *= alpha;
+#pragma unroll
+            for (int j = 0; j < 64; ++j) {
+                if (j < nk) {
+                    const float p = __expf(sc[j] - mn);
+                    l += p;
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) {
+                        const float4 vv = *(const float4*)&sV[j][c * 4];
+                        acc[c * 4] += p * vv.x;
+                        acc[c * 4 + 1] += p * vv.y;
+                        acc[c * 4 + 2] += p * vv.z;
+                        acc[c * 4 + 3] += p * vv.w;
+                    }
+                }
+            }
+            m = mn;
+        }
+        if (qv) {
+            const float il = 1.0f / l;
+            f16* o = ctx + (size_t)(rs + t) * H + h * 64;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                half8 v;
+#pragma unroll
+                for (int e = 0; e < 8; ++e) v[e] = (f16)(acc[c * 8 + e] * il);
+                *(half8*)(o + c * 8) = v;
+            }
+        }
+    }
+}
+
+// Last layer: one wave per (sequence, head), only the scored query row.  Lanes over keys
+// for QK^T, lanes over the 64 head dims for P.V.
+__global__ void __launch_bounds__(64)
+attn_query_kernel(const f16* __restrict__ qkv, const float* __restrict__ h32, SeqMeta sm, int s0,
+                  int row0, int H, f16* __restrict__ ctxq, float* __restrict__ resq) {
+    __shared__ float sq[64];
+    __shared__ float sp[64];
+    const int s = s0 + blockIdx.x, h = blockIdx.y;
+    const int T = sm.len[s], rs = sm.row[s] - row0, qi = sm.query[s];
+    const int lane = threadIdx.x;
+    const int ld = 3 * H;
+    const f16* base = qkv + (size_t)rs * ld + h * 64;
+    sq[lane] = (float)base[(size_t)qi * ld + lane] * 0.125f;
+    __syncthreads();
+    float m = -INFINITY, l = 0.f, acc = 0.f;
+    for (int k0 = 0; k0 < T; k0 += 64) {
+        const int j = k0 + lane;
+        float sc = -INFINITY;
+        if (j < T) {
+            const f16* kr = base + (size_t)j * ld + H;
+            float d = 0.f;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const half8 kv = *(const half8*)(kr + c * 8);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) d += sq[c * 8 + e] * (float)kv[e];
+            }
+            sc = d;
+        }
+        const float mn = fmaxf(m, wave_max(sc));
+        const float p = (j < T) ? __expf(sc - mn) : 0.f;
+        const float alpha = __expf(m - mn);
+        l = l * alpha + wave_sum(p);
+        acc *= alpha;
+        __syncthreads();
+        sp[lane] = p;
+        __syncthreads();
+        const int nk = min(64, T - k0);
+        for (int jj = 0; jj < nk; ++jj)
+            acc += sp[jj] * (float)base[(size_t)(k0 + jj) * ld + 2 * H + lane];
+        m = mn;
+    }
+    const int s_loc = s - s0;
+    ctxq[(size_t)s_loc * H + h * 64 + lane] = (f16)(acc / l);
+    resq[(size_t)s_loc * H + h * 64 + lane] = h32[(size_t)(rs + qi) * H + h * 64 + lane];
+}
+
+__global__ void gather_labels_kernel(const int* __restrict__ tok, SeqMeta sm, int s0, int n,
+                                     int* __restrict__ lab) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int s = s0 + i;
+    const int l = sm.label[s];
+    lab[i] = l >= 0 ? l : tok[sm.tok_off[s] + sm.query[s]];
+}
+
+__global__ void __launch_bounds__(256)
+lse_finalize_kernel(const float2* __restrict__ part, int n_parts, const float* __restrict__ ll,
+                    int rows, float* __restrict__ out) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    const float2* p = part + (size_t)row * n_parts;
+    float mx = -INFINITY;
+    for (int k = lane; k < n_parts; k += 64)
+        if (p[k].y > 0.f) mx = fmaxf(mx, p[k].x);
+    mx = wave_max(mx);
+    float sm = 0.f;
+    for (int k = lane; k < n_parts; k += 64)
+        if (p[k].y > 0.f) sm += p[k].y * __expf(p[k].x - mx);
+    sm = wave_sum(sm);
+    if (lane == 0) out[row] = ll[row] - (mx + logf(sm));
+}
+
+__global__ void __launch_bounds__(256)
+cls_linear_kernel(const float* __restrict__ h, int rows, int H, const float* __restrict__ w,
+                  const float* __restrict__ b, float* __restrict__ out) {
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    float d = 0.f;
+    for (int c = lane; c < H; c += 64) d += h[(size_t)row * H + c] * w[c];
+    d = wave_sum(d);
+    if (lane == 0) out[row] = d + b[0];
+}
+
+__global__ void segsum_f64_kernel(const float* __restrict__ row_lp, const int* __restrict__ off,
+                                  int n, double* __restrict__ out) {
+    const int h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= n) return;
+    double acc = 0.0;
+    for (int i = off[h]; i < off[h + 1]; ++i) acc += (double)row_lp[i];
+    out[h] = acc;
+}
+
+}  // namespace
+
+hipError_t launch_embed_ln(const int* tok, SeqMeta sm, int s0, int s1, int row0, int mask_id,
+                             int vocab, const float* word, const float* pos, const float* type0,
+                             const float* g, const float* b, float eps, int H, float* h32, f16* h16,
+                             hipStream_t st) {
+    const int n = s1 - s0;
+    if (n <= 0) return hipSuccess;
+    switch (H) {
+        case 256: hipLaunchKernelGGL(embed_ln_kernel<1>, dim3(n), dim3(256), 0, st, tok, sm, s0, row0, mask_id, vocab, word, pos, type0, g, b, eps, h32, h16); break;
+        case 512: hipLaunchKernelGGL(embed_ln_kernel<2>, dim3(n), dim3(256), 0, st, tok, sm, s0, row0, mask_id, vocab, word, pos, type0, g, b, eps, h32, h16); break;
+        case 768: hipLaunchKernelGGL(embed_ln_kernel<3>, dim3(n), dim3(256), 0, st, tok, sm, s0, row0, mask_id, vocab, word, pos, type0, g, b, eps, h32, h16); break;
+        case 1024: hipLaunchKernelGGL(embed_ln_kernel<4>, dim3(n), dim3(256), 0, st, tok, sm, s0, row0, mask_id, vocab, word, pos, type0, g, b, eps, h32, h16); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_ln_rows(const float* x, int rows, const float* g, const float* b, float eps,
+                          int H, float* y32, f16* y16, hipStream_t st) {
+    if (rows <= 0) return hipSuccess;
+    const dim3 grid((rows + 3) / 4);
+    switch (H) {
+        case 256: hipLaunchKernelGGL(ln_rows_kernel<1>, grid, dim3(256), 0, st, x, rows, g, b, eps, y32, y16); break;
+        case 512: hipLaunchKernelGGL(ln_rows_kernel<2>, grid, dim3(256), 0, st, x, rows, g, b, eps, y32, y16); break;
+        case 768: hipLaunchKernelGGL(ln_rows_kernel<3>, grid, dim3(256), 0, st, x, rows, g, b, eps, y32, y16); break;
+        case 1024: hipLaunchKernelGGL(ln_rows_kernel<4>, grid, dim3(256), 0, st, x, rows, g, b, eps, y32, y16); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_attention_full(const f16* qkv, SeqMeta sm, int s0, int s1, int row0, int H,
+                                 int heads, f16* ctx, hipStream_t st) {
+    if (s1 <= s0) return hipSuccess;
+    hipLaunchKernelGGL(attn_full_kernel, dim3(s1 - s0, heads), dim3(64), 0, st, qkv, sm, s0, row0, H, ctx);
+    return hipGetLastError();
+}
+
+hipError_t launch_attention_query(const f16* qkv, const float* h32, SeqMeta sm, int s0, int s1,
+                                  int row0, int H, int heads, f16* ctxq, float* resq,
+                                  hipStream_t st) {
+    if (s1 <= s0) return hipSuccess;
+    hipLaunchKernelGGL(attn_query_kernel, dim3(s1 - s0, heads), dim3(64), 0, st, qkv, h32, sm, s0, row0, H, ctxq, resq);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_labels(const int* tok, SeqMeta sm, int s0, int s1, int* lab, hipStream_t st) {
+    const int n = s1 - s0;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_labels_kernel, dim3((n + 255) / 256), dim3(256), 0, st, tok, sm, s0, n, lab);
+    return hipGetLastError();
+}
+
+hipError_t launch_lse_finalize(const float2* part, int n_parts, const float* label_logit, int rows,
+                               float* out, hipStream_t st) {
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(lse_finalize_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, part, n_parts, label_logit, rows, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_cls_linear(const float* h, int rows, int H, const float* w, const float* b,
+                             float* out, hipStream_t st) {
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(cls_linear_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, h, rows, H, w, b, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_segsum_f64(const float* row_lp, const int* hyp_seq_off, int n_hyp, double* out,
+                             hipStream_t st) {
+    if (n_hyp <= 0) return hipSuccess;
+    hipLaunchKernelGGL(segsum_f64_kernel, dim3((n_hyp + 255) / 256), dim3(256), 0, st, row_lp, hyp_seq_off, n_hyp, out);
+    return hipGetLastError();
+}

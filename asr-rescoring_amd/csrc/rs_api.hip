@@ -1,0 +1,611 @@
+// C-ABI host side of librescore (see include/rescore.h): weight packing, ragged
+// sequence scheduling into launch chunks, and the per-chunk kernel pipeline.
+//
+// Scheduling replaces the reference's DataLoader of 32 padded rows
+// (MLM_PLL/main.py:57-70, RescoreBert/main.py:71-79): all sequences of a call are
+// flattened into ragged token rows and cut into chunks of <= max_rows rows, so every
+// GEMM launch sees tens of thousands of rows and no padding tokens.
+#include <map>
+#include <string>
+#include <vector>
+#include <cstring>
+#include <cstdio>
+
+#include "common.h"
+#include "../../include/rescore.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPTRY(expr)                                                                   \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            return fail(RS_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));   \
+    } while (0)
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    template <class T> T* as() const { return (T*)p; }
+};
+
+struct Layer {
+    f16 *wqkv, *wo, *w1, *w2;
+    float *bqkv, *bo, *b1, *b2, *g1, *be1, *g2, *be2;
+};
+
+struct Chunk {
+    int s0, s1, rows;
+};
+
+}  // namespace
+
+struct rs_model {
+    rs_bert_cfg cfg{};
+    int device = 0;
+    bool finalized = false;
+    std::map<std::string, std::vector<float>> host;   // fp32 state_dict staged until finalize
+    std::vector<void*> allocs;                          // packed weights
+    // packed weights
+    float *word32 = nullptr, *pos32 = nullptr, *type32 = nullptr, *eg = nullptr, *eb = nullptr;
+    std::vector<Layer> layers;
+    f16* wt = nullptr;  float *bt = nullptr, *gt = nullptr, *bet = nullptr;   // MLM transform
+    f16* wdec = nullptr; float* bdec = nullptr; int vpad = 0;                // tied decoder
+    float *wlin = nullptr, *blin = nullptr;                                   // RescoreBert linear
+    // workspace
+    int64_t max_rows = 0;
+    int s_cap = 0, r_pad = 0, m_pad = 0;
+    DevBuf h32, h16, t32, qkv, ctx, inter;
+    DevBuf ctxq, resq, tq32, hq32, hq16, interq, lab, llog, part, rowlp_tmp;
+    DevBuf meta, hypoff;
+    std::vector<int> pinned_dummy;
+    int* pinned = nullptr;
+    size_t pinned_cap = 0;
+    hipEvent_t upload_done = nullptr;
+    // profiling
+    bool prof = false;
+    std::vector<hipEvent_t> ev_pool;
+    size_t ev_used = 0;
+    struct Rec { int kind; hipEvent_t a, b; double flops; };
+    std::vector<Rec> recs;
+    double prof_ms[RS_K_COUNT] = {};
+    int64_t prof_n[RS_K_COUNT] = {};
+    double prof_flops[RS_K_COUNT] = {};
+};
+
+namespace {
+
+f16* upload_f16(rs_model* m, const std::vector<float>& src, size_t rows_pad, size_t cols,
+                hipError_t* err) {
+    std::vector<f16> tmp(rows_pad * cols, (f16)0.0f);
+    for (size_t i = 0; i < src.size(); ++i) tmp[i] = (f16)src[i];
+    void* p = nullptr;
+    *err = hipMalloc(&p, tmp.size() * sizeof(f16));
+    if (*err != hipSuccess) return nullptr;
+    m->allocs.push_back(p);
+    *err = hipMemcpy(p, tmp.data(), tmp.size() * sizeof(f16), hipMemcpyHostToDevice);
+    return (f16*)p;
+}
+
+float* upload_f32(rs_model* m, const std::vector<float>& src, size_t n_pad, hipError_t* err) {
+    std::vector<float> tmp(std::max(n_pad, src.size()), 0.0f);
+    std::memcpy(tmp.data(), src.data(), src.size() * sizeof(float));
+    void* p = nullptr;
+    *err = hipMalloc(&p, tmp.size() * sizeof(float));
+    if (*err != hipSuccess) return nullptr;
+    m->allocs.push_back(p);
+    *err = hipMemcpy(p, tmp.data(), tmp.size() * sizeof(float), hipMemcpyHostToDevice);
+    return (float*)p;
+}
+
+int reserve_impl(rs_model* m, int64_t max_rows) {
+    const rs_bert_cfg& c = m->cfg;
+    if (max_rows < 512) return fail(RS_EARG, "max_rows must be >= 512");
+    if (max_rows > (int64_t)1 << 26) return fail(RS_EARG, "max_rows too large");
+    const int al = gemm_row_align();
+    m->max_rows = max_rows;
+    m->m_pad = (int)((max_rows + al - 1) / al * al);
+    m->s_cap = (int)(max_rows / 3) + 1;
+    m->r_pad = (m->s_cap + al - 1) / al * al;
+    const size_t M = m->m_pad, R = m->r_pad, H = c.hidden, F = c.intermediate;
+    HIPTRY(hipSetDevice(m->device));
+    HIPTRY(m->h32.ensure(M * H * 4));
+    HIPTRY(m->h16.ensure(M * H * 2));
+    HIPTRY(m->t32.ensure(M * H * 4));
+    HIPTRY(m->qkv.ensure(M * 3 * H * 2));
+    HIPTRY(m->ctx.ensure(M * H * 2));
+    HIPTRY(m->inter.ensure(M * F * 2));
+    HIPTRY(m->ctxq.ensure(R * H * 2));
+    HIPTRY(m->resq.ensure(R * H * 4));
+    HIPTRY(m->tq32.ensure(R * H * 4));
+    HIPTRY(m->hq32.ensure(R * H * 4));
+    HIPTRY(m->hq16.ensure(R * H * 2));
+    HIPTRY(m->interq.ensure(R * F * 2));
+    HIPTRY(m->lab.ensure(R * 4));
+    HIPTRY(m->llog.ensure(R * 4));
+    if (c.heads_mask & RS_HEAD_MLM) HIPTRY(m->part.ensure(R * (size_t)(m->vpad / 64) * sizeof(float2)));
+    // zero the padded activations once: GEMMs read pad rows (never stored back)
+    HIPTRY(hipMemset(m->h16.p, 0, m->h16.bytes));
+    HIPTRY(hipMemset(m->ctx.p, 0, m->ctx.bytes));
+    HIPTRY(hipMemset(m->inter.p, 0, m->inter.bytes));
+    HIPTRY(hipMemset(m->ctxq.p, 0, m->ctxq.bytes));
+    HIPTRY(hipMemset(m->hq16.p, 0, m->hq16.bytes));
+    HIPTRY(hipMemset(m->interq.p, 0, m->interq.bytes));
+    return RS_OK;
+}
+
+const std::vector<float>* need(rs_model* m, const std::string& k, size_t n, std::string* missing) {
+    auto it = m->host.find(k);
+    if (it == m->host.end()) {
+        if (missing->empty()) *missing = k + " (missing)";
+        return nullptr;
+    }
+    if (it->second.size() != n) {
+        if (missing->empty()) *missing = k + " (wrong size)";
+        return nullptr;
+    }
+    return &it->second;
+}
+
+// ---- profiling helpers ----------------------------------------------------------------
+hipEvent_t next_event(rs_model* m) {
+    if (m->ev_used == m->ev_pool.size()) {
+        hipEvent_t e;
+        if (hipEventCreate(&e) != hipSuccess) return nullptr;
+        m->ev_pool.push_back(e);
+    }
+    return m->ev_pool[m->ev_used++];
+}
+
+struct ProfScope {
+    rs_model* m;
+    hipStream_t st;
+    int kind;
+    double flops;
+    hipEvent_t a = nullptr;
+    ProfScope(rs_model* m_, hipStream_t st_, int kind_, double flops_) : m(m_), st(st_), kind(kind_), flops(flops_) {
+        if (m->prof) {
+            a = next_event(m);
+            if (a) (void)hipEventRecord(a, st);
+        }
+    }
+    ~ProfScope() {
+        if (m->prof && a) {
+            hipEvent_t b = next_event(m);
+            if (b) {
+                (void)hipEventRecord(b, st);
+                m->recs.push_back({kind, a, b, flops});
+            }
+        }
+    }
+};
+
+int gemm(rs_model* m, hipStream_t st, int kind, int epi, const f16* A, const f16* W, int m_valid,
+         int N_pad, int K, EpiArgs ep, int n_flop_cols) {
+    const int al = gemm_row_align();
+    const int M_pad = (m_valid + al - 1) / al * al;
+    ep.m_valid = m_valid;
+    ProfScope ps(m, st, kind, 2.0 * m_valid * (double)n_flop_cols * K);
+    HIPTRY(launch_gemm(epi, A, W, M_pad, N_pad, K, ep, st));
+    return RS_OK;
+}
+
+enum Mode { MODE_MLM = 0, MODE_CLS = 1 };
+
+// Runs the encoder + head over sequences [c.s0, c.s1) (one chunk).
+int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, const Chunk& c,
+              int mode, float* d_out_rows /* indexed by sequence */) {
+    const rs_bert_cfg& cf = m->cfg;
+    const int H = cf.hidden, F = cf.intermediate, nh = cf.heads;
+    const int rows = c.rows, ns = c.s1 - c.s0;
+    float* h32 = m->h32.as<float>();
+    f16* h16 = m->h16.as<f16>();
+    float* t32 = m->t32.as<float>();
+    f16* qkv = m->qkv.as<f16>();
+    f16* ctx = m->ctx.as<f16>();
+    f16* inter = m->inter.as<f16>();
+    {
+        ProfScope ps(m, st, RS_K_OTHER, 0);
+        HIPTRY(launch_embed_ln(d_tok, sm, c.s0, c.s1, 0, cf.mask_id, cf.vocab, m->word32, m->pos32,
+                               m->type32, m->eg, m->eb, cf.ln_eps, H, h32, h16, st));
+    }
+    EpiArgs ep{};
+    for (int li = 0; li < cf.layers; ++li) {
+        const Layer& L = m->layers[li];
+        const bool last = li == cf.layers - 1;
+        ep = EpiArgs{};
+        ep.bias = L.bqkv; ep.out = qkv; ep.ldc = 3 * H;
+        if (int r = gemm(m, st, RS_K_QKV, EPI_BIAS_F16, h16, L.wqkv, rows, 3 * H, H, ep, last ? 2 * H : 3 * H)) return r;
+        if (!last) {
+            {
+                ProfScope ps(m, st, RS_K_ATTN, 0);
+                HIPTRY(launch_attention_full(qkv, sm, c.s0, c.s1, 0, H, nh, ctx, st));
+            }
+            ep = EpiArgs{}; ep.bias = L.bo; ep.res = h32; ep.out = t32; ep.ldc = H;
+            if (int r = gemm(m, st, RS_K_OPROJ, EPI_RES_F32, ctx, L.wo, rows, H, H, ep, H)) return r;
+            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(t32, rows, L.g1, L.be1, cf.ln_eps, H, h32, h16, st)); }
+            ep = EpiArgs{}; ep.bias = L.b1; ep.out = inter; ep.ldc = F;
+            if (int r = gemm(m, st, RS_K_FFN1, EPI_GELU_F16, h16, L.w1, rows, F, H, ep, F)) return r;
+            ep = EpiArgs{}; ep.bias = L.b2; ep.res = h32; ep.out = t32; ep.ldc = H;
+            if (int r = gemm(m, st, RS_K_FFN2, EPI_RES_F32, inter, L.w2, rows, H, F, ep, H)) return r;
+            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(t32, rows, L.g2, L.be2, cf.ln_eps, H, h32, h16, st)); }
+        } else {
+            // last layer: only the scored row of every sequence (one row per sequence)
+            f16* ctxq = m->ctxq.as<f16>();
+            float* resq = m->resq.as<float>();
+            float* tq = m->tq32.as<float>();
+            float* hq32 = m->hq32.as<float>();
+            f16* hq16 = m->hq16.as<f16>();
+            f16* interq = m->interq.as<f16>();
+            {
+                ProfScope ps(m, st, RS_K_ATTN, 0);
+                HIPTRY(launch_attention_query(qkv, h32, sm, c.s0, c.s1, 0, H, nh, ctxq, resq, st));
+            }
+            ep = EpiArgs{}; ep.bias = L.bo; ep.res = resq; ep.out = tq; ep.ldc = H;
+            if (int r = gemm(m, st, RS_K_OPROJ, EPI_RES_F32, ctxq, L.wo, ns, H, H, ep, H)) return r;
+            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(tq, ns, L.g1, L.be1, cf.ln_eps, H, hq32, hq16, st)); }
+            ep = EpiArgs{}; ep.bias = L.b1; ep.out = interq; ep.ldc = F;
+            if (int r = gemm(m, st, RS_K_FFN1, EPI_GELU_F16, hq16, L.w1, ns, F, H, ep, F)) return r;
+            ep = EpiArgs{}; ep.bias = L.b2; ep.res = hq32; ep.out = tq; ep.ldc = H;
+            if (int r = gemm(m, st, RS_K_FFN2, EPI_RES_F32, interq, L.w2, ns, H, F, ep, H)) return r;
+            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(tq, ns, L.g2, L.be2, cf.ln_eps, H, hq32, hq16, st)); }
+        }
+    }
+    float* hq32 = m->hq32.as<float>();
+    f16* hq16 = m->hq16.as<f16>();
+    float* tq = m->tq32.as<float>();
+    if (mode == MODE_MLM) {
+        ep = EpiArgs{}; ep.bias = m->bt; ep.out = tq; ep.ldc = H;
+        if (int r = gemm(m, st, RS_K_DECODER, EPI_GELU_F32, hq16, m->wt, ns, H, H, ep, H)) return r;
+        { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(tq, ns, m->gt, m->bet, cf.ln_eps, H, hq32, hq16, st)); }
+        int* lab = m->lab.as<int>();
+        float* ll = m->llog.as<float>();
+        { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_gather_labels(d_tok, sm, c.s0, c.s1, lab, st)); }
+        ep = EpiArgs{}; ep.bias = m->bdec; ep.n_valid = cf.vocab; ep.lse_part = m->part.as<float2>();
+        ep.n_parts = m->vpad / 64; ep.label = lab; ep.label_logit = ll;
+        if (int r = gemm(m, st, RS_K_DECODER, EPI_LSE, hq16, m->wdec, ns, m->vpad, H, ep, cf.vocab)) return r;
+        ProfScope ps(m, st, RS_K_OTHER, 0);
+        HIPTRY(launch_lse_finalize(m->part.as<float2>(), m->vpad / 64, ll, ns, d_out_rows + c.s0, st));
+    } else {
+        ProfScope ps(m, st, RS_K_OTHER, 0);
+        HIPTRY(launch_cls_linear(hq32, ns, H, m->wlin, m->blin, d_out_rows + c.s0, st));
+    }
+    return RS_OK;
+}
+
+// Host-side sequence list (structure of arrays) for one call.
+struct SeqList {
+    std::vector<int> tok_off, len, mask, query, label, row;
+    void push(int to, int T, int mp, int q, int lb) {
+        tok_off.push_back(to); len.push_back(T); mask.push_back(mp); query.push_back(q);
+        label.push_back(lb); row.push_back(0);
+    }
+    size_t size() const { return len.size(); }
+};
+
+// Chunks the sequence list, uploads metadata, runs every chunk.  out_rows: one float per
+// sequence.  Extra int arrays (e.g. hypothesis -> sequence offsets) ride in the same upload.
+int run_all(rs_model* m, hipStream_t st, const int* d_tok, SeqList& sl, int mode, float* out_rows,
+            const std::vector<int>* extra, int** d_extra, const int* d_label = nullptr) {
+    if (!m->finalized) return fail(RS_ESTATE, "rs_model_finalize not called");
+    if (mode == MODE_MLM && !(m->cfg.heads_mask & RS_HEAD_MLM)) return fail(RS_ESTATE, "model has no MLM head");
+    if (mode == MODE_CLS && !(m->cfg.heads_mask & RS_HEAD_CLS)) return fail(RS_ESTATE, "model has no CLS linear head");
+    if (m->max_rows == 0)
+        if (int r = reserve_impl(m, 65536)) return r;
+    HIPTRY(hipSetDevice(m->device));
+    const size_t S = sl.size();
+    std::vector<Chunk> chunks;
+    int rows = 0, s0 = 0;
+    for (size_t s = 0; s < S; ++s) {
+        const int T = sl.len[s];
+        if (T > m->cfg.max_pos) return fail(RS_EUNSUP, "sequence longer than max_position_embeddings");
+        if (T < 1) return fail(RS_EARG, "empty sequence");
+        if (T > m->max_rows) return fail(RS_EARG, "sequence longer than the reserved rows");
+        if (rows + T > m->max_rows || (int)s - s0 >= m->s_cap) {
+            chunks.push_back({s0, (int)s, rows});
+            s0 = (int)s;
+            rows = 0;
+        }
+        sl.row[s] = rows;
+        rows += T;
+    }
+    if (S) chunks.push_back({s0, (int)S, rows});
+
+    // one upload of all metadata through a pinned staging buffer
+    const size_t n_extra = extra ? extra->size() : 0;
+    const size_t n_int = 6 * S + n_extra;
+    if (m->upload_done) HIPTRY(hipEventSynchronize(m->upload_done));
+    if (n_int > m->pinned_cap) {
+        if (m->pinned) (void)hipHostFree(m->pinned);
+        m->pinned = nullptr;
+        m->pinned_cap = 0;
+        HIPTRY(hipHostMalloc((void**)&m->pinned, std::max<size_t>(n_int, 1) * 4, hipHostMallocDefault));
+        m->pinned_cap = n_int;
+    }
+    int* p = m->pinned;
+    const std::vector<int>* cols[6] = {&sl.tok_off, &sl.len, &sl.mask, &sl.query, &sl.label, &sl.row};
+    for (int k = 0; k < 6; ++k) std::memcpy(p + k * S, cols[k]->data(), S * 4);
+    if (n_extra) std::memcpy(p + 6 * S, extra->data(), n_extra * 4);
+    HIPTRY(m->meta.ensure(std::max<size_t>(n_int, 1) * 4));
+    HIPTRY(hipMemcpyAsync(m->meta.p, p, n_int * 4, hipMemcpyHostToDevice, st));
+    if (!m->upload_done) HIPTRY(hipEventCreateWithFlags(&m->upload_done, hipEventDisableTiming));
+    HIPTRY(hipEventRecord(m->upload_done, st));
+    int* d = m->meta.as<int>();
+    if (d_label) HIPTRY(hipMemcpyAsync(d + 4 * S, d_label, S * 4, hipMemcpyDeviceToDevice, st));
+    SeqMeta sm{d, d + S, d + 2 * S, d + 3 * S, d + 4 * S, d + 5 * S};
+    if (d_extra) *d_extra = d + 6 * S;
+    for (const Chunk& c : chunks)
+        if (int r = run_chunk(m, st, d_tok, sm, c, mode, out_rows)) return r;
+    return RS_OK;
+}
+
+void prof_collect(rs_model* m) {
+    if (m->recs.empty()) return;
+    (void)hipEventSynchronize(m->recs.back().b);
+    for (auto& r : m->recs) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, r.a, r.b) == hipSuccess) {
+            m->prof_ms[r.kind] += ms;
+            m->prof_n[r.kind] += 1;
+            m->prof_flops[r.kind] += r.flops;
+        }
+    }
+    m->recs.clear();
+    m->ev_used = 0;
+}
+
+}  // namespace
+
+// =======================================================================================
+extern "C" {
+
+int rs_version(void) { return 1; }
+
+const char* rs_last_error(void) { return g_err.c_str(); }
+
+int rs_model_create(const rs_bert_cfg* cfg, int device, rs_model** out) {
+    if (!cfg || !out) return fail(RS_EARG, "null argument");
+    const rs_bert_cfg& c = *cfg;
+    if (c.hidden <= 0 || c.hidden % 256 || c.hidden > 1024) return fail(RS_EUNSUP, "hidden must be 256/512/768/1024");
+    if (c.heads <= 0 || c.hidden / c.heads != 64 || c.hidden % c.heads) return fail(RS_EUNSUP, "head_dim must be 64");
+    if (c.intermediate <= 0 || c.intermediate % 128) return fail(RS_EUNSUP, "intermediate must be a multiple of 128");
+    if (c.layers < 1 || c.vocab < 1 || c.max_pos < 3 || c.type_vocab < 1) return fail(RS_EARG, "bad config");
+    if (!(c.heads_mask & (RS_HEAD_MLM | RS_HEAD_CLS))) return fail(RS_EARG, "heads_mask selects no head");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
+        return fail(RS_EHIP, "no such HIP device");
+    rs_model* m = new (std::nothrow) rs_model();
+    if (!m) return fail(RS_ENOMEM, "alloc");
+    m->cfg = c;
+    m->device = device;
+    *out = m;
+    return RS_OK;
+}
+
+int rs_model_set_tensor(rs_model* m, const char* key, const void* host_ptr, int dtype,
+                        const int64_t* shape, int ndim) {
+    if (!m || !key || !host_ptr || (ndim > 0 && !shape)) return fail(RS_EARG, "null argument");
+    if (dtype != RS_DT_F32) return fail(RS_EUNSUP, "only float32 tensors are accepted");
+    if (m->finalized) return fail(RS_ESTATE, "model already finalized");
+    int64_t n = 1;
+    for (int i = 0; i < ndim; ++i) {
+        if (shape[i] < 0) return fail(RS_EARG, "negative dim");
+        n *= shape[i];
+    }
+    std::vector<float> v((size_t)n);
+    std::memcpy(v.data(), host_ptr, (size_t)n * 4);
+    m->host[key] = std::move(v);
+    return RS_OK;
+}
+
+int rs_model_finalize(rs_model* m) {
+    if (!m) return fail(RS_EARG, "null model");
+    if (m->finalized) return RS_OK;
+    HIPTRY(hipSetDevice(m->device));
+    const rs_bert_cfg& c = m->cfg;
+    const size_t H = c.hidden, F = c.intermediate, V = c.vocab;
+    std::string miss;
+    const std::string e = "bert.embeddings.";
+    auto* word = need(m, e + "word_embeddings.weight", V * H, &miss);
+    auto* pos = need(m, e + "position_embeddings.weight", (size_t)c.max_pos * H, &miss);
+    auto* typ = need(m, e + "token_type_embeddings.weight", (size_t)c.type_vocab * H, &miss);
+    auto* eg = need(m, e + "LayerNorm.weight", H, &miss);
+    auto* eb = need(m, e + "LayerNorm.bias", H, &miss);
+    if (!miss.empty()) return fail(RS_ESTATE, "tensor " + miss);
+    hipError_t err = hipSuccess;
+#define UP32(dst, src, n) do { dst = upload_f32(m, *(src), (n), &err); if (err != hipSuccess) return fail(RS_EHIP, "upload"); } while (0)
+#define UP16(dst, src, rp, cols) do { dst = upload_f16(m, *(src), (rp), (cols), &err); if (err != hipSuccess) return fail(RS_EHIP, "upload"); } while (0)
+    UP32(m->word32, word, V * H);
+    UP32(m->pos32, pos, (size_t)c.max_pos * H);
+    UP32(m->type32, typ, H);     // token_type_ids are all 0 (modeling_bert.py:88-94)
+    UP32(m->eg, eg, H);
+    UP32(m->eb, eb, H);
+    m->layers.resize(c.layers);
+    for (int i = 0; i < c.layers; ++i) {
+        const std::string p = "bert.encoder.layer." + std::to_string(i) + ".";
+        auto* wq = need(m, p + "attention.self.query.weight", H * H, &miss);
+        auto* bq = need(m, p + "attention.self.query.bias", H, &miss);
+        auto* wk = need(m, p + "attention.self.key.weight", H * H, &miss);
+        auto* bk = need(m, p + "attention.self.key.bias", H, &miss);
+        auto* wv = need(m, p + "attention.self.value.weight", H * H, &miss);
+        auto* bv = need(m, p + "attention.self.value.bias", H, &miss);
+        auto* wo = need(m, p + "attention.output.dense.weight", H * H, &miss);
+        auto* bo = need(m, p + "attention.output.dense.bias", H, &miss);
+        auto* g1 = need(m, p + "attention.output.LayerNorm.weight", H, &miss);
+        auto* be1 = need(m, p + "attention.output.LayerNorm.bias", H, &miss);
+        auto* w1 = need(m, p + "intermediate.dense.weight", F * H, &miss);
+        auto* b1 = need(m, p + "intermediate.dense.bias", F, &miss);
+        auto* w2 = need(m, p + "output.dense.weight", H * F, &miss);
+        auto* b2 = need(m, p + "output.dense.bias", H, &miss);
+        auto* g2 = need(m, p + "output.LayerNorm.weight", H, &miss);
+        auto* be2 = need(m, p + "output.LayerNorm.bias", H, &miss);
+        if (!miss.empty()) return fail(RS_ESTATE, "tensor " + miss);
+        std::vector<float> wqkv, bqkv;
+        wqkv.reserve(3 * H * H);
+        for (auto* w : {wq, wk, wv}) wqkv.insert(wqkv.end(), w->begin(), w->end());
+        for (auto* b : {bq, bk, bv}) bqkv.insert(bqkv.end(), b->begin(), b->end());
+        Layer& L = m->layers[i];
+        UP16(L.wqkv, &wqkv, 3 * H, H);
+        UP32(L.bqkv, &bqkv, 3 * H);
+        UP16(L.wo, wo, H, H);
+        UP32(L.bo, bo, H);
+        UP32(L.g1, g1, H);
+        UP32(L.be1, be1, H);
+        UP16(L.w1, w1, F, H);
+        UP32(L.b1, b1, F);
+        UP16(L.w2, w2, H, F);
+        UP32(L.b2, b2, H);
+        UP32(L.g2, g2, H);
+        UP32(L.be2, be2, H);
+    }
+    if (c.heads_mask & RS_HEAD_MLM) {
+        const std::string p = "cls.predictions.";
+        auto* wt = need(m, p + "transform.dense.weight", H * H, &miss);
+        auto* bt = need(m, p + "transform.dense.bias", H, &miss);
+        auto* gt = need(m, p + "transform.LayerNorm.weight", H, &miss);
+        auto* bet = need(m, p + "transform.LayerNorm.bias", H, &miss);
+        auto* bd = need(m, p + "bias", V, &miss);
+        if (!miss.empty()) return fail(RS_ESTATE, "tensor " + miss);
+        // decoder weight is tied to the word embeddings (BertForMaskedLM._tied_weights_keys);
+        // an explicitly provided cls.predictions.decoder.weight must equal it.
+        auto it = m->host.find(p + "decoder.weight");
+        const std::vector<float>* dec = word;
+        if (it != m->host.end()) {
+            if (it->second.size() != V * H) return fail(RS_EARG, "decoder.weight has wrong size");
+            dec = &it->second;
+        }
+        m->vpad = (int)((V + 127) / 128 * 128);
+        UP16(m->wt, wt, H, H);
+        UP32(m->bt, bt, H);
+        UP32(m->gt, gt, H);
+        UP32(m->bet, bet, H);
+        UP16(m->wdec, dec, (size_t)m->vpad, H);
+        UP32(m->bdec, bd, (size_t)m->vpad);
+    }
+    if (c.heads_mask & RS_HEAD_CLS) {
+        auto* wl = need(m, "linear.weight", H, &miss);
+        auto* bl = need(m, "linear.bias", 1, &miss);
+        if (!miss.empty()) return fail(RS_ESTATE, "tensor " + miss);
+        UP32(m->wlin, wl, H);
+        UP32(m->blin, bl, 1);
+    }
+#undef UP32
+#undef UP16
+    m->host.clear();
+    m->finalized = true;
+    return RS_OK;
+}
+
+int rs_model_reserve(rs_model* m, int64_t max_rows) {
+    if (!m) return fail(RS_EARG, "null model");
+    if (!m->finalized) return fail(RS_ESTATE, "rs_model_finalize not called");
+    return reserve_impl(m, max_rows);
+}
+
+int rs_pll_score(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, int32_t n_hyp,
+                 double* d_pll, float* d_row_lp, void* stream) {
+    if (!m || !h_hyp_off || n_hyp < 0 || (n_hyp > 0 && (!d_tok || !d_pll))) return fail(RS_EARG, "null argument");
+    hipStream_t st = (hipStream_t)stream;
+    SeqList sl;
+    std::vector<int> hso(n_hyp + 1, 0);
+    for (int h = 0; h < n_hyp; ++h) {
+        const int o = h_hyp_off[h], T = h_hyp_off[h + 1] - o;
+        if (T < 3) return fail(RS_EARG, "hypothesis " + std::to_string(h) + " has no word (T < 3)");
+        for (int p = 1; p <= T - 2; ++p) sl.push(o, T, p, p, -1);   // do_job rows, p = mask_pos
+        hso[h + 1] = (int)sl.size();
+    }
+    if (n_hyp == 0) return RS_OK;
+    float* rows = d_row_lp;
+    if (!rows) {
+        HIPTRY(m->rowlp_tmp.ensure(sl.size() * 4));
+        rows = m->rowlp_tmp.as<float>();
+    }
+    int* d_hso = nullptr;
+    if (int r = run_all(m, st, d_tok, sl, MODE_MLM, rows, &hso, &d_hso)) return r;
+    ProfScope ps(m, st, RS_K_OTHER, 0);
+    HIPTRY(launch_segsum_f64(rows, d_hso, n_hyp, d_pll, st));
+    return RS_OK;
+}
+
+int rs_masked_logprob(rs_model* m, const int32_t* d_ids, const int32_t* h_seq_off,
+                      const int32_t* h_query, const int32_t* d_label, int32_t n_seq, float* d_out,
+                      void* stream) {
+    if (!m || !h_seq_off || !h_query || n_seq < 0 || (n_seq > 0 && (!d_ids || !d_label || !d_out)))
+        return fail(RS_EARG, "null argument");
+    if (n_seq == 0) return RS_OK;
+    SeqList sl;
+    for (int s = 0; s < n_seq; ++s) {
+        const int o = h_seq_off[s], T = h_seq_off[s + 1] - o;
+        if (h_query[s] < 0 || h_query[s] >= T) return fail(RS_EARG, "query position outside its sequence");
+        sl.push(o, T, -1, h_query[s], 0);   // ids already masked by the caller
+    }
+    return run_all(m, (hipStream_t)stream, d_ids, sl, MODE_MLM, d_out, nullptr, nullptr, d_label);
+}
+
+int rs_cls_score(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, int32_t n_hyp,
+                 float* d_out, void* stream) {
+    if (!m || !h_hyp_off || n_hyp < 0 || (n_hyp > 0 && (!d_tok || !d_out))) return fail(RS_EARG, "null argument");
+    if (n_hyp == 0) return RS_OK;
+    SeqList sl;
+    for (int h = 0; h < n_hyp; ++h) {
+        const int o = h_hyp_off[h], T = h_hyp_off[h + 1] - o;
+        if (T < 1) return fail(RS_EARG, "empty hypothesis");
+        sl.push(o, T, -1, 0, 0);      // query = [CLS] (RescoreBert/model.py:19)
+    }
+    return run_all(m, (hipStream_t)stream, d_tok, sl, MODE_CLS, d_out, nullptr, nullptr);
+}
+
+int rs_profile_enable(rs_model* m, int on) {
+    if (!m) return fail(RS_EARG, "null model");
+    prof_collect(m);
+    m->prof = on != 0;
+    for (int k = 0; k < RS_K_COUNT; ++k) m->prof_ms[k] = 0, m->prof_n[k] = 0, m->prof_flops[k] = 0;
+    return RS_OK;
+}
+
+int rs_profile_read(rs_model* m, int kind, double* ms, int64_t* launches, double* flops) {
+    if (!m || kind < 0 || kind >= RS_K_COUNT) return fail(RS_EARG, "bad argument");
+    prof_collect(m);
+    if (ms) *ms = m->prof_ms[kind];
+    if (launches) *launches = m->prof_n[kind];
+    if (flops) *flops = m->prof_flops[kind];
+    return RS_OK;
+}
+
+void rs_model_destroy(rs_model* m) {
+    if (!m) return;
+    (void)hipSetDevice(m->device);
+    (void)hipDeviceSynchronize();
+    for (void* p : m->allocs) (void)hipFree(p);
+    for (DevBuf* b : {&m->h32, &m->h16, &m->t32, &m->qkv, &m->ctx, &m->inter, &m->ctxq, &m->resq,
+                      &m->tq32, &m->hq32, &m->hq16, &m->interq, &m->lab, &m->llog, &m->part,
+                      &m->rowlp_tmp, &m->meta, &m->hypoff})
+        b->release();
+    if (m->pinned) (void)hipHostFree(m->pinned);
+    if (m->upload_done) (void)hipEventDestroy(m->upload_done);
+    for (hipEvent_t e : m->ev_pool) (void)hipEventDestroy(e);
+    delete m;
+}
+
+}  // extern "C"

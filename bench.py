@@ -1,0 +1,179 @@
+"""Benchmark: MLM_PLL masked-token BERT-base forwards/s on MI355X (BASELINE.json metric).
+
+One step = one full scoring pass of the hot path over the step's synthetic N-best input
+(configs[2]: MLM_PLL full PLL, bert-base, N=50, mean L~32, U utterances per rank):
+  tokens resident in HBM -> on-device mask expansion -> 12-layer encoder -> fused
+  decoder/log-softmax gather -> fp64 PLL per hypothesis -> RCCL all_gather of
+  (am, lm) -> rank 0 fusion over the 101-weight grid + corpus-CER numerators.
+Every rank scores its own U utterances (weak scaling; utterances are independent).
+
+Prints ONE JSON line on rank 0.  Extra legs (not in the timed region): a HIP-event
+per-kernel-kind profile pass (roofline of the dominant kernel) and a bounded CPU
+baseline (the oracle's PyTorch-CPU restatement of the reference work pattern).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+import __graft_entry__  # noqa: E402
+
+__graft_entry__._import_pkg()
+from asr_rescoring_amd import data as D  # noqa: E402
+from asr_rescoring_amd import rerank  # noqa: E402
+from asr_rescoring_amd.weights import BERT_BASE, make_weights  # noqa: E402
+
+PEAK_FP16_TFLOPS = 2500.0   # MI355X dense FP16/BF16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0
+
+
+def forward_flops(T: int, s=BERT_BASE) -> float:
+    """Canonical algorithmic FLOPs of one MLM_PLL masked forward at length T."""
+    H, F, V, nl = s.hidden, s.intermediate, s.vocab, s.layers
+    dense = 2 * (4 * H * H + 2 * H * F)
+    return float((nl - 1) * (T * dense + 4 * T * T * H) + 4 * T * H * H
+                 + (2 * H * H + 4 * T * H + 2 * H * H + 4 * H * F) + 2 * (H * H + H * V))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--utts", type=int, default=200, help="utterances per rank per step (C3: 200)")
+    ap.add_argument("--nbest", type=int, default=50)
+    ap.add_argument("--max-rows", type=int, default=131072)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline budget (0 = skip)")
+    ap.add_argument("--no-profile", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from asr_rescoring_amd.scorer import PLLScorer
+    weights = make_weights(BERT_BASE, seed=1234)
+    scorer = PLLScorer(weights, BERT_BASE, device=local, max_rows=args.max_rows)
+
+    nb = D.synthetic_nbest(args.utts, args.nbest, seed=1 + 1000 * rank)
+    d_tok = torch.from_numpy(nb.tokens).to(dev)                 # resident in HBM
+    am_d = torch.from_numpy(nb.am).to(dev)
+    n_fwd = nb.n_forwards()
+    lens = np.diff(nb.hyp_off)
+    flops_step = float(sum(forward_flops(int(T)) * (int(T) - 2) for T in lens))
+    grid = rerank.weight_grid("norm")
+    hyp_len = nb.hyp_len()
+    # gathered buffers (fixed shapes: every rank has U*N hypotheses)
+    H = nb.n_hyp
+
+    def step():
+        lm = scorer.score_nbest(d_tok, nb.hyp_off)               # float64 [H]
+        pair = torch.stack([am_d, lm])                           # (am, lm) [2, H]
+        if world > 1:
+            out = torch.empty(world, 2, H, dtype=torch.float64, device=dev)
+            dist.all_gather_into_tensor(out, pair)
+        else:
+            out = pair[None]
+        if rank == 0:
+            am_all = out[:, 0].reshape(-1)
+            lm_all = out[:, 1].reshape(-1)
+            uo = np.arange(world * args.utts + 1, dtype=np.int32) * args.nbest
+            rerank.fuse_rerank(am_all, lm_all, np.tile(hyp_len, world), uo, grid, "norm", args.nbest, local)
+        return lm
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        lm = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    total_fwd = n_fwd * world * args.steps
+    value = total_fwd / dt
+
+    # ---- profile leg: per-kernel-kind HIP-event timing (separate, untimed pass) ----------
+    roof = None
+    kinds = {}
+    if not args.no_profile:
+        scorer.profile(True)
+        scorer.score_nbest(d_tok, nb.hyp_off)
+        torch.cuda.synchronize()
+        kinds = scorer.profile_read()
+        scorer.profile(False)
+        gemm_kinds = {k: v for k, v in kinds.items() if v[2] > 0}
+        dom = max(gemm_kinds, key=lambda k: gemm_kinds[k][0])
+        ms, n, fl = gemm_kinds[dom]
+        achieved = fl / (ms * 1e-3) / 1e12
+        roof = {"kernel": f"gemm_f16_{dom}", "bound": "mfma", "achieved": round(achieved, 2),
+                "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP16_TFLOPS, 4),
+                "traffic": None, "launches": n, "avg_launch_ms": round(ms / max(n, 1), 4),
+                "flops_per_launch": fl / max(n, 1)}
+
+    # ---- CPU baseline: oracle restatement of the reference work pattern ------------------
+    cpu = None
+    if rank == 0 and args.cpu_seconds > 0:
+        from oracle.bert_ref import TorchBert, set_cpu_threads, pll_rows
+        import oracle.bert_ref as OB
+        threads = set_cpu_threads()
+        model = TorchBert(weights, BERT_BASE)
+        rows_done, t_cpu = 0, 0.0
+        h = 0
+        while t_cpu < args.cpu_seconds and h < nb.n_hyp:
+            sub_off = nb.hyp_off[h:h + 2] - nb.hyp_off[h]
+            toks = nb.tokens[nb.hyp_off[h]:nb.hyp_off[h + 1]]
+            t1 = time.perf_counter()
+            OB.pll_reference_pattern(model, toks, sub_off, batch_size=32, full_head=True)
+            t_cpu += time.perf_counter() - t1
+            rows_done += int(sub_off[-1]) - 2
+            h += 1
+        cpu = {"value": round(rows_done / t_cpu, 2), "unit": "masked fwd/s", "cores": threads,
+               "kind": "port", "sample": f"{h} hypotheses ({rows_done} masked forwards) of rank-0 step "
+               f"input, reference work pattern (batch 32 padded rows, all-position logits + CE, "
+               f"fp64 accumulation), torch {torch.__version__} CPU"}
+        _ = pll_rows
+
+    if rank == 0:
+        mean_T = float(np.average(lens, weights=lens - 2))
+        rec = {"metric": "masked-token BERT forwards/sec (MLM_PLL, N=50, L~32)", "value": round(value, 2),
+               "unit": "masked fwd/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": "fp16-mfma/fp32-acc", "data": "synthetic (PCG64 seed 1; random-init bert-base weights seed 1234)",
+               "config": {"workload": "C3 MLM_PLL full PLL", "model": "bert-base-chinese shape (12L/768/12H/3072/V21128)",
+                          "utts_per_rank": args.utts, "n_best": args.nbest, "forwards_per_rank_step": n_fwd,
+                          "mean_T": round(mean_T, 2), "parallelism": f"dp{world} (utterance shards + RCCL all_gather)"},
+               "achieved_tflops_canonical": round(flops_step * world * args.steps / dt / 1e12, 2),
+               "roofline": roof, "cpu_baseline": cpu,
+               "kinds_ms": {k: round(v[0], 3) for k, v in kinds.items()}}
+        print(json.dumps(rec))
+    scorer.close()
+    del lm
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,160 @@
+/*
+ * librescore — C ABI of the MI355X-native N-best LM rescorer (gfx950 HIP kernels).
+ *
+ * The reference (ishine/ASR-Rescoring) is pure Python with no FFI; its seams on the hot
+ * path are Python calls.  Each entry point below names the reference interface it
+ * replaces (file:line, relative to the reference repo).  The Python host mirror in
+ * asr-rescoring_amd/ binds these with ctypes (see INTEGRATION.md for the binding a
+ * maintainer would add to the reference).
+ *
+ * Conventions
+ *   - d_* pointers are device memory owned by the caller (e.g. the PyTorch caching
+ *     allocator); h_* pointers are host memory read during the call only.
+ *   - stream is a hipStream_t (torch.cuda.current_stream().cuda_stream); every call is
+ *     asynchronous on it unless stated.  No C++ exception crosses the ABI.
+ *   - return 0 on success, a negative RS_E* code on failure; rs_last_error() gives a
+ *     thread-local message.
+ *   - A model handle is bound to one device and must not be used by two host threads
+ *     at once.  Results are deterministic (no float atomics, fixed reduction orders).
+ */
+#ifndef RESCORE_H_
+#define RESCORE_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RS_OK 0
+#define RS_EARG (-1)      /* bad argument / shape */
+#define RS_EHIP (-2)      /* HIP runtime error */
+#define RS_ESTATE (-3)    /* call order (e.g. scoring before rs_model_finalize) */
+#define RS_ENOMEM (-4)
+#define RS_EUNSUP (-5)    /* shape outside what the kernels support */
+
+#define RS_DT_F32 0
+
+#define RS_HEAD_MLM 1     /* BertForMaskedLM head: cls.predictions.* (MLM_PLL) */
+#define RS_HEAD_CLS 2     /* RescoreBert head: linear.weight [1,H], linear.bias [1] */
+
+#define RS_FUSE_NORM 0    /* (1-w)*am/len + w*lm/len      rescore.py:51 */
+#define RS_FUSE_LEGACY 1  /* (1-w)*am + w*lm              rescore_result/MLM_PLL/rescore.log:28 */
+#define RS_FUSE_AM_NORM 2 /* (1-w)*am/len + w*lm          rescore_result/RMBR/BertScore/rescore_mbr_normalize.log:29 */
+
+typedef struct rs_model rs_model;
+
+/* transformers.BertConfig fields used by the reference (bert-base-chinese:
+ * 21128/768/12/12/3072/512/2, eps 1e-12, [MASK] = 103). */
+typedef struct rs_bert_cfg {
+    int32_t vocab, hidden, layers, heads, intermediate, max_pos, type_vocab;
+    float ln_eps;
+    int32_t mask_id;
+    int32_t heads_mask;   /* RS_HEAD_MLM | RS_HEAD_CLS */
+} rs_bert_cfg;
+
+int rs_version(void);
+const char* rs_last_error(void);
+
+/* Replaces BertForMaskedLM.from_pretrained / RescoreBert(...) construction
+ * (MLM_PLL/main.py:184, RescoreBert/model.py:5-11).  Requires hidden % 256 == 0,
+ * head_dim == 64, intermediate % 128 == 0. */
+int rs_model_create(const rs_bert_cfg* cfg, int device, rs_model** out);
+
+/* Replaces model.load_state_dict(torch.load(checkpoint)) (MLM_PLL/main.py:185-186,
+ * RescoreBert/main.py:250-251): one HF state_dict tensor by key, host fp32. */
+int rs_model_set_tensor(rs_model* m, const char* hf_key, const void* host_ptr, int dtype,
+                        const int64_t* shape, int ndim);
+
+/* Packs the tensors into the kernel layouts (fp16 GEMM weights, fused QKV) on device.
+ * Fails with RS_ESTATE naming the first missing key. */
+int rs_model_finalize(rs_model* m);
+
+/* Sizes the activation workspace for up to max_rows token rows per launch chunk
+ * (>= 512).  Optional: scoring calls reserve a default on first use. */
+int rs_model_reserve(rs_model* m, int64_t max_rows);
+
+/* MLM_PLL scoring (MLM_PLL/preprocess.py:9-30 + MLM_PLL/main.py:83-107):
+ *   d_tok      int32 [h_hyp_off[n_hyp]]  hypotheses as [CLS] w_1..w_L [SEP]
+ *   h_hyp_off  int32 [n_hyp + 1]         host offsets into d_tok (T_h = L_h + 2 >= 3)
+ *   d_pll      float64 [n_hyp]           sum_p log p(w_p | w_{\p}) accumulated in row
+ *                                        order p = 1..L (== output_score[u][h])
+ *   d_row_lp   float32 [sum_h L_h] or NULL: per masked row log-prob (== token_score)
+ * The L masked copies are expanded on device. */
+int rs_pll_score(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, int32_t n_hyp,
+                 double* d_pll, float* d_row_lp, void* stream);
+
+/* Row-level MLM drop-in (MLM_PLL/main.py:89-105 for an arbitrary batch):
+ *   d_ids      int32 ragged sequences (already masked), h_seq_off int32 [n_seq+1] host
+ *   h_query    int32 [n_seq] host   position of the masked token in each sequence
+ *   d_label    int32 [n_seq]        label id at that position
+ *   d_out      float32 [n_seq]      log_softmax(logits[query])[label] */
+int rs_masked_logprob(rs_model* m, const int32_t* d_ids, const int32_t* h_seq_off,
+                      const int32_t* h_query, const int32_t* d_label, int32_t n_seq,
+                      float* d_out, void* stream);
+
+/* RescoreBert scoring (RescoreBert/model.py:13-21, RescoreBert/main.py:156-158):
+ * CLS hidden of the last layer -> Linear(H, 1).  d_out float32 [n_hyp]. */
+int rs_cls_score(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, int32_t n_hyp,
+                 float* d_out, void* stream);
+
+/* Per-kernel-kind device timing (HIP events around every launch of that kind, on the
+ * call's stream).  Enable before a scoring call; read after it (synchronises).
+ * kind: RS_K_QKV, RS_K_OPROJ, RS_K_FFN1, RS_K_FFN2, RS_K_DECODER, RS_K_ATTN, RS_K_OTHER.
+ * flops = algorithmic FLOPs of the launches of that kind (2*M*N*K over valid rows). */
+#define RS_K_QKV 0
+#define RS_K_OPROJ 1
+#define RS_K_FFN1 2
+#define RS_K_FFN2 3
+#define RS_K_DECODER 4
+#define RS_K_ATTN 5
+#define RS_K_OTHER 6
+#define RS_K_COUNT 7
+int rs_profile_enable(rs_model* m, int on);
+int rs_profile_read(rs_model* m, int kind, double* ms, int64_t* launches, double* flops);
+
+void rs_model_destroy(rs_model* m);
+
+/* RMBR CER utility (RMBR/utility_functions.py:28-33 via RMBR/mbr.py:5-28): the
+ * pairwise Levenshtein matrix of every utterance's hypotheses, computed once.
+ *   d_chars   int32 symbols, d_str_off int32 [n_str+1], d_utt_off int32 [n_utt+1]
+ *             (strings of utterance u = utt_off[u]..utt_off[u+1])
+ *   d_mat_off int64 [n_utt+1] offsets of each n_u x n_u block in d_ed (row-major)
+ *   d_ed      int32 out: d_ed[mat_off[u] + i*n_u + j] = ed(string_i, string_j)
+ * Strings up to 64 symbols use a Myers/Hyyro bit-parallel kernel; longer ones a DP. */
+int rs_pairwise_edit(const int32_t* d_chars, const int32_t* d_str_off, const int32_t* d_utt_off,
+                     const int64_t* d_mat_off, int32_t n_utt, int32_t max_n, int32_t* d_ed,
+                     void* stream);
+
+/* RMBR mbr_decode scores for top-k (RMBR/mbr.py:17-22):
+ *   score[u][i] = float32 torch-CPU-order sum over j != i (j < k) of
+ *                 float32(1 - ed(hyp_j, hyp_i) / len(hyp_j));  argmax[u] = first max.
+ * d_len int32 [n_str]; d_scores float32 [n_utt * k]; d_argmax int32 [n_utt]. */
+int rs_mbr_scores(const int32_t* d_ed, const int64_t* d_mat_off, const int32_t* d_utt_off,
+                  const int32_t* d_len, int32_t n_utt, int32_t k, float* d_scores,
+                  int32_t* d_argmax, void* stream);
+
+/* Fusion + argmax over a weight grid (rescore.py:37-58), fp64 with the reference's
+ * operation order, no contraction.  Utterance u has hypotheses utt_off[u]..utt_off[u+1]
+ * (first n_best of them used).  d_argmax int32 [n_w * n_utt] (first max). */
+int rs_fuse_rerank(const double* d_am, const double* d_lm, const int32_t* d_len,
+                   const int32_t* d_utt_off, int32_t n_utt, int32_t n_best, const double* d_w,
+                   int32_t n_w, int32_t mode, int32_t* d_argmax, void* stream);
+
+/* Corpus-CER numerators for every weight (jiwer.cer at rescore.py:40): edits[w] =
+ * sum_u ed_ref[utt_off[u] + argmax[w][u]] over d_ed_ref int32 [n_hyp] (edit distance of
+ * each hypothesis to its reference).  d_edits int64 [n_w]. */
+int rs_corpus_edits(const int32_t* d_ed_ref, const int32_t* d_utt_off, const int32_t* d_argmax,
+                    int32_t n_utt, int32_t n_w, int64_t* d_edits, void* stream);
+
+/* Edit distance of every hypothesis to its utterance's reference (the per-hypothesis
+ * table behind jiwer.cer's numerator): d_ref_chars/d_ref_off int32 [n_utt+1] are the
+ * references, hypotheses as in rs_pairwise_edit.  d_ed_ref int32 [n_hyp]. */
+int rs_ref_edit(const int32_t* d_chars, const int32_t* d_str_off, const int32_t* d_utt_off,
+                const int32_t* d_ref_chars, const int32_t* d_ref_off, int32_t n_utt,
+                int32_t* d_ed_ref, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RESCORE_H_ */

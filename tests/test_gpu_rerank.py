@@ -1,0 +1,77 @@
+"""GPU parity of the rerank kernels (bit-exact: integer edits, fp64 fusion argmax)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from asr_rescoring_amd import data as D
+
+pytestmark = pytest.mark.gpu
+
+
+def test_ref_and_pairwise_edit_vs_oracle():
+    from asr_rescoring_amd import rerank
+    from oracle import rescore_ref as R
+    nb = D.synthetic_nbest(7, 9, seed=2, vocab=140, len_lo=1, len_hi=90, max_edits=6)
+    ed = rerank.ref_edits(nb).cpu().numpy()
+    for u in range(nb.n_utt):
+        for h in range(nb.utt_off[u], nb.utt_off[u + 1]):
+            assert ed[h] == R.levenshtein(nb.refs[u], nb.hyp_words(h))
+    mat, moff = rerank.pairwise_edit(nb)
+    mat = mat.cpu().numpy()
+    for u in range(nb.n_utt):
+        n = nb.utt_off[u + 1] - nb.utt_off[u]
+        M = mat[moff[u]:moff[u + 1]].reshape(n, n)
+        for i in range(n):
+            for j in range(n):
+                assert M[i, j] == R.levenshtein(nb.hyp_words(nb.utt_off[u] + i), nb.hyp_words(nb.utt_off[u] + j))
+
+
+def test_mbr_golden(golden_dir):
+    from asr_rescoring_amd import rerank
+    g = np.load(os.path.join(golden_dir, "rmbr.npz"), allow_pickle=False)
+    nb = D.NBest(g["tokens"], g["hyp_off"], g["utt_off"], np.zeros(len(g["hyp_off"]) - 1),
+                 [np.zeros(1, np.int32)] * (len(g["utt_off"]) - 1), [], [])
+    ed, moff = rerank.pairwise_edit(nb)
+    for k in range(2, 13):
+        am, sc = rerank.mbr_scores(nb, k, ed, moff)
+        assert np.array_equal(am, g[f"argmax_k{k}"])
+        assert np.array_equal(sc, g[f"scores_k{k}"])        # bit-exact float32
+
+
+def test_fuse_rerank_vs_oracle_random():
+    from asr_rescoring_amd import rerank
+    from oracle import rescore_ref as R
+    rng = np.random.default_rng(5)
+    U, N = 300, 10
+    am = -np.abs(rng.normal(5.8, 4, size=(U, N)))
+    lm = -np.abs(rng.normal(150, 30, size=(U, N)))
+    lens = rng.integers(3, 30, size=(U, N))
+    # exact ties in am to exercise first-index argmax
+    am[:20, 1] = am[:20, 0]
+    lm[:20, 1] = lm[:20, 0]
+    lens[:20, 1] = lens[:20, 0]
+    uo = np.arange(U + 1) * N
+    for mode in R.MODES:
+        grid = R.weight_grid(mode)
+        got = rerank.fuse_rerank(am.reshape(-1), lm.reshape(-1), lens.reshape(-1), uo, grid, mode).cpu().numpy()
+        for wi, w in enumerate(grid):
+            ref = np.argmax(R.fuse(w, lens, am, lm, mode), axis=-1)
+            assert np.array_equal(got[wi], ref), (mode, w)
+
+
+def test_c1_plumbing_fusion(golden_dir):
+    """C1 fixture: reference rescore.find_best_weight outputs (argmax per weight, CER, best w)."""
+    from asr_rescoring_amd import rerank
+    g = json.load(open(os.path.join(golden_dir, "c1_plumbing.json"), encoding="utf-8"))
+    tok = D.CharTokenizer(list(g["charset"]))
+    uids = g["utt_ids"]
+    words = [[tok.encode_words(t) for t in g["hyps_text"][u].values()] for u in uids]
+    am = [list(g["hyps_score"][u].values()) for u in uids]
+    nb = D.from_lists(words, am, [tok.encode_words(g["ref_text"][u]) for u in uids], uids)
+    lm = np.asarray([v for u in uids for v in g["lm"][u].values()], np.float64)
+    best_w, best_cer, arg, cers = rerank.find_best_weight(nb, lm, n_best=10)
+    assert np.array_equal(arg, np.asarray(g["argmax_per_weight"]))
+    assert np.allclose(cers, g["cer_per_weight"], rtol=0, atol=1e-15)
+    assert best_w == g["best_weight"] and best_cer == g["best_cer"]
