@@ -26,7 +26,10 @@ class RsBertCfg(ctypes.Structure):
                 ("heads", ctypes.c_int32), ("intermediate", ctypes.c_int32),
                 ("max_pos", ctypes.c_int32), ("type_vocab", ctypes.c_int32),
                 ("ln_eps", ctypes.c_float), ("mask_id", ctypes.c_int32),
-                ("heads_mask", ctypes.c_int32)]
+                ("heads_mask", ctypes.c_int32), ("precision", ctypes.c_int32)]
+
+
+RS_PREC = {"fp16": 0, "fp16x3": 1}
 
 
 class RescoreError(RuntimeError):

@@ -18,6 +18,7 @@ enum EpiKind {
     EPI_GELU_F32 = 2,   // out32 = gelu(acc + bias)                (MLM transform, pre-LN)
     EPI_RES_F32 = 3,    // out32 = acc + bias + res32              (BertSelfOutput / BertOutput, pre-LN)
     EPI_LSE = 4,        // per-row partial (max, sum exp) over a 64-column slab + label logit
+    EPI_BIAS_F32 = 5,   // out32 = acc + bias                      (QKV in the fp16x3 precision mode)
 };
 
 struct EpiArgs {
@@ -31,7 +32,33 @@ struct EpiArgs {
     int n_parts;
     const int* label;      // [M] label column per row (EPI_LSE)
     float* label_logit;    // [M]
+    int kx;                // fp16 operand image width factor of the output (EPI_GELU_F16): 1 or 3
+    int nlog;              // logical N (column offset of the image sections)
 };
+
+// fp16 operand image of an fp32 activation row with logical width K:
+//   kx == 1: [hi]                  (RS_PREC_FP16)
+//   kx == 3: [hi | hi | lo]        (RS_PREC_FP16X3, lo = fp16(x - hi))
+// paired with the weight image [W_hi | W_lo | W_hi] the K-concatenated MFMA product is
+// A_hi.W_hi + A_hi.W_lo + A_lo.W_hi: fp32-level accuracy from fp16 MFMA in one accumulator.
+__device__ __forceinline__ void put_split(f16* row, int c, int K, int kx, float v) {
+    const f16 hi = (f16)v;
+    row[c] = hi;
+    if (kx == 3) {
+        row[K + c] = hi;
+        row[2 * K + c] = (f16)(v - (float)hi);
+    }
+}
+__device__ __forceinline__ void put_split4(f16* row, int c, int K, int kx, float4 v) {
+    const half4 hi = {(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
+    *(half4*)(row + c) = hi;
+    if (kx == 3) {
+        *(half4*)(row + K + c) = hi;
+        const half4 lo = {(f16)(v.x - (float)hi[0]), (f16)(v.y - (float)hi[1]),
+                          (f16)(v.z - (float)hi[2]), (f16)(v.w - (float)hi[3])};
+        *(half4*)(row + 2 * K + c) = lo;
+    }
+}
 
 // Per-sequence metadata of a scoring call (structure of arrays, device).  A "sequence"
 // is one BERT input: a masked copy of a hypothesis (MLM_PLL), a hypothesis
@@ -66,16 +93,18 @@ hipError_t launch_gemm(int epi, const f16* A, const f16* W, int M_pad, int N_pad
                        const EpiArgs& ep, hipStream_t st);
 int gemm_row_align();   // M padding granularity required by launch_gemm
 
+// kx: width factor of the fp16 operand images written (1 or 3, see put_split);
+// qkv32: the QKV projection is fp32 (fp16x3 mode) instead of fp16.
 hipError_t launch_embed_ln(const int* tok, SeqMeta sm, int s0, int s1, int row0, int mask_id,
                            int vocab, const float* word, const float* pos, const float* type0,
                            const float* g, const float* b, float eps, int H, float* h32, f16* h16,
-                           hipStream_t st);
+                           int kx, hipStream_t st);
 hipError_t launch_ln_rows(const float* x, int rows, const float* g, const float* b, float eps,
-                          int H, float* y32, f16* y16, hipStream_t st);
-hipError_t launch_attention_full(const f16* qkv, SeqMeta sm, int s0, int s1, int row0, int H,
-                                 int heads, f16* ctx, hipStream_t st);
-hipError_t launch_attention_query(const f16* qkv, const float* h32, SeqMeta sm, int s0, int s1,
-                                  int row0, int H, int heads, f16* ctxq, float* resq,
+                          int H, float* y32, f16* y16, int kx, hipStream_t st);
+hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0, int s1, int row0,
+                                 int H, int heads, f16* ctx, int kx, hipStream_t st);
+hipError_t launch_attention_query(const void* qkv, bool qkv32, const float* h32, SeqMeta sm, int s0,
+                                  int s1, int row0, int H, int heads, f16* ctxq, float* resq, int kx,
                                   hipStream_t st);
 hipError_t launch_gather_labels(const int* tok, SeqMeta sm, int s0, int s1, int* lab,
                                 hipStream_t st);

@@ -12,13 +12,16 @@
 //                  (MLM_PLL/main.py:101-105)
 //  cls_linear      RescoreBert Linear(H, 1) on the CLS state (RescoreBert/model.py:19-20)
 //  segsum_f64      per-hypothesis PLL, float64, in row order (MLM_PLL/main.py:106-107)
+//
+// Every producer of a GEMM operand writes the fp16 operand image (put_split: [hi] or
+// [hi | hi | lo]) next to the fp32 value the residual path keeps.
 #include "common.h"
 
 namespace {
 
 template <int NV>
 __device__ __forceinline__ void ln_store(float4 (&x)[NV], const float* g, const float* b, float eps,
-                                         int lane, float* y32, f16* y16) {
+                                         int lane, float* y32, f16* y16, int kx) {
     constexpr int H = NV * 256;
     float s = 0.f;
 #pragma unroll
@@ -42,8 +45,7 @@ __device__ __forceinline__ void ln_store(float4 (&x)[NV], const float* g, const 
         y.z = x[v].z * inv * gg.z + bb.z;
         y.w = x[v].w * inv * gg.w + bb.w;
         *(float4*)(y32 + c) = y;
-        half4 h = {(f16)y.x, (f16)y.y, (f16)y.z, (f16)y.w};
-        *(half4*)(y16 + c) = h;
+        put_split4(y16, c, H, kx, y);
     }
 }
 
@@ -53,7 +55,7 @@ embed_ln_kernel(const int* __restrict__ tok, SeqMeta sm, int s0, int row0, int m
                 const float* __restrict__ word, const float* __restrict__ pos,
                 const float* __restrict__ type0, const float* __restrict__ g,
                 const float* __restrict__ b, float eps, float* __restrict__ h32,
-                f16* __restrict__ h16) {
+                f16* __restrict__ h16, int kx) {
     constexpr int H = NV * 256;
     const int s = s0 + blockIdx.x;
     const int T = sm.len[s], toff = sm.tok_off[s], mp = sm.mask_pos[s];
@@ -72,15 +74,16 @@ embed_ln_kernel(const int* __restrict__ tok, SeqMeta sm, int s0, int row0, int m
             // transformers order: (inputs_embeds + token_type) + position
             x[v] = make_float4((w.x + ty.x) + p.x, (w.y + ty.y) + p.y, (w.z + ty.z) + p.z, (w.w + ty.w) + p.w);
         }
-        const size_t o = (size_t)(rs + t) * H;
-        ln_store<NV>(x, g, b, eps, lane, h32 + o, h16 + o);
+        const size_t r = (size_t)(rs + t);
+        ln_store<NV>(x, g, b, eps, lane, h32 + r * H, h16 + r * kx * H, kx);
     }
 }
 
 template <int NV>
 __global__ void __launch_bounds__(256)
 ln_rows_kernel(const float* __restrict__ xin, int rows, const float* __restrict__ g,
-               const float* __restrict__ b, float eps, float* __restrict__ y32, f16* __restrict__ y16) {
+               const float* __restrict__ b, float eps, float* __restrict__ y32, f16* __restrict__ y16,
+               int kx) {
     constexpr int H = NV * 256;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -88,21 +91,32 @@ ln_rows_kernel(const float* __restrict__ xin, int rows, const float* __restrict_
     float4 x[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) x[v] = *(const float4*)(xin + (size_t)row * H + v * 256 + lane * 4);
-    ln_store<NV>(x, g, b, eps, lane, y32 + (size_t)row * H, y16 + (size_t)row * H);
+    ln_store<NV>(x, g, b, eps, lane, y32 + (size_t)row * H, y16 + (size_t)row * kx * H, kx);
+}
+
+__device__ __forceinline__ void load8(const f16* p, float (&o)[8]) {
+    const half8 v = *(const half8*)p;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (float)v[e];
+}
+__device__ __forceinline__ void load8(const float* p, float (&o)[8]) {
+    const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+    o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w; o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
 }
 
 // One wave per (sequence, head), one query row per lane, keys in blocks of 64 staged
 // in LDS as fp32; online softmax across key blocks (T > 64).
+template <class QT>
 __global__ void __launch_bounds__(64)
-attn_full_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
-                 f16* __restrict__ ctx) {
+attn_full_kernel(const QT* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
+                 f16* __restrict__ ctx, int kx) {
     __shared__ __attribute__((aligned(16))) float sK[64][64];
     __shared__ __attribute__((aligned(16))) float sV[64][64];
     const int s = s0 + blockIdx.x, h = blockIdx.y;
     const int T = sm.len[s], rs = sm.row[s] - row0;
     const int lane = threadIdx.x;
     const int ld = 3 * H;
-    const f16* base = qkv + (size_t)rs * ld + h * 64;
+    const QT* base = qkv + (size_t)rs * ld + h * 64;
     const float scale = 0.125f;   // head_dim ** -0.5 with head_dim = 64
 
     for (int q0 = 0; q0 < T; q0 += 64) {
@@ -111,9 +125,10 @@ attn_full_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int 
         float q[64];
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-            half8 v = qv ? *(const half8*)(base + (size_t)t * ld + c * 8) : (half8){};
+            float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+            if (qv) load8(base + (size_t)t * ld + c * 8, v);
 #pragma unroll
-            for (int e = 0; e < 8; ++e) q[c * 8 + e] = (float)v[e];
+            for (int e = 0; e < 8; ++e) q[c * 8 + e] = v[e];
         }
         float acc[64];
 #pragma unroll
@@ -126,16 +141,16 @@ attn_full_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int 
 #pragma unroll
             for (int it = 0; it < 8; ++it) {
                 const int kr = it * 8 + (lane >> 3), ch = lane & 7;
-                half8 kv = {}, vv = {};
+                float kv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+                float vv[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
                 if (kr < nk) {
-                    kv = *(const half8*)(base + (size_t)(k0 + kr) * ld + H + ch * 8);
-                    vv = *(const half8*)(base + (size_t)(k0 + kr) * ld + 2 * H + ch * 8);
+                    load8(base + (size_t)(k0 + kr) * ld + H + ch * 8, kv);
+                    load8(base + (size_t)(k0 + kr) * ld + 2 * H + ch * 8, vv);
                 }
-#pragma unroll
-                for (int e = 0; e < 8; ++e) {
-                    sK[kr][ch * 8 + e] = (float)kv[e];
-                    sV[kr][ch * 8 + e] = (float)vv[e];
-                }
+                *(float4*)&sK[kr][ch * 8] = make_float4(kv[0], kv[1], kv[2], kv[3]);
+                *(float4*)&sK[kr][ch * 8 + 4] = make_float4(kv[4], kv[5], kv[6], kv[7]);
+                *(float4*)&sV[kr][ch * 8] = make_float4(vv[0], vv[1], vv[2], vv[3]);
+                *(float4*)&sV[kr][ch * 8 + 4] = make_float4(vv[4], vv[5], vv[6], vv[7]);
             }
             __syncthreads();
             float sc[64];
@@ -181,30 +196,28 @@ attn_full_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int 
         }
         if (qv) {
             const float il = 1.0f / l;
-            f16* o = ctx + (size_t)(rs + t) * H + h * 64;
+            f16* o = ctx + (size_t)(rs + t) * kx * H;
 #pragma unroll
-            for (int c = 0; c < 8; ++c) {
-                half8 v;
-#pragma unroll
-                for (int e = 0; e < 8; ++e) v[e] = (f16)(acc[c * 8 + e] * il);
-                *(half8*)(o + c * 8) = v;
-            }
+            for (int c = 0; c < 16; ++c)
+                put_split4(o, h * 64 + c * 4, H, kx,
+                           make_float4(acc[c * 4] * il, acc[c * 4 + 1] * il, acc[c * 4 + 2] * il, acc[c * 4 + 3] * il));
         }
     }
 }
 
 // Last layer: one wave per (sequence, head), only the scored query row.  Lanes over keys
 // for QK^T, lanes over the 64 head dims for P.V.
+template <class QT>
 __global__ void __launch_bounds__(64)
-attn_query_kernel(const f16* __restrict__ qkv, const float* __restrict__ h32, SeqMeta sm, int s0,
-                  int row0, int H, f16* __restrict__ ctxq, float* __restrict__ resq) {
+attn_query_kernel(const QT* __restrict__ qkv, const float* __restrict__ h32, SeqMeta sm, int s0,
+                  int row0, int H, f16* __restrict__ ctxq, float* __restrict__ resq, int kx) {
     __shared__ float sq[64];
     __shared__ float sp[64];
     const int s = s0 + blockIdx.x, h = blockIdx.y;
     const int T = sm.len[s], rs = sm.row[s] - row0, qi = sm.query[s];
     const int lane = threadIdx.x;
     const int ld = 3 * H;
-    const f16* base = qkv + (size_t)rs * ld + h * 64;
+    const QT* base = qkv + (size_t)rs * ld + h * 64;
     sq[lane] = (float)base[(size_t)qi * ld + lane] * 0.125f;
     __syncthreads();
     float m = -INFINITY, l = 0.f, acc = 0.f;
@@ -212,13 +225,14 @@ attn_query_kernel(const f16* __restrict__ qkv, const float* __restrict__ h32, Se
         const int j = k0 + lane;
         float sc = -INFINITY;
         if (j < T) {
-            const f16* kr = base + (size_t)j * ld + H;
+            const QT* kr = base + (size_t)j * ld + H;
             float d = 0.f;
 #pragma unroll
             for (int c = 0; c < 8; ++c) {
-                const half8 kv = *(const half8*)(kr + c * 8);
+                float kv[8];
+                load8(kr + c * 8, kv);
 #pragma unroll
-                for (int e = 0; e < 8; ++e) d += sq[c * 8 + e] * (float)kv[e];
+                for (int e = 0; e < 8; ++e) d += sq[c * 8 + e] * kv[e];
             }
             sc = d;
         }
@@ -236,7 +250,7 @@ attn_query_kernel(const f16* __restrict__ qkv, const float* __restrict__ h32, Se
         m = mn;
     }
     const int s_loc = s - s0;
-    ctxq[(size_t)s_loc * H + h * 64 + lane] = (f16)(acc / l);
+    put_split(ctxq + (size_t)s_loc * kx * H, h * 64 + lane, H, kx, acc / l);
     resq[(size_t)s_loc * H + h * 64 + lane] = h32[(size_t)(rs + qi) * H + h * 64 + lane];
 }
 
@@ -291,47 +305,59 @@ __global__ void segsum_f64_kernel(const float* __restrict__ row_lp, const int* _
 }  // namespace
 
 hipError_t launch_embed_ln(const int* tok, SeqMeta sm, int s0, int s1, int row0, int mask_id,
-                             int vocab, const float* word, const float* pos, const float* type0,
-                             const float* g, const float* b, float eps, int H, float* h32, f16* h16,
-                             hipStream_t st) {
+                           int vocab, const float* word, const float* pos, const float* type0,
+                           const float* g, const float* b, float eps, int H, float* h32, f16* h16,
+                           int kx, hipStream_t st) {
     const int n = s1 - s0;
     if (n <= 0) return hipSuccess;
+#define RS_EMB(NV) hipLaunchKernelGGL(embed_ln_kernel<NV>, dim3(n), dim3(256), 0, st, tok, sm, s0, row0, mask_id, vocab, word, pos, type0, g, b, eps, h32, h16, kx)
     switch (H) {
-        case 256: hipLaunchKernelGGL(embed_ln_kernel<1>, dim3(n), dim3(256), 0, st, tok, sm, s0, row0, mask_id, vocab, word, pos, type0, g, b, eps, h32, h16); break;
-        case 512: hipLaunchKernelGGL(embed_ln_kernel<2>, dim3(n), dim3(256), 0, st, tok, sm, s0, row0, mask_id, vocab, word, pos, type0, g, b, eps, h32, h16); break;
-        case 768: hipLaunchKernelGGL(embed_ln_kernel<3>, dim3(n), dim3(256), 0, st, tok, sm, s0, row0, mask_id, vocab, word, pos, type0, g, b, eps, h32, h16); break;
-        case 1024: hipLaunchKernelGGL(embed_ln_kernel<4>, dim3(n), dim3(256), 0, st, tok, sm, s0, row0, mask_id, vocab, word, pos, type0, g, b, eps, h32, h16); break;
+        case 256: RS_EMB(1); break;
+        case 512: RS_EMB(2); break;
+        case 768: RS_EMB(3); break;
+        case 1024: RS_EMB(4); break;
         default: return hipErrorInvalidValue;
     }
+#undef RS_EMB
     return hipGetLastError();
 }
 
 hipError_t launch_ln_rows(const float* x, int rows, const float* g, const float* b, float eps,
-                          int H, float* y32, f16* y16, hipStream_t st) {
+                          int H, float* y32, f16* y16, int kx, hipStream_t st) {
     if (rows <= 0) return hipSuccess;
     const dim3 grid((rows + 3) / 4);
+#define RS_LN(NV) hipLaunchKernelGGL(ln_rows_kernel<NV>, grid, dim3(256), 0, st, x, rows, g, b, eps, y32, y16, kx)
     switch (H) {
-        case 256: hipLaunchKernelGGL(ln_rows_kernel<1>, grid, dim3(256), 0, st, x, rows, g, b, eps, y32, y16); break;
-        case 512: hipLaunchKernelGGL(ln_rows_kernel<2>, grid, dim3(256), 0, st, x, rows, g, b, eps, y32, y16); break;
-        case 768: hipLaunchKernelGGL(ln_rows_kernel<3>, grid, dim3(256), 0, st, x, rows, g, b, eps, y32, y16); break;
-        case 1024: hipLaunchKernelGGL(ln_rows_kernel<4>, grid, dim3(256), 0, st, x, rows, g, b, eps, y32, y16); break;
+        case 256: RS_LN(1); break;
+        case 512: RS_LN(2); break;
+        case 768: RS_LN(3); break;
+        case 1024: RS_LN(4); break;
         default: return hipErrorInvalidValue;
     }
+#undef RS_LN
     return hipGetLastError();
 }
 
-hipError_t launch_attention_full(const f16* qkv, SeqMeta sm, int s0, int s1, int row0, int H,
-                                 int heads, f16* ctx, hipStream_t st) {
+hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0, int s1, int row0,
+                                 int H, int heads, f16* ctx, int kx, hipStream_t st) {
     if (s1 <= s0) return hipSuccess;
-    hipLaunchKernelGGL(attn_full_kernel, dim3(s1 - s0, heads), dim3(64), 0, st, qkv, sm, s0, row0, H, ctx);
+    const dim3 grid(s1 - s0, heads);
+    if (qkv32)
+        hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
+    else
+        hipLaunchKernelGGL(attn_full_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
     return hipGetLastError();
 }
 
-hipError_t launch_attention_query(const f16* qkv, const float* h32, SeqMeta sm, int s0, int s1,
-                                  int row0, int H, int heads, f16* ctxq, float* resq,
+hipError_t launch_attention_query(const void* qkv, bool qkv32, const float* h32, SeqMeta sm, int s0,
+                                  int s1, int row0, int H, int heads, f16* ctxq, float* resq, int kx,
                                   hipStream_t st) {
     if (s1 <= s0) return hipSuccess;
-    hipLaunchKernelGGL(attn_query_kernel, dim3(s1 - s0, heads), dim3(64), 0, st, qkv, h32, sm, s0, row0, H, ctxq, resq);
+    const dim3 grid(s1 - s0, heads);
+    if (qkv32)
+        hipLaunchKernelGGL(attn_query_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, h32, sm, s0, row0, H, ctxq, resq, kx);
+    else
+        hipLaunchKernelGGL(attn_query_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, h32, sm, s0, row0, H, ctxq, resq, kx);
     return hipGetLastError();
 }
 

@@ -164,8 +164,10 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                     const size_t o = (size_t)row * ep.ldc + col;
                     if constexpr (EPI == EPI_BIAS_F16) {
                         ((f16*)ep.out)[o] = (f16)x;
+                    } else if constexpr (EPI == EPI_BIAS_F32) {
+                        ((float*)ep.out)[o] = x;
                     } else if constexpr (EPI == EPI_GELU_F16) {
-                        ((f16*)ep.out)[o] = (f16)gelu_erf(x);
+                        put_split((f16*)ep.out + (size_t)row * ep.ldc, col, ep.nlog, ep.kx, gelu_erf(x));
                     } else if constexpr (EPI == EPI_GELU_F32) {
                         ((float*)ep.out)[o] = gelu_erf(x);
                     } else {  // EPI_RES_F32
@@ -208,6 +210,7 @@ hipError_t launch_gemm(int epi, const f16* A, const f16* W, int M_pad, int N_pad
         case EPI_GELU_F32: return launch_t<128, 128, 2, 2, EPI_GELU_F32>(A, W, M_pad, N_pad, K, ep, st);
         case EPI_RES_F32: return launch_t<128, 128, 2, 2, EPI_RES_F32>(A, W, M_pad, N_pad, K, ep, st);
         case EPI_LSE: return launch_t<128, 128, 2, 2, EPI_LSE>(A, W, M_pad, N_pad, K, ep, st);
+        case EPI_BIAS_F32: return launch_t<128, 128, 2, 2, EPI_BIAS_F32>(A, W, M_pad, N_pad, K, ep, st);
     }
     return hipErrorInvalidValue;
 }

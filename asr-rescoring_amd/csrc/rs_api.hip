@@ -76,6 +76,7 @@ struct rs_model {
     // workspace
     int64_t max_rows = 0;
     int s_cap = 0, r_pad = 0, m_pad = 0;
+    int kx = 1;                 // fp16 operand image width (1: fp16, 3: fp16x3)
     DevBuf h32, h16, t32, qkv, ctx, inter;
     DevBuf ctxq, resq, tq32, hq32, hq16, interq, lab, llog, part, rowlp_tmp;
     DevBuf meta, hypoff;
@@ -96,10 +97,23 @@ struct rs_model {
 
 namespace {
 
-f16* upload_f16(rs_model* m, const std::vector<float>& src, size_t rows_pad, size_t cols,
+// Weight W [rows, cols] (nn.Linear [out, in]) -> fp16 operand image [rows_pad, kx*cols]:
+// kx == 1: [hi]; kx == 3: [hi | lo | hi] (pairs with the activation image [hi | hi | lo]).
+f16* upload_f16(rs_model* m, const std::vector<float>& src, size_t rows_pad, size_t cols, int kx,
                 hipError_t* err) {
-    std::vector<f16> tmp(rows_pad * cols, (f16)0.0f);
-    for (size_t i = 0; i < src.size(); ++i) tmp[i] = (f16)src[i];
+    std::vector<f16> tmp(rows_pad * cols * kx, (f16)0.0f);
+    const size_t rows = src.size() / cols;
+    for (size_t r = 0; r < rows; ++r)
+        for (size_t c = 0; c < cols; ++c) {
+            const float v = src[r * cols + c];
+            const f16 hi = (f16)v;
+            f16* row = tmp.data() + r * cols * kx;
+            row[c] = hi;
+            if (kx == 3) {
+                row[cols + c] = (f16)(v - (float)hi);
+                row[2 * cols + c] = hi;
+            }
+        }
     void* p = nullptr;
     *err = hipMalloc(&p, tmp.size() * sizeof(f16));
     if (*err != hipSuccess) return nullptr;
@@ -130,18 +144,19 @@ int reserve_impl(rs_model* m, int64_t max_rows) {
     m->r_pad = (m->s_cap + al - 1) / al * al;
     const size_t M = m->m_pad, R = m->r_pad, H = c.hidden, F = c.intermediate;
     HIPTRY(hipSetDevice(m->device));
+    const size_t kx = m->kx;
     HIPTRY(m->h32.ensure(M * H * 4));
-    HIPTRY(m->h16.ensure(M * H * 2));
+    HIPTRY(m->h16.ensure(M * H * 2 * kx));
     HIPTRY(m->t32.ensure(M * H * 4));
-    HIPTRY(m->qkv.ensure(M * 3 * H * 2));
-    HIPTRY(m->ctx.ensure(M * H * 2));
-    HIPTRY(m->inter.ensure(M * F * 2));
-    HIPTRY(m->ctxq.ensure(R * H * 2));
+    HIPTRY(m->qkv.ensure(M * 3 * H * (kx == 3 ? 4 : 2)));
+    HIPTRY(m->ctx.ensure(M * H * 2 * kx));
+    HIPTRY(m->inter.ensure(M * F * 2 * kx));
+    HIPTRY(m->ctxq.ensure(R * H * 2 * kx));
     HIPTRY(m->resq.ensure(R * H * 4));
     HIPTRY(m->tq32.ensure(R * H * 4));
     HIPTRY(m->hq32.ensure(R * H * 4));
-    HIPTRY(m->hq16.ensure(R * H * 2));
-    HIPTRY(m->interq.ensure(R * F * 2));
+    HIPTRY(m->hq16.ensure(R * H * 2 * kx));
+    HIPTRY(m->interq.ensure(R * F * 2 * kx));
     HIPTRY(m->lab.ensure(R * 4));
     HIPTRY(m->llog.ensure(R * 4));
     if (c.heads_mask & RS_HEAD_MLM) HIPTRY(m->part.ensure(R * (size_t)(m->vpad / 64) * sizeof(float2)));
@@ -217,39 +232,46 @@ enum Mode { MODE_MLM = 0, MODE_CLS = 1 };
 int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, const Chunk& c,
               int mode, float* d_out_rows /* indexed by sequence */) {
     const rs_bert_cfg& cf = m->cfg;
-    const int H = cf.hidden, F = cf.intermediate, nh = cf.heads;
+    const int H = cf.hidden, F = cf.intermediate, nh = cf.heads, kx = m->kx;
+    const bool q32 = kx == 3;                 // fp16x3: QKV kept in fp32 for attention
+    const int qkv_epi = q32 ? EPI_BIAS_F32 : EPI_BIAS_F16;
     const int rows = c.rows, ns = c.s1 - c.s0;
     float* h32 = m->h32.as<float>();
     f16* h16 = m->h16.as<f16>();
     float* t32 = m->t32.as<float>();
-    f16* qkv = m->qkv.as<f16>();
+    void* qkv = m->qkv.p;
     f16* ctx = m->ctx.as<f16>();
     f16* inter = m->inter.as<f16>();
     {
         ProfScope ps(m, st, RS_K_OTHER, 0);
         HIPTRY(launch_embed_ln(d_tok, sm, c.s0, c.s1, 0, cf.mask_id, cf.vocab, m->word32, m->pos32,
-                               m->type32, m->eg, m->eb, cf.ln_eps, H, h32, h16, st));
+                               m->type32, m->eg, m->eb, cf.ln_eps, H, h32, h16, kx, st));
     }
     EpiArgs ep{};
+    auto gelu_ep = [&](const float* bias, f16* out) {
+        EpiArgs e{};
+        e.bias = bias; e.out = out; e.ldc = kx * F; e.kx = kx; e.nlog = F;
+        return e;
+    };
     for (int li = 0; li < cf.layers; ++li) {
         const Layer& L = m->layers[li];
         const bool last = li == cf.layers - 1;
         ep = EpiArgs{};
         ep.bias = L.bqkv; ep.out = qkv; ep.ldc = 3 * H;
-        if (int r = gemm(m, st, RS_K_QKV, EPI_BIAS_F16, h16, L.wqkv, rows, 3 * H, H, ep, last ? 2 * H : 3 * H)) return r;
+        if (int r = gemm(m, st, RS_K_QKV, qkv_epi, h16, L.wqkv, rows, 3 * H, kx * H, ep, last ? 2 * H : 3 * H)) return r;
         if (!last) {
             {
                 ProfScope ps(m, st, RS_K_ATTN, 0);
-                HIPTRY(launch_attention_full(qkv, sm, c.s0, c.s1, 0, H, nh, ctx, st));
+                HIPTRY(launch_attention_full(qkv, q32, sm, c.s0, c.s1, 0, H, nh, ctx, kx, st));
             }
             ep = EpiArgs{}; ep.bias = L.bo; ep.res = h32; ep.out = t32; ep.ldc = H;
-            if (int r = gemm(m, st, RS_K_OPROJ, EPI_RES_F32, ctx, L.wo, rows, H, H, ep, H)) return r;
-            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(t32, rows, L.g1, L.be1, cf.ln_eps, H, h32, h16, st)); }
-            ep = EpiArgs{}; ep.bias = L.b1; ep.out = inter; ep.ldc = F;
-            if (int r = gemm(m, st, RS_K_FFN1, EPI_GELU_F16, h16, L.w1, rows, F, H, ep, F)) return r;
+            if (int r = gemm(m, st, RS_K_OPROJ, EPI_RES_F32, ctx, L.wo, rows, H, kx * H, ep, H)) return r;
+            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(t32, rows, L.g1, L.be1, cf.ln_eps, H, h32, h16, kx, st)); }
+            ep = gelu_ep(L.b1, inter);
+            if (int r = gemm(m, st, RS_K_FFN1, EPI_GELU_F16, h16, L.w1, rows, F, kx * H, ep, F)) return r;
             ep = EpiArgs{}; ep.bias = L.b2; ep.res = h32; ep.out = t32; ep.ldc = H;
-            if (int r = gemm(m, st, RS_K_FFN2, EPI_RES_F32, inter, L.w2, rows, H, F, ep, H)) return r;
-            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(t32, rows, L.g2, L.be2, cf.ln_eps, H, h32, h16, st)); }
+            if (int r = gemm(m, st, RS_K_FFN2, EPI_RES_F32, inter, L.w2, rows, H, kx * F, ep, H)) return r;
+            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(t32, rows, L.g2, L.be2, cf.ln_eps, H, h32, h16, kx, st)); }
         } else {
             // last layer: only the scored row of every sequence (one row per sequence)
             f16* ctxq = m->ctxq.as<f16>();
@@ -260,16 +282,16 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
             f16* interq = m->interq.as<f16>();
             {
                 ProfScope ps(m, st, RS_K_ATTN, 0);
-                HIPTRY(launch_attention_query(qkv, h32, sm, c.s0, c.s1, 0, H, nh, ctxq, resq, st));
+                HIPTRY(launch_attention_query(qkv, q32, h32, sm, c.s0, c.s1, 0, H, nh, ctxq, resq, kx, st));
             }
             ep = EpiArgs{}; ep.bias = L.bo; ep.res = resq; ep.out = tq; ep.ldc = H;
-            if (int r = gemm(m, st, RS_K_OPROJ, EPI_RES_F32, ctxq, L.wo, ns, H, H, ep, H)) return r;
-            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(tq, ns, L.g1, L.be1, cf.ln_eps, H, hq32, hq16, st)); }
-            ep = EpiArgs{}; ep.bias = L.b1; ep.out = interq; ep.ldc = F;
-            if (int r = gemm(m, st, RS_K_FFN1, EPI_GELU_F16, hq16, L.w1, ns, F, H, ep, F)) return r;
+            if (int r = gemm(m, st, RS_K_OPROJ, EPI_RES_F32, ctxq, L.wo, ns, H, kx * H, ep, H)) return r;
+            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(tq, ns, L.g1, L.be1, cf.ln_eps, H, hq32, hq16, kx, st)); }
+            ep = gelu_ep(L.b1, interq);
+            if (int r = gemm(m, st, RS_K_FFN1, EPI_GELU_F16, hq16, L.w1, ns, F, kx * H, ep, F)) return r;
             ep = EpiArgs{}; ep.bias = L.b2; ep.res = hq32; ep.out = tq; ep.ldc = H;
-            if (int r = gemm(m, st, RS_K_FFN2, EPI_RES_F32, interq, L.w2, ns, H, F, ep, H)) return r;
-            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(tq, ns, L.g2, L.be2, cf.ln_eps, H, hq32, hq16, st)); }
+            if (int r = gemm(m, st, RS_K_FFN2, EPI_RES_F32, interq, L.w2, ns, H, kx * F, ep, H)) return r;
+            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(tq, ns, L.g2, L.be2, cf.ln_eps, H, hq32, hq16, kx, st)); }
         }
     }
     float* hq32 = m->hq32.as<float>();
@@ -277,14 +299,14 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
     float* tq = m->tq32.as<float>();
     if (mode == MODE_MLM) {
         ep = EpiArgs{}; ep.bias = m->bt; ep.out = tq; ep.ldc = H;
-        if (int r = gemm(m, st, RS_K_DECODER, EPI_GELU_F32, hq16, m->wt, ns, H, H, ep, H)) return r;
-        { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(tq, ns, m->gt, m->bet, cf.ln_eps, H, hq32, hq16, st)); }
+        if (int r = gemm(m, st, RS_K_DECODER, EPI_GELU_F32, hq16, m->wt, ns, H, kx * H, ep, H)) return r;
+        { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(tq, ns, m->gt, m->bet, cf.ln_eps, H, hq32, hq16, kx, st)); }
         int* lab = m->lab.as<int>();
         float* ll = m->llog.as<float>();
         { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_gather_labels(d_tok, sm, c.s0, c.s1, lab, st)); }
         ep = EpiArgs{}; ep.bias = m->bdec; ep.n_valid = cf.vocab; ep.lse_part = m->part.as<float2>();
         ep.n_parts = m->vpad / 64; ep.label = lab; ep.label_logit = ll;
-        if (int r = gemm(m, st, RS_K_DECODER, EPI_LSE, hq16, m->wdec, ns, m->vpad, H, ep, cf.vocab)) return r;
+        if (int r = gemm(m, st, RS_K_DECODER, EPI_LSE, hq16, m->wdec, ns, m->vpad, kx * H, ep, cf.vocab)) return r;
         ProfScope ps(m, st, RS_K_OTHER, 0);
         HIPTRY(launch_lse_finalize(m->part.as<float2>(), m->vpad / 64, ll, ns, d_out_rows + c.s0, st));
     } else {
@@ -399,6 +421,11 @@ int rs_model_create(const rs_bert_cfg* cfg, int device, rs_model** out) {
     if (!m) return fail(RS_ENOMEM, "alloc");
     m->cfg = c;
     m->device = device;
+    if (c.precision != RS_PREC_FP16 && c.precision != RS_PREC_FP16X3) {
+        delete m;
+        return fail(RS_EARG, "unknown precision");
+    }
+    m->kx = c.precision == RS_PREC_FP16X3 ? 3 : 1;
     *out = m;
     return RS_OK;
 }
@@ -435,7 +462,7 @@ int rs_model_finalize(rs_model* m) {
     if (!miss.empty()) return fail(RS_ESTATE, "tensor " + miss);
     hipError_t err = hipSuccess;
 #define UP32(dst, src, n) do { dst = upload_f32(m, *(src), (n), &err); if (err != hipSuccess) return fail(RS_EHIP, "upload"); } while (0)
-#define UP16(dst, src, rp, cols) do { dst = upload_f16(m, *(src), (rp), (cols), &err); if (err != hipSuccess) return fail(RS_EHIP, "upload"); } while (0)
+#define UP16(dst, src, rp, cols) do { dst = upload_f16(m, *(src), (rp), (cols), m->kx, &err); if (err != hipSuccess) return fail(RS_EHIP, "upload"); } while (0)
     UP32(m->word32, word, V * H);
     UP32(m->pos32, pos, (size_t)c.max_pos * H);
     UP32(m->type32, typ, H);     // token_type_ids are all 0 (modeling_bert.py:88-94)

@@ -13,7 +13,7 @@ Tensors cross the C ABI as device pointers on ``torch.cuda.current_stream()``.
 from __future__ import annotations
 
 import ctypes
-from typing import Dict, Optional, Tuple
+from typing import Dict, Tuple
 
 import numpy as np
 import torch
@@ -28,7 +28,7 @@ class BertEngine:
 
     def __init__(self, weights: Dict[str, np.ndarray], shape: BertShape = BERT_BASE,
                  heads: int = _lib.RS_HEAD_MLM, device: int | str | torch.device = 0,
-                 max_rows: int = 65536):
+                 max_rows: int = 65536, precision: str = "fp16"):
         if not torch.cuda.is_available():
             raise RuntimeError("librescore needs a HIP GPU (no CPU fallback)")
         self.lib = _lib.load()
@@ -37,7 +37,9 @@ class BertEngine:
                                    else device)
         torch.cuda.set_device(self.device)
         cfg = _lib.RsBertCfg(shape.vocab, shape.hidden, shape.layers, shape.heads, shape.intermediate,
-                             shape.max_pos, shape.type_vocab, shape.ln_eps, shape.mask_id, heads)
+                             shape.max_pos, shape.type_vocab, shape.ln_eps, shape.mask_id, heads,
+                             _lib.RS_PREC[precision])
+        self.precision = precision
         h = ctypes.c_void_p()
         _lib.check(self.lib.rs_model_create(ctypes.byref(cfg), self.device.index, ctypes.byref(h)))
         self.handle = h
@@ -85,8 +87,9 @@ class BertEngine:
 class PLLScorer(BertEngine):
     """MLM_PLL scorer (BertForMaskedLM head)."""
 
-    def __init__(self, weights, shape: BertShape = BERT_BASE, device=0, max_rows: int = 65536):
-        super().__init__(weights, shape, _lib.RS_HEAD_MLM, device, max_rows)
+    def __init__(self, weights, shape: BertShape = BERT_BASE, device=0, max_rows: int = 65536,
+                 precision: str = "fp16"):
+        super().__init__(weights, shape, _lib.RS_HEAD_MLM, device, max_rows, precision)
 
     def score_nbest(self, tokens, hyp_off, return_rows: bool = False):
         """tokens int32 [sum T] ([CLS] w.. [SEP] per hypothesis), hyp_off int [H+1].
@@ -157,8 +160,9 @@ class PLLScorer(BertEngine):
 class RescoreBertScorer(BertEngine):
     """RescoreBert scorer on ragged hypotheses (CLS head)."""
 
-    def __init__(self, weights, shape: BertShape = BERT_BASE, device=0, max_rows: int = 65536):
-        super().__init__(weights, shape, _lib.RS_HEAD_CLS, device, max_rows)
+    def __init__(self, weights, shape: BertShape = BERT_BASE, device=0, max_rows: int = 65536,
+                 precision: str = "fp16x3"):
+        super().__init__(weights, shape, _lib.RS_HEAD_CLS, device, max_rows, precision)
 
     def score_nbest(self, tokens, hyp_off) -> torch.Tensor:
         off = np.ascontiguousarray(hyp_off, np.int32)
@@ -180,9 +184,9 @@ class RescoreBertHIP(torch.nn.Module):
     a model name, since nothing can be fetched offline."""
 
     def __init__(self, weights: Dict[str, np.ndarray], shape: BertShape = BERT_BASE, device=0,
-                 max_rows: int = 65536):
+                 max_rows: int = 65536, precision: str = "fp16x3"):
         super().__init__()
-        self.engine = RescoreBertScorer(weights, shape, device, max_rows)
+        self.engine = RescoreBertScorer(weights, shape, device, max_rows, precision)
 
     def forward(self, input_ids: torch.Tensor, attention_mask: torch.Tensor) -> torch.Tensor:
         am = attention_mask.detach().to("cpu", torch.int64)
@@ -204,5 +208,3 @@ def pll_of(weights, nb: NBest, shape: BertShape = BERT_BASE, device=0) -> np.nda
     finally:
         sc.close()
 
-
-_unused: Optional[int] = None

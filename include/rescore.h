@@ -51,7 +51,16 @@ typedef struct rs_bert_cfg {
     float ln_eps;
     int32_t mask_id;
     int32_t heads_mask;   /* RS_HEAD_MLM | RS_HEAD_CLS */
+    int32_t precision;    /* RS_PREC_FP16 or RS_PREC_FP16X3 */
 } rs_bert_cfg;
+
+/* GEMM operand precision.  FP16: fp16 MFMA inputs, fp32 accumulation (MLM_PLL default:
+ * per-row log-probs within 1e-4 relative of fp32).  FP16X3: each fp32 operand is split
+ * into fp16 hi + lo and the three significant products are accumulated by the same MFMA
+ * kernel along a 3x longer K (fp32-level accuracy at 1/3 the fp16 rate; RescoreBert
+ * default, whose O(1) CLS scores need it for 1e-3 relative). */
+#define RS_PREC_FP16 0
+#define RS_PREC_FP16X3 1
 
 int rs_version(void);
 const char* rs_last_error(void);

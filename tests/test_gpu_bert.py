@@ -76,6 +76,17 @@ def test_pll_tiny_golden(pll_tiny, golden_dir):
     assert rel_err(rows.cpu().numpy(), g["row_lp"]).max() < REL
 
 
+def test_pll_fp16x3_golden(w_base, golden_dir):
+    """Split-fp16 (x3) precision mode: fp32-level accuracy from fp16 MFMA."""
+    from asr_rescoring_amd.scorer import PLLScorer
+    g = _load(golden_dir, "pll_base.npz")
+    s = PLLScorer(w_base, BERT_BASE, device=0, max_rows=4096, precision="fp16x3")
+    pll, rows = s.score_nbest(g["tokens"], g["hyp_off"], return_rows=True)
+    s.close()
+    assert rel_err(pll.cpu().numpy(), g["pll"]).max() < 2e-5
+    assert rel_err(rows.cpu().numpy(), g["row_lp"]).max() < 2e-5
+
+
 def test_cls_golden(w_base, w_tiny, golden_dir):
     from asr_rescoring_amd.scorer import RescoreBertScorer
     for w, shape, name, key in ((w_base, BERT_BASE, "cls_base.npz", "cls"), (w_tiny, BERT_TINY, "pll_tiny.npz", "cls")):
