@@ -6,14 +6,18 @@
 // MLM_PLL/main.py:101-105 fused as an online logsumexp epilogue).
 //
 // gfx950 design:
-//  * v_mfma_f32_32x32x16_f16, fp32 accumulators; A and W both K-contiguous, so A and B
-//    fragments are the same 16-byte ds_read_b128 pattern (lane l: row l&31, k-chunk l>>5).
-//  * BK = 64 (128-byte tile rows), two LDS stages filled by global_load_lds_dwordx4
-//    (1 KiB = 8 rows per wave-instruction).  The LDS image is written lane-linear, so the
-//    XOR swizzle (chunk ^= (row>>1)&7) is applied to the per-lane global SOURCE address and
-//    to the ds_read address (the same involution): conflict-free ds_read_b128 for the
-//    16-lane groups of a 32-row fragment read.
-//  * XCD-aware bijective block remap: consecutive tiles (same A row panel) share an XCD L2.
+//  * v_mfma_f32_32x32x16_f16, fp32 accumulators, operands SWAPPED (D = W_tile . A_tile^T):
+//    the accumulator's lane index is the output ROW and its registers run along the output
+//    COLUMNS, so every lane owns 4 consecutive columns of a row -> 16-byte epilogue stores,
+//    16-byte bias/residual loads, and row reductions (decoder logsumexp) mostly in-register.
+//  * A and W are both K-contiguous: both fragments are one ds_read_b128 (lane l: row l&31,
+//    k-chunk l>>5).  BK = 64 (128-byte LDS tile rows).
+//  * LDS ring of NSTAGE stages filled by global_load_lds_dwordx4 (1 KiB = 8 rows per
+//    wave-instruction); counted `s_waitcnt vmcnt` + raw s_barrier (one per K-step) keep the
+//    next stage's DMA in flight across the barrier (a __syncthreads() would drain it).
+//    The LDS image is lane-linear, so the XOR swizzle (chunk ^= (row>>1)&7) goes on the
+//    per-lane global SOURCE address and on the ds_read address: conflict-free b128 reads.
+//  * Bijective XCD-aware block remap: consecutive tiles (same A row panel) share an XCD L2.
 #include "common.h"
 
 namespace {
@@ -22,7 +26,30 @@ constexpr int BK = 64;
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
-template <int BM, int BN, int WM, int WN, int EPI>
+// GELU(x) = 0.5 x erfc(-x/sqrt2); erfc by the Chebyshev fit of Numerical Recipes
+// (fractional error < 1.2e-7 everywhere): one exp + one rcp + 10 FMAs.
+__device__ __forceinline__ float gelu_fast(float x) {
+    const float z = fabsf(x) * 0.70710678118654752f;
+    const float t = __frcp_rn(1.0f + 0.5f * z);
+    float p = 0.17087277f;
+    p = fmaf(p, t, -0.82215223f);
+    p = fmaf(p, t, 1.48851587f);
+    p = fmaf(p, t, -1.13520398f);
+    p = fmaf(p, t, 0.27886807f);
+    p = fmaf(p, t, -0.18628806f);
+    p = fmaf(p, t, 0.09678418f);
+    p = fmaf(p, t, 0.37409196f);
+    p = fmaf(p, t, 1.00002368f);
+    p = fmaf(p, t, -1.26551223f);
+    const float y = t * __expf(p - z * z);          // erfc(|x|/sqrt2)
+    return x >= 0.f ? 0.5f * x * (2.0f - y) : 0.5f * x * y;
+}
+
+__device__ __forceinline__ void store4(f16* p, float4 v) {
+    *(half4*)p = (half4){(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
+}
+
+template <int BM, int BN, int WM, int WN, int NSTAGE, int EPI>
 __global__ void __launch_bounds__(WM * WN * 64)
 gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int n_tiles_n,
                 EpiArgs ep) {
@@ -81,97 +108,127 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){};
 
     const int nk = K / BK;
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < NSTAGE - 1; ++s)
+        if (s < nk) stage(s, s * BK);
 
     const int frow = lane & 31, fh = lane >> 5;
+    int buf = 0;
     for (int kt = 0; kt < nk; ++kt) {
-        const int cur = kt & 1;
-        if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
-        const char* sA = smem + cur * STAGE;
+        // tile kt landed for this wave: all later-issued stages may stay in flight
+        if (kt + NSTAGE - 2 < nk) {
+            if constexpr (NSTAGE == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+        // every wave's part of tile kt landed; every wave finished reading tile kt-1
+        asm volatile("s_barrier" ::: "memory");
+        if (kt + NSTAGE - 1 < nk) {
+            int nb = buf + NSTAGE - 1;
+            if (nb >= NSTAGE) nb -= NSTAGE;
+            stage(nb, (kt + NSTAGE - 1) * BK);
+        }
+        const char* sA = smem + buf * STAGE;
         const char* sB = sA + A_BYTES;
-#pragma unroll
-        for (int s = 0; s < BK / 16; ++s) {
-            half8 af[TM], bf[TN];
+        // fragments of k-substep s+1 are read while the MFMAs of substep s issue
+        half8 af0[TM], bf0[TN], af1[TM], bf1[TN];
+        auto load_frags = [&](int s, half8 (&af)[TM], half8 (&bf)[TN]) {
             const int lc = 2 * s + fh;
-#pragma unroll
-            for (int i = 0; i < TM; ++i) {
-                const int row = wm * WTM + i * 32 + frow;
-                af[i] = *(const half8*)(sA + row * 128 + (swz(row, lc) << 4));
-            }
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int row = wn * WTN + j * 32 + frow;
                 bf[j] = *(const half8*)(sB + row * 128 + (swz(row, lc) << 4));
             }
 #pragma unroll
+            for (int i = 0; i < TM; ++i) {
+                const int row = wm * WTM + i * 32 + frow;
+                af[i] = *(const half8*)(sA + row * 128 + (swz(row, lc) << 4));
+            }
+        };
+        auto mfmas = [&](const half8 (&af)[TM], const half8 (&bf)[TN]) {
+#pragma unroll
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(af[i], bf[j], acc[i][j], 0, 0, 0);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+        };
+        load_frags(0, af0, bf0);
+        load_frags(1, af1, bf1);
+        mfmas(af0, bf0);
+        load_frags(2, af0, bf0);
+        mfmas(af1, bf1);
+        load_frags(3, af1, bf1);
+        mfmas(af0, bf0);
+        mfmas(af1, bf1);
+        buf = buf + 1 == NSTAGE ? 0 : buf + 1;
     }
 
-    // ---------------- epilogue (C/D layout: col = lane&31, row = (r&3)+8(r>>2)+4(lane>>5))
-    const int rbase = m0 + wm * WTM + 4 * fh;
-    const int cbase = n0 + wn * WTN + frow;
+    // ---------------- epilogue.  acc[i][j][4g + e] = C[row][col + e],
+    //   row = m0 + wm*WTM + 32i + (lane&31),  col = n0 + wn*WTN + 32j + 8g + 4(lane>>5)
+    const int rbase = m0 + wm * WTM + frow;
+    const int cbase = n0 + wn * WTN + 4 * fh;
     if constexpr (EPI == EPI_LSE) {
+        // per (row, 64-column wave slab): max and sum exp over the slab + label logit
         const int slab = (n0 + wn * WTN) / WTN;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
+            const int row = rbase + i * 32;
+            const int lab = row < ep.m_valid ? ep.label[row] : -1;
+            float v[TN][16];
+            float mx = -INFINITY;
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
-                float v[TN];
-                float mx = -INFINITY;
+            for (int j = 0; j < TN; ++j)
 #pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    const int col = cbase + j * 32;
-                    v[j] = col < ep.n_valid ? acc[i][j][r] + ep.bias[col] : -INFINITY;
-                    mx = fmaxf(mx, v[j]);
+                for (int g = 0; g < 4; ++g) {
+                    const int col = cbase + j * 32 + 8 * g;
+                    const float4 b4 = *(const float4*)(ep.bias + col);
+                    const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const float x = col + e < ep.n_valid ? acc[i][j][4 * g + e] + bb[e] : -INFINITY;
+                        v[j][4 * g + e] = x;
+                        mx = fmaxf(mx, x);
+                        if (col + e == lab) ep.label_logit[row] = x;
+                    }
                 }
+            mx = fmaxf(mx, __shfl_xor(mx, 32));
+            float sm = 0.f;
 #pragma unroll
-                for (int o = 16; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-                float sm = 0.f;
+            for (int j = 0; j < TN; ++j)
 #pragma unroll
-                for (int j = 0; j < TN; ++j) sm += (v[j] == -INFINITY) ? 0.f : __expf(v[j] - mx);
-#pragma unroll
-                for (int o = 16; o > 0; o >>= 1) sm += __shfl_xor(sm, o);
-                if (row < ep.m_valid) {
-                    if (frow == 0) ep.lse_part[(size_t)row * ep.n_parts + slab] = make_float2(mx, sm);
-                    const int lab = ep.label[row];
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        if (cbase + j * 32 == lab) ep.label_logit[row] = v[j];
-                }
-            }
+                for (int e = 0; e < 16; ++e) sm += v[j][e] == -INFINITY ? 0.f : __expf(v[j][e] - mx);
+            sm += __shfl_xor(sm, 32);
+            if (fh == 0 && row < ep.m_valid)
+                ep.lse_part[(size_t)row * ep.n_parts + slab] = make_float2(mx, sm);
         }
     } else {
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
+        for (int j = 0; j < TN; ++j) {
 #pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                const int col = cbase + j * 32;
-                const float bias = ep.bias[col];
+            for (int g = 0; g < 4; ++g) {
+                const int col = cbase + j * 32 + 8 * g;
+                const float4 b4 = *(const float4*)(ep.bias + col);
 #pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const int row = rbase + i * 32 + (r & 3) + 8 * (r >> 2);
+                for (int i = 0; i < TM; ++i) {
+                    const int row = rbase + i * 32;
                     if (row >= ep.m_valid) continue;
-                    float x = acc[i][j][r] + bias;
+                    float4 x = make_float4(acc[i][j][4 * g] + b4.x, acc[i][j][4 * g + 1] + b4.y,
+                                           acc[i][j][4 * g + 2] + b4.z, acc[i][j][4 * g + 3] + b4.w);
                     const size_t o = (size_t)row * ep.ldc + col;
                     if constexpr (EPI == EPI_BIAS_F16) {
-                        ((f16*)ep.out)[o] = (f16)x;
+                        store4((f16*)ep.out + o, x);
                     } else if constexpr (EPI == EPI_BIAS_F32) {
-                        ((float*)ep.out)[o] = x;
+                        *(float4*)((float*)ep.out + o) = x;
                     } else if constexpr (EPI == EPI_GELU_F16) {
-                        put_split((f16*)ep.out + (size_t)row * ep.ldc, col, ep.nlog, ep.kx, gelu_erf(x));
+                        x = make_float4(gelu_fast(x.x), gelu_fast(x.y), gelu_fast(x.z), gelu_fast(x.w));
+                        put_split4((f16*)ep.out + (size_t)row * ep.ldc, col, ep.nlog, ep.kx, x);
                     } else if constexpr (EPI == EPI_GELU_F32) {
-                        ((float*)ep.out)[o] = gelu_erf(x);
+                        *(float4*)((float*)ep.out + o) =
+                            make_float4(gelu_fast(x.x), gelu_fast(x.y), gelu_fast(x.z), gelu_fast(x.w));
                     } else {  // EPI_RES_F32
-                        ((float*)ep.out)[o] = x + ep.res[o];
+                        const float4 rr = *(const float4*)(ep.res + o);
+                        *(float4*)((float*)ep.out + o) = make_float4(x.x + rr.x, x.y + rr.y, x.z + rr.z, x.w + rr.w);
                     }
                 }
             }
@@ -179,38 +236,65 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     }
 }
 
-template <int BM, int BN, int WM, int WN, int EPI>
+template <int BM, int BN, int WM, int WN, int NSTAGE, int EPI>
 hipError_t launch_t(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep,
                     hipStream_t st) {
-    constexpr int smem = 2 * (BM + BN) * BK * 2;
+    constexpr int smem = NSTAGE * (BM + BN) * BK * 2;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_f16_kernel<BM, BN, WM, WN, EPI>,
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_f16_kernel<BM, BN, WM, WN, NSTAGE, EPI>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, smem);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     const int ntn = N_pad / BN;
     const int grid = (M_pad / BM) * ntn;
-    hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WM, WN, EPI>), dim3(grid), dim3(WM * WN * 64),
+    hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WM, WN, NSTAGE, EPI>), dim3(grid), dim3(WM * WN * 64),
                        smem, st, A, W, K, ntn, ep);
     return hipGetLastError();
 }
 
+// Tile configuration (selected per call; env RS_GEMM_CFG overrides for A/B runs):
+//   0: 256x256, 8 waves (2x4, 128x64 per wave), 2 stages (128 KiB LDS)
+//   1: 256x128, 8 waves (4x2,  64x64 per wave), 3 stages (144 KiB LDS)
+//   2: 128x128, 4 waves (2x2,  64x64 per wave), 2 stages ( 64 KiB LDS)
+int g_cfg = -1;
+
+int pick_cfg(int N_pad) {
+    if (g_cfg < 0) {
+        const char* e = getenv("RS_GEMM_CFG");
+        g_cfg = e ? atoi(e) : 100;
+    }
+    int c = g_cfg;
+    if (c == 100) c = (N_pad % 256 == 0) ? 0 : 1;
+    if (c == 0 && N_pad % 256) c = 1;
+    return c;
+}
+
+template <int EPI>
+hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep,
+                      hipStream_t st) {
+    switch (pick_cfg(N_pad)) {
+        case 0: return launch_t<256, 256, 2, 4, 2, EPI>(A, W, M_pad, N_pad, K, ep, st);
+        case 1: return launch_t<256, 128, 4, 2, 3, EPI>(A, W, M_pad, N_pad, K, ep, st);
+        default: return launch_t<128, 128, 2, 2, 2, EPI>(A, W, M_pad, N_pad, K, ep, st);
+    }
+}
+
 }  // namespace
 
-int gemm_row_align() { return 128; }
+int gemm_row_align() { return 256; }
 
 hipError_t launch_gemm(int epi, const f16* A, const f16* W, int M_pad, int N_pad, int K,
                        const EpiArgs& ep, hipStream_t st) {
-    if (M_pad % 128 || N_pad % 128 || K % BK || M_pad <= 0) return hipErrorInvalidValue;
+    if (M_pad % 256 || N_pad % 128 || K % BK || M_pad <= 0) return hipErrorInvalidValue;
     switch (epi) {
-        case EPI_BIAS_F16: return launch_t<128, 128, 2, 2, EPI_BIAS_F16>(A, W, M_pad, N_pad, K, ep, st);
-        case EPI_GELU_F16: return launch_t<128, 128, 2, 2, EPI_GELU_F16>(A, W, M_pad, N_pad, K, ep, st);
-        case EPI_GELU_F32: return launch_t<128, 128, 2, 2, EPI_GELU_F32>(A, W, M_pad, N_pad, K, ep, st);
-        case EPI_RES_F32: return launch_t<128, 128, 2, 2, EPI_RES_F32>(A, W, M_pad, N_pad, K, ep, st);
-        case EPI_LSE: return launch_t<128, 128, 2, 2, EPI_LSE>(A, W, M_pad, N_pad, K, ep, st);
-        case EPI_BIAS_F32: return launch_t<128, 128, 2, 2, EPI_BIAS_F32>(A, W, M_pad, N_pad, K, ep, st);
+        case EPI_BIAS_F16: return launch_epi<EPI_BIAS_F16>(A, W, M_pad, N_pad, K, ep, st);
+        case EPI_GELU_F16: return launch_epi<EPI_GELU_F16>(A, W, M_pad, N_pad, K, ep, st);
+        case EPI_GELU_F32: return launch_epi<EPI_GELU_F32>(A, W, M_pad, N_pad, K, ep, st);
+        case EPI_RES_F32: return launch_epi<EPI_RES_F32>(A, W, M_pad, N_pad, K, ep, st);
+        case EPI_LSE: return launch_epi<EPI_LSE>(A, W, M_pad, N_pad, K, ep, st);
+        case EPI_BIAS_F32: return launch_epi<EPI_BIAS_F32>(A, W, M_pad, N_pad, K, ep, st);
     }
     return hipErrorInvalidValue;
 }
