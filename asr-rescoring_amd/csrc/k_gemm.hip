@@ -22,9 +22,14 @@
 
 namespace {
 
-constexpr int BK = 64;
-
-__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+// LDS tile rows are BK fp16 = 2*BK bytes (BK = 64: 128 B, 8 chunks; BK = 32: 64 B, 4 chunks).
+// Chunk swizzle spreading the 16 rows a ds_read_b128 lane group reads over the 16 slots of
+// a 256-byte bank row: BK 64 -> chunk ^ ((row>>1)&7), BK 32 -> chunk ^ ((row>>2)&3).
+template <int BK>
+__device__ __forceinline__ int swz(int row, int chunk) {
+    if constexpr (BK == 64) return chunk ^ ((row >> 1) & 7);
+    else return chunk ^ ((row >> 2) & 3);
+}
 
 // GELU(x) = 0.5 x erfc(-x/sqrt2); erfc by the Chebyshev fit of Numerical Recipes
 // (fractional error < 1.2e-7 everywhere): one exp + one rcp + 10 FMAs.
@@ -49,7 +54,7 @@ __device__ __forceinline__ void store4(f16* p, float4 v) {
     *(half4*)p = (half4){(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
 }
 
-template <int BM, int BN, int WM, int WN, int NSTAGE, int EPI>
+template <int BM, int BN, int WM, int WN, int NSTAGE, int BK, int EPI>
 __global__ void __launch_bounds__(WM * WN * 64)
 gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int n_tiles_n,
                 EpiArgs ep) {
@@ -58,7 +63,10 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     constexpr int STAGE = (BM + BN) * BK * 2;
     constexpr int WTM = BM / WM, WTN = BN / WN;
     constexpr int TM = WTM / 32, TN = WTN / 32;
-    constexpr int A_PIECES = BM / 8, PIECES = (BM + BN) / 8;
+    constexpr int RB = BK * 2;            // LDS row bytes
+    constexpr int CPR = BK / 8;           // 16-byte chunks per row
+    constexpr int RPP = 1024 / RB;        // rows per 1 KiB LDS-DMA piece
+    constexpr int A_PIECES = BM / RPP, PIECES = (BM + BN) / RPP;
     static_assert(PIECES % NW == 0, "pieces per wave");
     constexpr int PPW = PIECES / NW;
 
@@ -81,13 +89,13 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
 #pragma unroll
     for (int p = 0; p < PPW; ++p) {
         const int piece = p * NW + wave;
-        const int lrow = lane >> 3, pc = lane & 7;
+        const int lrow = lane / CPR, pc = lane % CPR;
         if (piece < A_PIECES) {
-            const int row = piece * 8 + lrow;
-            src[p] = A + (size_t)(m0 + row) * K + swz(row, pc) * 8;
+            const int row = piece * RPP + lrow;
+            src[p] = A + (size_t)(m0 + row) * K + swz<BK>(row, pc) * 8;
         } else {
-            const int row = (piece - A_PIECES) * 8 + lrow;
-            src[p] = W + (size_t)(n0 + row) * K + swz(row, pc) * 8;
+            const int row = (piece - A_PIECES) * RPP + lrow;
+            src[p] = W + (size_t)(n0 + row) * K + swz<BK>(row, pc) * 8;
         }
         ldsoff[p] = piece * 1024;
     }
@@ -138,12 +146,12 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
                 const int row = wn * WTN + j * 32 + frow;
-                bf[j] = *(const half8*)(sB + row * 128 + (swz(row, lc) << 4));
+                bf[j] = *(const half8*)(sB + row * RB + (swz<BK>(row, lc) << 4));
             }
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
                 const int row = wm * WTM + i * 32 + frow;
-                af[i] = *(const half8*)(sA + row * 128 + (swz(row, lc) << 4));
+                af[i] = *(const half8*)(sA + row * RB + (swz<BK>(row, lc) << 4));
             }
         };
         auto mfmas = [&](const half8 (&af)[TM], const half8 (&bf)[TN]) {
@@ -156,10 +164,12 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         load_frags(0, af0, bf0);
         load_frags(1, af1, bf1);
         mfmas(af0, bf0);
-        load_frags(2, af0, bf0);
-        mfmas(af1, bf1);
-        load_frags(3, af1, bf1);
-        mfmas(af0, bf0);
+        if constexpr (BK == 64) {
+            load_frags(2, af0, bf0);
+            mfmas(af1, bf1);
+            load_frags(3, af1, bf1);
+            mfmas(af0, bf0);
+        }
         mfmas(af1, bf1);
         buf = buf + 1 == NSTAGE ? 0 : buf + 1;
     }
@@ -236,20 +246,21 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     }
 }
 
-template <int BM, int BN, int WM, int WN, int NSTAGE, int EPI>
+template <int BM, int BN, int WM, int WN, int NSTAGE, int BK, int EPI>
 hipError_t launch_t(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep,
                     hipStream_t st) {
     constexpr int smem = NSTAGE * (BM + BN) * BK * 2;
+    if (K % BK) return hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_f16_kernel<BM, BN, WM, WN, NSTAGE, EPI>,
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_f16_kernel<BM, BN, WM, WN, NSTAGE, BK, EPI>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, smem);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     const int ntn = N_pad / BN;
     const int grid = (M_pad / BM) * ntn;
-    hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WM, WN, NSTAGE, EPI>), dim3(grid), dim3(WM * WN * 64),
+    hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WM, WN, NSTAGE, BK, EPI>), dim3(grid), dim3(WM * WN * 64),
                        smem, st, A, W, K, ntn, ep);
     return hipGetLastError();
 }
@@ -258,6 +269,8 @@ hipError_t launch_t(const f16* A, const f16* W, int M_pad, int N_pad, int K, con
 //   0: 256x256, 8 waves (2x4, 128x64 per wave), 2 stages (128 KiB LDS)
 //   1: 256x128, 8 waves (4x2,  64x64 per wave), 3 stages (144 KiB LDS)
 //   2: 128x128, 4 waves (2x2,  64x64 per wave), 2 stages ( 64 KiB LDS)
+//   3: 256x128, 8 waves (4x2,  64x64 per wave), 3 stages of BK=32 (72 KiB LDS: 2 blocks/CU)
+//   4: 256x256, 8 waves (2x4, 128x64 per wave), 3 stages of BK=32 (96 KiB LDS)
 int g_cfg = -1;
 
 int pick_cfg(int N_pad) {
@@ -267,7 +280,7 @@ int pick_cfg(int N_pad) {
     }
     int c = g_cfg;
     if (c == 100) c = (N_pad % 256 == 0) ? 0 : 1;
-    if (c == 0 && N_pad % 256) c = 1;
+    if ((c == 0 || c == 4) && N_pad % 256) c = 1;
     return c;
 }
 
@@ -275,9 +288,11 @@ template <int EPI>
 hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep,
                       hipStream_t st) {
     switch (pick_cfg(N_pad)) {
-        case 0: return launch_t<256, 256, 2, 4, 2, EPI>(A, W, M_pad, N_pad, K, ep, st);
-        case 1: return launch_t<256, 128, 4, 2, 3, EPI>(A, W, M_pad, N_pad, K, ep, st);
-        default: return launch_t<128, 128, 2, 2, 2, EPI>(A, W, M_pad, N_pad, K, ep, st);
+        case 0: return launch_t<256, 256, 2, 4, 2, 64, EPI>(A, W, M_pad, N_pad, K, ep, st);
+        case 1: return launch_t<256, 128, 4, 2, 3, 64, EPI>(A, W, M_pad, N_pad, K, ep, st);
+        case 3: return launch_t<256, 128, 4, 2, 3, 32, EPI>(A, W, M_pad, N_pad, K, ep, st);
+        case 4: return launch_t<256, 256, 2, 4, 3, 32, EPI>(A, W, M_pad, N_pad, K, ep, st);
+        default: return launch_t<128, 128, 2, 2, 2, 64, EPI>(A, W, M_pad, N_pad, K, ep, st);
     }
 }
 
@@ -287,7 +302,7 @@ int gemm_row_align() { return 256; }
 
 hipError_t launch_gemm(int epi, const f16* A, const f16* W, int M_pad, int N_pad, int K,
                        const EpiArgs& ep, hipStream_t st) {
-    if (M_pad % 256 || N_pad % 128 || K % BK || M_pad <= 0) return hipErrorInvalidValue;
+    if (M_pad % 256 || N_pad % 128 || K % 64 || M_pad <= 0) return hipErrorInvalidValue;
     switch (epi) {
         case EPI_BIAS_F16: return launch_epi<EPI_BIAS_F16>(A, W, M_pad, N_pad, K, ep, st);
         case EPI_GELU_F16: return launch_epi<EPI_GELU_F16>(A, W, M_pad, N_pad, K, ep, st);
