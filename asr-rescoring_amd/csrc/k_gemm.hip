@@ -54,7 +54,9 @@ __device__ __forceinline__ void store4(f16* p, float4 v) {
     *(half4*)p = (half4){(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
 }
 
-template <int BM, int BN, int WM, int WN, int NSTAGE, int BK, int EPI>
+// DBG (timing experiments only, rs_debug_gemm): bit0 = no K-loop staging (MFMA + LDS
+// reads on stale tiles), bit1 = no epilogue (accumulators kept alive, nothing stored).
+template <int BM, int BN, int WM, int WN, int NSTAGE, int BK, int EPI, int DBG = 0>
 __global__ void __launch_bounds__(WM * WN * 64)
 gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int n_tiles_n,
                 EpiArgs ep) {
@@ -132,7 +134,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         }
         // every wave's part of tile kt landed; every wave finished reading tile kt-1
         asm volatile("s_barrier" ::: "memory");
-        if (kt + NSTAGE - 1 < nk) {
+        if (!(DBG & 1) && kt + NSTAGE - 1 < nk) {
             int nb = buf + NSTAGE - 1;
             if (nb >= NSTAGE) nb -= NSTAGE;
             stage(nb, (kt + NSTAGE - 1) * BK);
@@ -174,6 +176,13 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         buf = buf + 1 == NSTAGE ? 0 : buf + 1;
     }
 
+    if constexpr (DBG & 2) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
+        return;
+    }
     // ---------------- epilogue.  acc[i][j][4g + e] = C[row][col + e],
     //   row = m0 + wm*WTM + 32i + (lane&31),  col = n0 + wn*WTN + 32j + 8g + 4(lane>>5)
     const int rbase = m0 + wm * WTM + frow;
@@ -246,21 +255,21 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     }
 }
 
-template <int BM, int BN, int WM, int WN, int NSTAGE, int BK, int EPI>
+template <int BM, int BN, int WM, int WN, int NSTAGE, int BK, int EPI, int DBG = 0>
 hipError_t launch_t(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep,
                     hipStream_t st) {
     constexpr int smem = NSTAGE * (BM + BN) * BK * 2;
     if (K % BK) return hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_f16_kernel<BM, BN, WM, WN, NSTAGE, BK, EPI>,
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_f16_kernel<BM, BN, WM, WN, NSTAGE, BK, EPI, DBG>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, smem);
         if (e != hipSuccess) return e;
         attr_set = true;
     }
     const int ntn = N_pad / BN;
     const int grid = (M_pad / BM) * ntn;
-    hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WM, WN, NSTAGE, BK, EPI>), dim3(grid), dim3(WM * WN * 64),
+    hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WM, WN, NSTAGE, BK, EPI, DBG>), dim3(grid), dim3(WM * WN * 64),
                        smem, st, A, W, K, ntn, ep);
     return hipGetLastError();
 }
@@ -312,4 +321,32 @@ hipError_t launch_gemm(int epi, const f16* A, const f16* W, int M_pad, int N_pad
         case EPI_BIAS_F32: return launch_epi<EPI_BIAS_F32>(A, W, M_pad, N_pad, K, ep, st);
     }
     return hipErrorInvalidValue;
+}
+
+// Timing/diagnostic entry (not part of the scoring path): one GEMM with an explicit tile
+// configuration and DBG bits, C = A[M,K].W[N,K]^T + bias -> fp16 [M, N].
+extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, const float* bias, void* out,
+                             int M, int N, int K, void* stream) {
+    EpiArgs ep{};
+    ep.bias = bias; ep.out = out; ep.ldc = N; ep.m_valid = M; ep.kx = 1; ep.nlog = N;
+    hipStream_t st = (hipStream_t)stream;
+    const f16* a = (const f16*)A;
+    const f16* w = (const f16*)W;
+    hipError_t e = hipErrorInvalidValue;
+#define RS_DBG(D)                                                                                     \
+    switch (cfg) {                                                                                    \
+        case 0: e = launch_t<256, 256, 2, 4, 2, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
+        case 1: e = launch_t<256, 128, 4, 2, 3, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
+        case 3: e = launch_t<256, 128, 4, 2, 3, 32, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
+        default: e = launch_t<128, 128, 2, 2, 2, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;   \
+    }
+    if (M % 256 || N % 256 || K % 64) return -1;
+    switch (dbg) {
+        case 0: RS_DBG(0); break;
+        case 1: RS_DBG(1); break;
+        case 2: RS_DBG(2); break;
+        default: RS_DBG(3); break;
+    }
+#undef RS_DBG
+    return e == hipSuccess ? 0 : -2;
 }

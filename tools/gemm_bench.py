@@ -1,0 +1,62 @@
+"""GEMM microbenchmark of librescore's fp16 MFMA kernel at the BERT projection shapes.
+
+Runs every tile configuration with the diagnostic DBG bits (0 full, 1 no K-loop staging,
+2 no epilogue, 3 neither) via ``rs_debug_gemm`` and prints TFLOP/s (HIP events on the
+current stream, random [-1, 1) operands).  Usage: python tools/gemm_bench.py [M]
+"""
+import ctypes
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import __graft_entry__  # noqa: E402
+
+__graft_entry__._import_pkg()
+from asr_rescoring_amd import _lib  # noqa: E402
+
+
+def main():
+    M = int(sys.argv[1]) if len(sys.argv) > 1 else 131072
+    cfgs = [int(c) for c in os.environ.get("CFGS", "0,1,2,3").split(",")]
+    lib = _lib.load()
+    fn = lib.rs_debug_gemm
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_int] * 3 + [ctypes.c_void_p]
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(0)
+    shapes = [(2304, 768), (768, 768), (3072, 768), (768, 3072)]
+    for N, K in shapes:
+        A = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).half()
+        W = (torch.rand(N, K, device=dev, generator=g) * 2 - 1).half()
+        b = torch.rand(N, device=dev, generator=g)
+        out = torch.empty(M, N, device=dev, dtype=torch.float16)
+        ref = None
+        for cfg in cfgs:
+            res = []
+            for dbg in (0, 1, 2, 3):
+                st = torch.cuda.current_stream().cuda_stream
+                call = lambda: fn(cfg, dbg, A.data_ptr(), W.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, st)  # noqa
+                for _ in range(3):
+                    assert call() == 0
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                reps = 10
+                e0.record()
+                for _ in range(reps):
+                    call()
+                e1.record()
+                torch.cuda.synchronize()
+                ms = e0.elapsed_time(e1) / reps
+                res.append(2.0 * M * N * K / (ms * 1e-3) / 1e12)
+                if dbg == 0:
+                    if ref is None:
+                        ref = (A[:4096].float() @ W.float().t() + b).half()
+                    err = (out[:4096].float() - ref.float()).abs().max().item()
+                    assert err < 0.05 * K ** 0.5, (cfg, err)
+            print(f"M={M} N={N} K={K} cfg={cfg}: full {res[0]:7.1f}  nostage {res[1]:7.1f}  "
+                  f"noepi {res[2]:7.1f}  neither {res[3]:7.1f} TF/s", flush=True)
+
+
+if __name__ == "__main__":
+    main()
