@@ -180,7 +180,11 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
-            for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
+            for (int j = 0; j < TN; ++j) {
+#if defined(__HIP_DEVICE_COMPILE__)
+                asm volatile("" ::"v"(acc[i][j]));
+#endif
+            }
         return;
     }
     // ---------------- epilogue.  acc[i][j][4g + e] = C[row][col + e],
