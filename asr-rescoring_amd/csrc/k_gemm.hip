@@ -226,32 +226,70 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 ep.lse_part[(size_t)row * ep.n_parts + slab] = make_float2(mx, sm);
         }
     } else {
+        // Through LDS: each wave parks one 32-row slice of its accumulators (fp32, row
+        // stride WTN+4 floats: conflict-free b128 writes) in a private region, then reads it
+        // back 8 consecutive columns per lane, so every global store covers whole 128/256-B
+        // row segments instead of 16-B pieces of 32 rows.
+        static_assert(WTN == 64, "epilogue assumes 64-column wave tiles");
+        constexpr int LDW = WTN + 4;
+        static_assert(NW * 32 * LDW * 4 <= NSTAGE * STAGE, "epilogue LDS");
+        __syncthreads();                                   // the LDS ring is no longer read
+        float* lw = (float*)smem + wave * 32 * LDW;
+        const int rr0 = lane >> 3, cc = (lane & 7) * 8;
+        const int col = n0 + wn * WTN + cc;
+        float bias[8];
+        {
+            const float4 b0 = *(const float4*)(ep.bias + col), b1 = *(const float4*)(ep.bias + col + 4);
+            bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w;
+            bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
+        }
 #pragma unroll
-        for (int j = 0; j < TN; ++j) {
+        for (int i = 0; i < TM; ++i) {
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int col = cbase + j * 32 + 8 * g;
-                const float4 b4 = *(const float4*)(ep.bias + col);
+            for (int j = 0; j < TN; ++j)
 #pragma unroll
-                for (int i = 0; i < TM; ++i) {
-                    const int row = rbase + i * 32;
-                    if (row >= ep.m_valid) continue;
-                    float4 x = make_float4(acc[i][j][4 * g] + b4.x, acc[i][j][4 * g + 1] + b4.y,
-                                           acc[i][j][4 * g + 2] + b4.z, acc[i][j][4 * g + 3] + b4.w);
+                for (int g = 0; g < 4; ++g)
+                    *(float4*)(lw + frow * LDW + j * 32 + 8 * g + 4 * fh) =
+                        make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+                const int rr = it * 8 + rr0;
+                const int row = m0 + wm * WTM + i * 32 + rr;
+                const float4 u0 = *(const float4*)(lw + rr * LDW + cc);
+                const float4 u1 = *(const float4*)(lw + rr * LDW + cc + 4);
+                float x[8] = {u0.x + bias[0], u0.y + bias[1], u0.z + bias[2], u0.w + bias[3],
+                              u1.x + bias[4], u1.y + bias[5], u1.z + bias[6], u1.w + bias[7]};
+                if (row < ep.m_valid) {
                     const size_t o = (size_t)row * ep.ldc + col;
+                    if constexpr (EPI == EPI_GELU_F16 || EPI == EPI_GELU_F32) {
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) x[e] = gelu_fast(x[e]);
+                    }
                     if constexpr (EPI == EPI_BIAS_F16) {
-                        store4((f16*)ep.out + o, x);
-                    } else if constexpr (EPI == EPI_BIAS_F32) {
-                        *(float4*)((float*)ep.out + o) = x;
+                        half8 h;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) h[e] = (f16)x[e];
+                        *(half8*)((f16*)ep.out + o) = h;
                     } else if constexpr (EPI == EPI_GELU_F16) {
-                        x = make_float4(gelu_fast(x.x), gelu_fast(x.y), gelu_fast(x.z), gelu_fast(x.w));
-                        put_split4((f16*)ep.out + (size_t)row * ep.ldc, col, ep.nlog, ep.kx, x);
-                    } else if constexpr (EPI == EPI_GELU_F32) {
-                        *(float4*)((float*)ep.out + o) =
-                            make_float4(gelu_fast(x.x), gelu_fast(x.y), gelu_fast(x.z), gelu_fast(x.w));
-                    } else {  // EPI_RES_F32
-                        const float4 rr = *(const float4*)(ep.res + o);
-                        *(float4*)((float*)ep.out + o) = make_float4(x.x + rr.x, x.y + rr.y, x.z + rr.z, x.w + rr.w);
+                        f16* orow = (f16*)ep.out + (size_t)row * ep.ldc;
+                        half8 h, l;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) {
+                            h[e] = (f16)x[e];
+                            l[e] = (f16)(x[e] - (float)h[e]);
+                        }
+                        *(half8*)(orow + col) = h;
+                        if (ep.kx == 3) {
+                            *(half8*)(orow + ep.nlog + col) = h;
+                            *(half8*)(orow + 2 * ep.nlog + col) = l;
+                        }
+                    } else if constexpr (EPI == EPI_RES_F32) {
+                        const float4 r0 = *(const float4*)(ep.res + o), r1 = *(const float4*)(ep.res + o + 4);
+                        *(float4*)((float*)ep.out + o) = make_float4(x[0] + r0.x, x[1] + r0.y, x[2] + r0.z, x[3] + r0.w);
+                        *(float4*)((float*)ep.out + o + 4) = make_float4(x[4] + r1.x, x[5] + r1.y, x[6] + r1.z, x[7] + r1.w);
+                    } else {  // EPI_BIAS_F32, EPI_GELU_F32
+                        *(float4*)((float*)ep.out + o) = make_float4(x[0], x[1], x[2], x[3]);
+                        *(float4*)((float*)ep.out + o + 4) = make_float4(x[4], x[5], x[6], x[7]);
                     }
                 }
             }
