@@ -205,6 +205,129 @@ attn_full_kernel(const QT* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H
     }
 }
 
+// MFMA attention (fp16 mode): one wave per (sequence, head); queries and keys in blocks
+// of 64 (two 32-row tiles each), online softmax across key blocks.
+//   X = S^T = K . Q^T   (v_mfma_f32_32x32x16_f16, A = K rows, B = Q rows: both 16-byte
+//                        row loads straight from the QKV buffer)
+//   accumulator layout: lane = query, registers = keys  -> softmax over keys in-lane
+//   (+ one xor-32 shuffle), no cross-lane reductions per element.
+//   O^T = V^T . P^T      the fp16 P built from X's registers is the B operand as is
+//                        (k-step s of key tile kt = registers 8s..8s+7, key order
+//                        16s + 8(j>>2) + 4h + (j&3)); V^T comes from LDS, written
+//                        transposed once per key block.
+__global__ void __launch_bounds__(64)
+attn_mfma_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
+                 f16* __restrict__ ctx, int kx) {
+    constexpr int VTS = 72;                       // V^T row stride (halfs): 64 keys + pad
+    __shared__ __attribute__((aligned(16))) f16 sVT[64 * VTS];
+    const int s = s0 + blockIdx.x, hd = blockIdx.y;
+    const int T = sm.len[s], rs = sm.row[s] - row0;
+    const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5;
+    const int ld = 3 * H;
+    const f16* base = qkv + (size_t)rs * ld + hd * 64;
+    const float scale = 0.125f;                   // head_dim ** -0.5
+    const bool one_block = T <= 64;               // V^T staged once for all query tiles
+
+    for (int q0 = 0; q0 < T; q0 += 32) {
+        // Q fragments (B operand): lane (query r, half h), k-step s: dims 16s + 8h .. +7
+        const int t = q0 + r;
+        half8 qf[4];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+            qf[ks] = t < T ? *(const half8*)(base + (size_t)t * ld + ks * 16 + hf * 8) : (half8){};
+        f32x16 o[2] = {(f32x16){}, (f32x16){}};  // O^T[d tile], lane = query
+        float m = -INFINITY, l = 0.f;
+
+        for (int k0 = 0; k0 < T; k0 += 64) {
+            if (!one_block || q0 == 0) {
+                // ---- V^T of this key block into LDS (zeros past T)
+                __syncthreads();
+#pragma unroll
+                for (int it = 0; it < 8; ++it) {
+                    const int kr = it * 8 + (lane >> 3), d0 = (lane & 7) * 8;
+                    const half8 v = k0 + kr < T ? *(const half8*)(base + (size_t)(k0 + kr) * ld + 2 * H + d0) : (half8){};
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) sVT[(d0 + e) * VTS + kr] = v[e];
+                }
+            }
+            // ---- X = K . Q^T  (two key tiles)
+            f32x16 x[2];
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt) {
+                const int key = k0 + kt * 32 + r;
+                f32x16 a = {};
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) {
+                    const half8 kf = key < T ? *(const half8*)(base + (size_t)key * ld + H + ks * 16 + hf * 8) : (half8){};
+                    a = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[ks], a, 0, 0, 0);
+                }
+                x[kt] = a;
+            }
+            // ---- online softmax over keys (registers + the other half-wave)
+            float bm = -INFINITY;
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int key = k0 + kt * 32 + (j & 3) + 8 * (j >> 2) + 4 * hf;
+                    const float v = key < T ? x[kt][j] * scale : -INFINITY;
+                    x[kt][j] = v;
+                    bm = fmaxf(bm, v);
+                }
+            bm = fmaxf(bm, __shfl_xor(bm, 32));
+            const float mn = fmaxf(m, bm);
+            const float alpha = __expf(m - mn);
+            half8 pf[2][2];                       // [kt][k-step]
+            float ls = 0.f;
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                for (int sk = 0; sk < 2; ++sk)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const f16 ph = (f16)__expf(x[kt][sk * 8 + e] - mn);
+                        pf[kt][sk][e] = ph;
+                        ls += (float)ph;
+                    }
+            ls += __shfl_xor(ls, 32);
+            l = l * alpha + ls;
+            m = mn;
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                for (int j = 0; j < 16; ++j) o[dt][j] *= alpha;
+            if (!one_block || q0 == 0) __syncthreads();   // sVT written by every lane
+            // ---- O^T += V^T . P^T
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt) {
+                const int d = dt * 32 + r;
+#pragma unroll
+                for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+                    for (int sk = 0; sk < 2; ++sk) {
+                        const int kb = kt * 32 + sk * 16 + 4 * hf;
+                        const half4 lo = *(const half4*)(sVT + d * VTS + kb);
+                        const half4 hi = *(const half4*)(sVT + d * VTS + kb + 8);
+                        const half8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf[kt][sk], o[dt], 0, 0, 0);
+                    }
+            }
+        }
+        // ---- store: lane = query, registers = dims (j&3) + 8(j>>2) + 4h of d tile dt
+        if (t < T) {
+            const float il = 1.0f / l;
+            f16* orow = ctx + (size_t)(rs + t) * kx * H;
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    put_split4(orow, hd * 64 + dt * 32 + 8 * g + 4 * hf, H, kx,
+                               make_float4(o[dt][4 * g] * il, o[dt][4 * g + 1] * il,
+                                           o[dt][4 * g + 2] * il, o[dt][4 * g + 3] * il));
+        }
+    }
+}
+
 // Last layer: one wave per (sequence, head), only the scored query row.  Lanes over keys
 // for QK^T, lanes over the 64 head dims for P.V.
 template <class QT>
@@ -342,10 +465,13 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
                                  int H, int heads, f16* ctx, int kx, hipStream_t st) {
     if (s1 <= s0) return hipSuccess;
     const dim3 grid(s1 - s0, heads);
+    static const int valu = getenv("RS_ATTN_VALU") ? atoi(getenv("RS_ATTN_VALU")) : 0;
     if (qkv32)
         hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
-    else
+    else if (valu)
         hipLaunchKernelGGL(attn_full_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
+    else
+        hipLaunchKernelGGL(attn_mfma_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
     return hipGetLastError();
 }
 
