@@ -76,19 +76,20 @@ def mlm_keys(shape: BertShape, with_mlm_head: bool = True,
         yield p + "output.dense.bias", (H,), "bias"
         yield p + "output.LayerNorm.weight", (H,), "ln_w"
         yield p + "output.LayerNorm.bias", (H,), "ln_b"
-    if with_pooler:
-        yield "bert.pooler.dense.weight", (H, H), "mat"
-        yield "bert.pooler.dense.bias", (H,), "bias"
-    if with_mlm_head:
-        c = "cls.predictions."
-        yield c + "transform.dense.weight", (H, H), "mat"
-        yield c + "transform.dense.bias", (H,), "bias"
-        yield c + "transform.LayerNorm.weight", (H,), "ln_w"
-        yield c + "transform.LayerNorm.bias", (H,), "ln_b"
-        yield c + "bias", (V,), "bias"
-    if with_cls_linear:
-        yield "linear.weight", (1, H), "mat"
-        yield "linear.bias", (1,), "bias"
+    # Heads come last, in a fixed order, and are always drawn (then filtered by the flags)
+    # so that a given seed yields the same tensor for a given key whatever heads are kept.
+    c = "cls.predictions."
+    heads = [(c + "transform.dense.weight", (H, H), "mat", with_mlm_head),
+             (c + "transform.dense.bias", (H,), "bias", with_mlm_head),
+             (c + "transform.LayerNorm.weight", (H,), "ln_w", with_mlm_head),
+             (c + "transform.LayerNorm.bias", (H,), "ln_b", with_mlm_head),
+             (c + "bias", (V,), "bias", with_mlm_head),
+             ("bert.pooler.dense.weight", (H, H), "mat", with_pooler),
+             ("bert.pooler.dense.bias", (H,), "bias", with_pooler),
+             ("linear.weight", (1, H), "mat", with_cls_linear),
+             ("linear.bias", (1,), "bias", with_cls_linear)]
+    for key, shp, kind, keep in heads:
+        yield key, shp, kind + ("" if keep else ":skip")
 
 
 def make_weights(shape: BertShape = BERT_BASE, seed: int = 1234, std: float = 0.05,
@@ -106,6 +107,8 @@ def make_weights(shape: BertShape = BERT_BASE, seed: int = 1234, std: float = 0.
     for key, shp, kind in mlm_keys(shape, with_mlm_head, with_cls_linear, with_pooler):
         n = int(np.prod(shp))
         z = rng.standard_normal(n, dtype=np.float32).reshape(shp)
+        if kind.endswith(":skip"):
+            continue
         if kind == "mat":
             z *= np.float32(std)
         elif kind in ("bias", "ln_b"):
