@@ -128,9 +128,27 @@ def main():
         dom = max(gemm_kinds, key=lambda k: gemm_kinds[k][0])
         ms, n, fl = gemm_kinds[dom]
         achieved = fl / (ms * 1e-3) / 1e12
+        # HBM(+MALL) bytes per launch from the committed rocprofv3 PMC summary (FETCH_SIZE x2
+        # gfx950 correction + WRITE_SIZE, per row), scaled to this run's rows per launch
+        traffic, tsrc = None, None
+        nk = {"qkv": (2304, 768, "qkv"), "oproj": (768, 768, "oproj/ffn2"), "ffn1": (3072, 768, "ffn1"),
+              "ffn2": (768, 3072, "oproj/ffn2")}.get(dom)
+        pmc_files = sorted(f for f in os.listdir(os.path.join(REPO, "profiles")) if f.endswith("_pmc_gemm_traffic.json"))
+        if nk and pmc_files:
+            pm = json.load(open(os.path.join(REPO, "profiles", pmc_files[-1])))
+            e = pm.get(nk[2], {})
+            if e.get("fetch_size_bytes_per_row") and e.get("write_size_bytes_per_row"):
+                rows_per_launch = fl / max(n, 1) / (2.0 * nk[0] * nk[1])
+                traffic = (e["fetch_size_bytes_per_row"] + e["write_size_bytes_per_row"]) * rows_per_launch
+                tsrc = f"profiles/{pmc_files[-1]}"
+        alg_bytes = None
+        if nk:
+            rows_per_launch = fl / max(n, 1) / (2.0 * nk[0] * nk[1])
+            alg_bytes = rows_per_launch * (nk[1] + nk[0]) * 2 + nk[0] * nk[1] * 2
         roof = {"kernel": f"gemm_f16_{dom}", "bound": "mfma", "achieved": round(achieved, 2),
                 "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP16_TFLOPS, 4),
-                "traffic": None, "launches": n, "avg_launch_ms": round(ms / max(n, 1), 4),
+                "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes": alg_bytes,
+                "launches": n, "avg_launch_ms": round(ms / max(n, 1), 4),
                 "flops_per_launch": fl / max(n, 1)}
 
     # ---- CPU baseline: oracle restatement of the reference work pattern ------------------
