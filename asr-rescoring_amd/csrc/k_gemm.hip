@@ -322,6 +322,8 @@ hipError_t launch_t(const f16* A, const f16* W, int M_pad, int N_pad, int K, con
 //   2: 128x128, 4 waves (2x2,  64x64 per wave), 2 stages ( 64 KiB LDS)
 //   3: 256x128, 8 waves (4x2,  64x64 per wave), 3 stages of BK=32 (72 KiB LDS: 2 blocks/CU)
 //   4: 256x256, 8 waves (2x4, 128x64 per wave), 3 stages of BK=32 (96 KiB LDS)
+//   5: 256x128, 4 waves (2x2, 128x64 per wave), 3 stages of BK=32 (72 KiB LDS: 2 blocks/CU)
+//   6: 256x128, 4 waves (2x2, 128x64 per wave), 2 stages of BK=32 (48 KiB LDS: 3 blocks/CU)
 int g_cfg = -1;
 
 int pick_cfg(int N_pad) {
@@ -343,6 +345,8 @@ hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
         case 1: return launch_t<256, 128, 4, 2, 3, 64, EPI>(A, W, M_pad, N_pad, K, ep, st);
         case 3: return launch_t<256, 128, 4, 2, 3, 32, EPI>(A, W, M_pad, N_pad, K, ep, st);
         case 4: return launch_t<256, 256, 2, 4, 3, 32, EPI>(A, W, M_pad, N_pad, K, ep, st);
+        case 5: return launch_t<256, 128, 2, 2, 3, 32, EPI>(A, W, M_pad, N_pad, K, ep, st);
+        case 6: return launch_t<256, 128, 2, 2, 2, 32, EPI>(A, W, M_pad, N_pad, K, ep, st);
         default: return launch_t<128, 128, 2, 2, 2, 64, EPI>(A, W, M_pad, N_pad, K, ep, st);
     }
 }
@@ -380,6 +384,9 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 0: e = launch_t<256, 256, 2, 4, 2, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
         case 1: e = launch_t<256, 128, 4, 2, 3, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
         case 3: e = launch_t<256, 128, 4, 2, 3, 32, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
+        case 5: e = launch_t<256, 128, 2, 2, 3, 32, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
+        case 6: e = launch_t<256, 128, 2, 2, 2, 32, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
+        case 4: e = launch_t<256, 256, 2, 4, 3, 32, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
         default: e = launch_t<128, 128, 2, 2, 2, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;   \
     }
     if (M % 256 || N % 256 || K % 64) return -1;
