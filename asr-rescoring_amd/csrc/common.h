@@ -34,6 +34,7 @@ struct EpiArgs {
     float* label_logit;    // [M]
     int kx;                // fp16 operand image width factor of the output (EPI_GELU_F16): 1 or 3
     int nlog;              // logical N (column offset of the image sections)
+    int group_m;           // tile order: row panels per group (set by launch_gemm)
 };
 
 // fp16 operand image of an fp32 activation row with logical width K:

@@ -78,7 +78,18 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     const int nwg = gridDim.x, bid = blockIdx.x;
     const int xcd = bid & 7, pos = bid >> 3, q = nwg >> 3, r = nwg & 7;
     const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
-    const int tm = wgid / n_tiles_n, tn = wgid - tm * n_tiles_n;
+    // grouped order: GM row panels x all column panels per group, column-major inside the
+    // group, so the tiles an XCD runs together share weight panels in its L2
+    int tm, tn;
+    {
+        const int GM = ep.group_m;
+        const int n_tiles_m = nwg / n_tiles_n;
+        const int per_group = GM * n_tiles_n;
+        const int g = wgid / per_group, loc = wgid - g * per_group;
+        const int gm = min(GM, n_tiles_m - g * GM);
+        tn = loc / gm;
+        tm = g * GM + (loc - tn * gm);
+    }
     const int m0 = tm * BM, n0 = tn * BN;
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -311,8 +322,11 @@ hipError_t launch_t(const f16* A, const f16* W, int M_pad, int N_pad, int K, con
     }
     const int ntn = N_pad / BN;
     const int grid = (M_pad / BM) * ntn;
+    static const int gm_env = getenv("RS_GEMM_GROUP_M") ? atoi(getenv("RS_GEMM_GROUP_M")) : 0;
+    EpiArgs e2 = ep;
+    e2.group_m = gm_env > 0 ? gm_env : (M_pad / BM);   // default: plain row-major tile order
     hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WM, WN, NSTAGE, BK, EPI, DBG>), dim3(grid), dim3(WM * WN * 64),
-                       smem, st, A, W, K, ntn, ep);
+                       smem, st, A, W, K, ntn, e2);
     return hipGetLastError();
 }
 
