@@ -27,6 +27,9 @@ def main():
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     shapes = [(2304, 768), (768, 768), (3072, 768), (768, 3072)]
+    if os.environ.get("SHAPES"):
+        shapes = [tuple(int(v) for v in x.split("x")) for x in os.environ["SHAPES"].split(",")]
+    dbgs = tuple(int(d) for d in os.environ.get("DBGS", "0,1,2,3").split(","))
     for N, K in shapes:
         A = (torch.rand(M, K, device=dev, generator=g) * 2 - 1).half()
         W = (torch.rand(N, K, device=dev, generator=g) * 2 - 1).half()
@@ -35,7 +38,7 @@ def main():
         ref = None
         for cfg in cfgs:
             res = []
-            for dbg in (0, 1, 2, 3):
+            for dbg in dbgs:
                 st = torch.cuda.current_stream().cuda_stream
                 call = lambda: fn(cfg, dbg, A.data_ptr(), W.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, st)  # noqa
                 for _ in range(3):
@@ -54,8 +57,9 @@ def main():
                         ref = (A[:4096].float() @ W.float().t() + b).half()
                     err = (out[:4096].float() - ref.float()).abs().max().item()
                     assert err < 0.05 * K ** 0.5, (cfg, err)
-            print(f"M={M} N={N} K={K} cfg={cfg}: full {res[0]:7.1f}  nostage {res[1]:7.1f}  "
-                  f"noepi {res[2]:7.1f}  neither {res[3]:7.1f} TF/s", flush=True)
+            names = {0: "full", 1: "nostage", 2: "noepi", 3: "neither"}
+            print(f"M={M} N={N} K={K} cfg={cfg}: " + "  ".join(f"{names[d]} {v:7.1f}" for d, v in zip(dbgs, res))
+                  + " TF/s", flush=True)
 
 
 if __name__ == "__main__":
