@@ -50,6 +50,27 @@ __device__ __forceinline__ float gelu_fast(float x) {
     return x >= 0.f ? 0.5f * x * (2.0f - y) : 0.5f * x * y;
 }
 
+// Packed GELU for the epilogues: two values per v_pk_* instruction.
+// erf(z) = 1 - (a1 t + .. + a5 t^5) exp(-z^2), t = 1/(1 + p z)  (Abramowitz-Stegun 7.1.26,
+// |error| <= 1.5e-7), z = |x|/sqrt2;  GELU(x) = 0.5 x (1 + sign(x) erf(z)).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu2(f32x2 x) {
+    const f32x2 z = __builtin_elementwise_abs(x) * 0.70710678118654752f;
+    const f32x2 den = __builtin_elementwise_fma(z, (f32x2)(0.3275911f), (f32x2)(1.0f));
+    const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+    f32x2 p = __builtin_elementwise_fma(t, (f32x2)(1.061405429f), (f32x2)(-1.453152027f));
+    p = __builtin_elementwise_fma(p, t, (f32x2)(1.421413741f));
+    p = __builtin_elementwise_fma(p, t, (f32x2)(-0.284496736f));
+    p = __builtin_elementwise_fma(p, t, (f32x2)(0.254829592f));
+    p = p * t;
+    const f32x2 a = z * z * (-1.4426950408889634f);          // -z^2 log2(e)
+    const f32x2 e = {__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)};
+    const f32x2 erfz = __builtin_elementwise_fma(-p, e, (f32x2)(1.0f));
+    const f32x2 s = {x.x < 0.f ? -0.5f : 0.5f, x.y < 0.f ? -0.5f : 0.5f};
+    const f32x2 hx = x * 0.5f;
+    return __builtin_elementwise_fma(s * erfz, x, hx);      // 0.5x + sign*0.5*erf*x
+}
+
 __device__ __forceinline__ void store4(f16* p, float4 v) {
     *(half4*)p = (half4){(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
 }
@@ -274,7 +295,11 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                     const size_t o = (size_t)row * ep.ldc + col;
                     if constexpr (EPI == EPI_GELU_F16 || EPI == EPI_GELU_F32) {
 #pragma unroll
-                        for (int e = 0; e < 8; ++e) x[e] = gelu_fast(x[e]);
+                        for (int e = 0; e < 8; e += 2) {
+                            const f32x2 gv = gelu2((f32x2){x[e], x[e + 1]});
+                            x[e] = gv.x;
+                            x[e + 1] = gv.y;
+                        }
                     }
                     if constexpr (EPI == EPI_BIAS_F16) {
                         half8 h;
