@@ -31,25 +31,6 @@ __device__ __forceinline__ int swz(int row, int chunk) {
     else return chunk ^ ((row >> 2) & 3);
 }
 
-// GELU(x) = 0.5 x erfc(-x/sqrt2); erfc by the Chebyshev fit of Numerical Recipes
-// (fractional error < 1.2e-7 everywhere): one exp + one rcp + 10 FMAs.
-__device__ __forceinline__ float gelu_fast(float x) {
-    const float z = fabsf(x) * 0.70710678118654752f;
-    const float t = __frcp_rn(1.0f + 0.5f * z);
-    float p = 0.17087277f;
-    p = fmaf(p, t, -0.82215223f);
-    p = fmaf(p, t, 1.48851587f);
-    p = fmaf(p, t, -1.13520398f);
-    p = fmaf(p, t, 0.27886807f);
-    p = fmaf(p, t, -0.18628806f);
-    p = fmaf(p, t, 0.09678418f);
-    p = fmaf(p, t, 0.37409196f);
-    p = fmaf(p, t, 1.00002368f);
-    p = fmaf(p, t, -1.26551223f);
-    const float y = t * __expf(p - z * z);          // erfc(|x|/sqrt2)
-    return x >= 0.f ? 0.5f * x * (2.0f - y) : 0.5f * x * y;
-}
-
 // Packed GELU for the epilogues: two values per v_pk_* instruction.
 // erf(z) = 1 - (a1 t + .. + a5 t^5) exp(-z^2), t = 1/(1 + p z)  (Abramowitz-Stegun 7.1.26,
 // |error| <= 1.5e-7), z = |x|/sqrt2;  GELU(x) = 0.5 x (1 + sign(x) erf(z)).
@@ -69,10 +50,6 @@ __device__ __forceinline__ f32x2 gelu2(f32x2 x) {
     const f32x2 s = {x.x < 0.f ? -0.5f : 0.5f, x.y < 0.f ? -0.5f : 0.5f};
     const f32x2 hx = x * 0.5f;
     return __builtin_elementwise_fma(s * erfz, x, hx);      // 0.5x + sign*0.5*erf*x
-}
-
-__device__ __forceinline__ void store4(f16* p, float4 v) {
-    *(half4*)p = (half4){(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
 }
 
 // DBG (timing experiments only, rs_debug_gemm): bit0 = no K-loop staging (MFMA + LDS
