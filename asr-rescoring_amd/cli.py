@@ -1,0 +1,259 @@
+"""Command-line drivers with the reference's entry points, YAML keys and output files.
+
+  python -m asr_rescoring_amd.cli mlm_pll     --config score.yaml    # MLM_PLL/main.py (task: scoring)
+  python -m asr_rescoring_amd.cli rescorebert --config MD_score.yaml # RescoreBert/main.py (task: scoring)
+  python -m asr_rescoring_amd.cli rescore     --config rescore.yaml  # rescore.py
+  python -m asr_rescoring_amd.cli rmbr        --config CER.yaml      # RMBR/main.py (utility: cer)
+
+Differences forced by the offline image (no model hub): ``model.bert`` cannot be fetched,
+so weights come from ``checkpoint_path`` (an HF-keyed state_dict, loaded with
+``torch.load(weights_only=True)`` or safetensors) or, for testing, from the seeded
+generator when ``random_init_seed`` is set.  The tokenizer is ``BertTokenizer``-like
+per-character for CJK (``data.CharTokenizer``) built from the data, unless ``model.vocab``
+names a ``vocab.txt``.  Extra keys: ``precision`` (fp16 / fp16x3), ``max_rows``,
+``mode`` (rescore fusion formula: norm / legacy / am_norm).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import sys
+from typing import Dict, List
+
+import numpy as np
+
+from . import data as D
+from .config import ArgParser, get
+from .weights import BERT_BASE, BertShape, load_state_dict_file, make_weights
+
+
+def _load(path):
+    return json.load(open(path, "r", encoding="utf-8"))
+
+
+def _weights(cfg, kind: str):
+    ck = get(cfg, "checkpoint_path")
+    if ck and os.path.exists(ck):
+        w = load_state_dict_file(ck)
+        if kind == "cls":    # RescoreBert state_dict: bert.* + linear.*
+            return w
+        return w
+    seed = get(cfg, "random_init_seed")
+    if seed is None:
+        raise FileNotFoundError(f"checkpoint_path {ck!r} not found (set random_init_seed to score with "
+                                "seeded random weights)")
+    return make_weights(BERT_BASE, seed=int(seed), with_cls_linear=(kind == "cls"), with_pooler=(kind == "cls"))
+
+
+class VocabTokenizer(D.CharTokenizer):
+    """BertTokenizer-compatible ids from a vocab.txt (one token per line, id = line index);
+    CJK text is split per character as BertTokenizer does."""
+
+    def __init__(self, vocab_path: str):
+        self.vocab = {l.rstrip("\n"): i for i, l in enumerate(open(vocab_path, encoding="utf-8"))}
+
+    def convert_tokens_to_ids(self, toks):
+        unk = self.vocab.get("[UNK]", D.UNK_ID)
+        return [self.vocab.get(t, unk) for t in toks]
+
+
+def _tokenizer(cfg, texts: List[str]):
+    v = get(cfg, "model.vocab")
+    if v and os.path.exists(v):
+        return VocabTokenizer(v)
+    chars = sorted({c for t in texts for c in t})
+    return D.CharTokenizer(chars)
+
+
+def _nbest_tokens(hyps_text: Dict[str, Dict[str, str]], tok, max_utt=1 << 30, n_best=1 << 30):
+    words, keys = [], []
+    for u, (uid, hyps) in enumerate(hyps_text.items()):
+        if u == max_utt:
+            break
+        row = []
+        for k, (hid, text) in enumerate(hyps.items()):
+            if k == n_best:
+                break
+            row.append(tok.encode_words(text))
+            keys.append((uid, hid))
+        words.append(row)
+    return D.from_lists(words), keys
+
+
+# --------------------------------------------------------------------------------------
+def mlm_pll(cfg) -> Dict[str, str]:
+    """MLM_PLL/main.py:164-203 (pll_bert_scoring).  Accepts the reference's preprocessed
+    rows (``*_data_path``: do_job output) or raw ``*_hyps_text_path`` JSON."""
+    from .scorer import PLLScorer
+    scorer = PLLScorer(_weights(cfg, "mlm"), BERT_BASE, device=_dev(cfg), max_rows=get(cfg, "max_rows", 65536),
+                       precision=get(cfg, "precision", "fp16"))
+    out_files = {}
+    for split in ("train", "dev", "test"):
+        rows_path = get(cfg, f"{split}_data_path")
+        text_path = get(cfg, f"{split}_hyps_text_path")
+        if rows_path and os.path.exists(rows_path):
+            rows = _load(rows_path)[:get(cfg, "num_of_data", 1 << 62)]
+            output_score: Dict[str, Dict[str, float]] = {}
+            for r in rows:                                   # MLM_PLL/main.py:189-193
+                if r["hyp_id"] == "hyp_1":
+                    output_score[r["utt_id"]] = {}
+                output_score[r["utt_id"]][r["hyp_id"]] = 0
+            output_score = scorer.run_one_epoch(rows, output_score)
+        elif text_path and os.path.exists(text_path):
+            hyps = _load(text_path)
+            tok = _tokenizer(cfg, [t for h in hyps.values() for t in h.values()])
+            nb, keys = _nbest_tokens(hyps, tok)
+            pll = scorer.score(nb)
+            output_score = {}
+            for (u, h), s in zip(keys, pll):
+                output_score.setdefault(u, {})[h] = float(s)
+        else:
+            continue
+        path = cfg.output_path + f"{split}_lm.json"          # MLM_PLL/main.py:203 naming
+        D.json_saving(path, output_score)
+        out_files[split] = path
+    scorer.close()
+    return out_files
+
+
+def rescorebert(cfg) -> Dict[str, str]:
+    """RescoreBert/main.py:232-285 (score): dev/test hyps -> CLS scores -> dev_lm/test_lm.json."""
+    from .scorer import RescoreBertScorer
+    sc = RescoreBertScorer(_weights(cfg, "cls"), BERT_BASE, device=_dev(cfg), max_rows=get(cfg, "max_rows", 65536),
+                           precision=get(cfg, "precision", "fp16x3"))
+    out_files = {}
+    for split in ("dev", "test"):
+        feats = get(cfg, f"{split}_feature", [])
+        paths = get(cfg, f"{split}_feature_path", [])
+        fmt = get(cfg, f"{split}_output_format")
+        if "hyps_token_ids" not in feats or not fmt or not os.path.exists(fmt):
+            continue
+        hyps = _load(paths[feats.index("hyps_token_ids")])
+        tok = _tokenizer(cfg, [t for h in hyps.values() for t in h.values()])
+        max_utt, n_best = get(cfg, "max_utt", 1 << 30), get(cfg, "n_best", 1 << 30)
+        nb, keys = _nbest_tokens(hyps, tok, max_utt, n_best)
+        scores = sc.score(nb)
+        out = D.get_output_format(fmt, max_utt, n_best)      # util/get_output_format.py:4-16
+        for (u, h), s in zip(keys, scores):
+            out[u][h] = float(s)
+        path = os.path.join(cfg.output_path, f"{split}_lm.json")
+        D.json_saving(path, out)
+        out_files[split] = path
+    sc.close()
+    return out_files
+
+
+def rescore(cfg) -> Dict[str, float]:
+    """rescore.py:61-120: best weight on dev, CER on test, logged to output_path/rescore.log."""
+    from . import rerank
+    os.makedirs(cfg.output_path, exist_ok=True)
+    log = _logger(os.path.join(cfg.output_path, "rescore.log"))
+    log.info(str(cfg))
+    mode = get(cfg, "mode", "norm")
+    n_best = cfg.n_best
+
+    def split_nb(prefix):
+        hyps = _load(getattr(cfg, f"{prefix}_hyps_text_path"))
+        refs = _load(getattr(cfg, f"{prefix}_ref_text_path"))
+        am = _load(getattr(cfg, f"{prefix}_am_path"))
+        lm_j = _load(getattr(cfg, f"{prefix}_lm_path"))
+        nb = D.from_texts(hyps, refs, am, n_best=n_best)
+        lm = np.asarray([lm_j[u][h] for u in nb.utt_ids for h in list(lm_j[u])[:n_best]], np.float64)
+        return nb, lm
+
+    dev_nb, dev_lm = split_nb("dev")
+    best_w, best_cer, _, _ = rerank.find_best_weight(dev_nb, dev_lm, n_best=n_best, mode=mode, device=_dev(cfg))
+    log.info("best_weight: " + str(best_w))
+    log.info("dev cer: " + str(best_cer))
+    print("best_weight: ", best_w)
+    print("dev cer: ", best_cer)
+    test_nb, test_lm = split_nb("test")
+    import torch
+    arg = rerank.fuse_rerank(test_nb.am, test_lm, test_nb.hyp_len(), test_nb.utt_off, [best_w], mode, n_best,
+                             device=_dev(cfg))
+    ed = rerank.ref_edits(test_nb, device=_dev(cfg))
+    edits = rerank.corpus_edits(ed, test_nb.utt_off, arg).cpu().numpy()[0]
+    test_cer = float(edits) / sum(len(r) for r in test_nb.refs)
+    log.info("test cer: " + str(test_cer))
+    print("test cer: ", test_cer)
+    _ = torch
+    return {"best_weight": best_w, "dev_cer": best_cer, "test_cer": test_cer}
+
+
+def rmbr(cfg) -> Dict[str, float]:
+    """RMBR/main.py:38-108 with utility_function: cer."""
+    from . import rerank
+    if get(cfg, "utility_function", "cer") != "cer":
+        raise NotImplementedError("only the CER utility runs offline (bert_score is not available)")
+    os.makedirs(cfg.output_path, exist_ok=True)
+    log = _logger(os.path.join(cfg.output_path, "mbr.log"))
+    n_best, max_utt = cfg.n_best, get(cfg, "max_utt", 1 << 30)
+
+    def split_nb(prefix):
+        feats, paths = getattr(cfg, f"{prefix}_feature"), getattr(cfg, f"{prefix}_feature_path")
+        refs = _load(paths[feats.index("ref_text")])
+        hyps = _load(paths[feats.index("hyps_text")])
+        return D.from_texts(hyps, refs, None, n_best=n_best, max_utt=max_utt)
+
+    dev = split_nb("dev")
+    log.info("Running MBR on dev set to find best length ...")
+    best_cer, best_len, best_sc = rerank.find_best_length(dev, n_best, device=_dev(cfg))
+    log.info(f"best_cer: {best_cer}")
+    log.info(f"best_length: {best_len}")
+    print("best_cer: ", best_cer)
+    print("best_length: ", best_len)
+    res = {"best_cer": best_cer, "best_length": best_len}
+    for split, nb, sc in (("dev", dev, best_sc), ("test", None, None)):
+        if split == "test":
+            nb = split_nb("test")
+            log.info("Running MBR on test set ...")
+            idx, sc = rerank.mbr_decode(nb, best_len, device=_dev(cfg))
+            import torch
+            ed = rerank.ref_edits(nb, device=_dev(cfg))
+            arg = torch.from_numpy(idx.astype(np.int32)).to(ed.device)[None, :]
+            test_cer = float(rerank.corpus_edits(ed, nb.utt_off, arg).cpu()[0]) / sum(len(r) for r in nb.refs)
+            log.info(f"test cer: {test_cer}")
+            print("test cer: ", test_cer)
+            res["test_cer"] = test_cer
+        fmt = getattr(cfg, f"{split}_output_format")
+        out = D.get_output_format(fmt, max_utt, n_best)
+        for (uid, hyps), row in zip(out.items(), sc.tolist()):   # RMBR/main.py:80-89
+            for (hid, _), v in zip(hyps.items(), row):
+                out[uid][hid] = v
+        D.json_saving(os.path.join(cfg.output_path, f"{split}_MBR.json"), out)
+    return res
+
+
+def _dev(cfg) -> int:
+    d = str(get(cfg, "device", "cuda:0"))
+    return int(d.split(":")[1]) if ":" in d else 0
+
+
+def _logger(path):
+    log = logging.getLogger("asr_rescoring_amd." + os.path.basename(path))
+    log.setLevel(logging.INFO)
+    h = logging.FileHandler(path, mode="w")
+    h.setFormatter(logging.Formatter("%(asctime)s,%(msecs)d %(name)s %(levelname)s %(message)s", "%H:%M:%S"))
+    log.handlers = [h]
+    return log
+
+
+COMMANDS = {"mlm_pll": mlm_pll, "rescorebert": rescorebert, "rescore": rescore, "rmbr": rmbr}
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    if not argv or argv[0] not in COMMANDS:
+        print("usage: python -m asr_rescoring_amd.cli {" + ",".join(COMMANDS) + "} --config <yaml>")
+        return 2
+    cfg = ArgParser().parse(argv[1:])
+    COMMANDS[argv[0]](cfg)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
+
+
+_ = BertShape

@@ -33,6 +33,7 @@ class NBest:
     refs: List[np.ndarray]      # per utterance int32 reference ids (no CLS/SEP)
     utt_ids: List[str]
     hyp_ids: List[str]
+    lens: Optional[np.ndarray] = None   # per-hypothesis len(text) when built from text
 
     @property
     def n_hyp(self) -> int:
@@ -44,6 +45,8 @@ class NBest:
 
     def hyp_len(self) -> np.ndarray:
         """Length in words/characters (T - 2); ``rescore.py:28-35`` uses ``len(hyp)``."""
+        if self.lens is not None:
+            return np.asarray(self.lens, np.int32)
         return (np.diff(self.hyp_off) - 2).astype(np.int32)
 
     def hyp_words(self, h: int) -> np.ndarray:
@@ -88,6 +91,29 @@ def from_lists(hyps: List[List[Sequence[int]]], am: Optional[List[List[float]]] 
          [np.asarray(h[0], np.int32) for h in hyps]
     return NBest(np.asarray(toks, np.int32), np.asarray(hoff, np.int32),
                  np.asarray(uoff, np.int32), np.asarray(amv, np.float64), rf, uids, hyp_ids)
+
+
+def from_texts(hyps_text: Dict[str, Dict[str, str]], ref_text: Optional[Dict[str, str]] = None,
+               am: Optional[Dict[str, Dict[str, float]]] = None, n_best: int = 1 << 30,
+               max_utt: int = 1 << 30) -> NBest:
+    """N-best of raw strings for the CER side (jiwer semantics): symbols are the characters
+    of ``text.strip()`` (Unicode code points), ``lens`` keeps ``len(text)`` as
+    ``rescore.py:28-35`` computes it.  JSON key order defines utterance / hypothesis order
+    (``rescore.py:13-23`` relies on it too)."""
+    words, ams, refs, uids, lens = [], [], [], [], []
+    for u, (uid, hyps) in enumerate(hyps_text.items()):
+        if u == max_utt:
+            break
+        items = list(hyps.items())[:n_best]
+        words.append([[ord(c) for c in t.strip()] for _, t in items])
+        lens.extend(len(t) for _, t in items)
+        ams.append([float(am[uid][h]) for h, _ in items] if am is not None else [0.0] * len(items))
+        refs.append([ord(c) for c in ref_text[uid].strip()] if ref_text is not None else [])
+        uids.append(uid)
+    nb = from_lists(words, ams, refs, uids)
+    nb.hyp_ids = [h for uid in uids for h in list(hyps_text[uid])[:n_best]]
+    nb.lens = np.asarray(lens, np.int32)
+    return nb
 
 
 def _edit(rng: np.random.Generator, base: List[int], k: int, vocab: int) -> List[int]:

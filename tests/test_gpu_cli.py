@@ -1,0 +1,69 @@
+"""End-to-end C1 plumbing through the CLI drivers (reference entry points) on the GPU:
+hyps_text -> mlm_pll (PLL JSON) -> rescore (best weight, dev/test CER) -> rmbr (CER utility)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import yaml
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def c1(golden_dir, tmp_path_factory):
+    g = json.load(open(os.path.join(golden_dir, "c1_plumbing.json"), encoding="utf-8"))
+    d = tmp_path_factory.mktemp("c1")
+    for name in ("hyps_text", "ref_text", "hyps_score"):
+        json.dump(g[name], open(d / f"{name}.json", "w", encoding="utf-8"), ensure_ascii=False)
+    # vocab.txt reproducing the fixture's char ids (106 + index in the sorted charset)
+    special = {0: "[PAD]", 100: "[UNK]", 101: "[CLS]", 102: "[SEP]", 103: "[MASK]"}
+    lines = [special.get(i, f"[unused{i}]") for i in range(106)] + list(g["charset"])
+    (d / "vocab.txt").write_text("\n".join(lines) + "\n", encoding="utf-8")
+    return g, d
+
+
+def _cfg(d, name, obj):
+    p = d / name
+    p.write_text(yaml.safe_dump(obj, allow_unicode=True), encoding="utf-8")
+    return str(p)
+
+
+def test_cli_c1_pipeline(c1):
+    from asr_rescoring_amd import cli
+    g, d = c1
+    out = str(d) + "/"
+    assert cli.main(["mlm_pll", "--config", _cfg(d, "score.yaml", {
+        "task": "scoring", "seed": 10, "device": "cuda:0", "random_init_seed": 1234,
+        "train_hyps_text_path": str(d / "hyps_text.json"), "output_path": out,
+        "model": {"bert": "bert-base-chinese", "vocab": str(d / "vocab.txt")}})]) == 0
+    lm = json.load(open(out + "train_lm.json", encoding="utf-8"))
+    assert list(lm) == g["utt_ids"]
+    got = np.array([v for u in lm for v in lm[u].values()])
+    ref = np.array([v for u in g["lm"] for v in g["lm"][u].values()])
+    assert (np.abs(got - ref) / np.abs(ref)).max() < 1e-3
+
+    paths = {f"{s}_{k}_path": str(d / f) for s in ("dev", "test")
+             for k, f in (("am", "hyps_score.json"), ("hyps_text", "hyps_text.json"), ("ref_text", "ref_text.json"))}
+    paths.update({"dev_lm_path": out + "train_lm.json", "test_lm_path": out + "train_lm.json"})
+    res = cli.rescore(cli.ArgParser().parse(["--config", _cfg(d, "rescore.yaml", {
+        **paths, "n_best": 10, "output_path": str(d / "rescore_out")})]))
+    assert res["best_weight"] == g["best_weight"] and res["dev_cer"] == g["best_cer"]
+    log = (d / "rescore_out" / "rescore.log").read_text()
+    assert "best_weight: " in log and "dev cer: " in log and "test cer: " in log
+
+    res2 = cli.rmbr(cli.ArgParser().parse(["--config", _cfg(d, "CER.yaml", {
+        "device": "cuda:0", "utility_function": "cer",
+        "dev_feature": ["ref_text", "hyps_text"], "test_feature": ["ref_text", "hyps_text"],
+        "dev_feature_path": [str(d / "ref_text.json"), str(d / "hyps_text.json")],
+        "test_feature_path": [str(d / "ref_text.json"), str(d / "hyps_text.json")],
+        "dev_output_format": str(d / "hyps_score.json"), "test_output_format": str(d / "hyps_score.json"),
+        "output_path": str(d / "mbr_out"), "max_utt": 99999999, "n_best": 10})]))
+    # oracle restatement of RMBR on the same texts
+    from oracle import rescore_ref as R
+    hyps = [[[ord(c) for c in t.strip()] for t in g["hyps_text"][u].values()] for u in g["utt_ids"]]
+    refs = [[ord(c) for c in g["ref_text"][u].strip()] for u in g["utt_ids"]]
+    bc, bl, _ = R.find_best_length(10, refs, hyps)
+    assert res2["best_length"] == bl and res2["best_cer"] == bc
+    mbr = json.load(open(d / "mbr_out" / "test_MBR.json", encoding="utf-8"))
+    assert list(mbr) == g["utt_ids"]
