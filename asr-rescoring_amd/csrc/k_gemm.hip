@@ -135,11 +135,11 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     int buf = 0;
     for (int kt = 0; kt < nk; ++kt) {
         // tile kt landed for this wave: all later-issued stages may stay in flight
-        if (kt + NSTAGE - 2 < nk) {
-            if constexpr (NSTAGE == 3) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+        {
+            const int ahead = min(NSTAGE - 2, nk - 1 - kt);   // stages issued after tile kt
+            if (NSTAGE >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+            else if (NSTAGE >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         // every wave's part of tile kt landed; every wave finished reading tile kt-1
         asm volatile("s_barrier" ::: "memory");
@@ -349,7 +349,7 @@ int pick_cfg(int N_pad) {
     }
     int c = g_cfg;
     if (c == 100) c = (N_pad % 256 == 0) ? 0 : 1;
-    if ((c == 0 || c == 4) && N_pad % 256) c = 1;
+    if ((c == 0 || c == 4 || c == 7) && N_pad % 256) c = 1;
     return c;
 }
 
@@ -363,6 +363,7 @@ hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
         case 4: return launch_t<256, 256, 2, 4, 3, 32, EPI>(A, W, M_pad, N_pad, K, ep, st);
         case 5: return launch_t<256, 128, 2, 2, 3, 32, EPI>(A, W, M_pad, N_pad, K, ep, st);
         case 6: return launch_t<256, 128, 2, 2, 2, 32, EPI>(A, W, M_pad, N_pad, K, ep, st);
+        case 7: return launch_t<256, 256, 2, 4, 4, 32, EPI>(A, W, M_pad, N_pad, K, ep, st);
         default: return launch_t<128, 128, 2, 2, 2, 64, EPI>(A, W, M_pad, N_pad, K, ep, st);
     }
 }
@@ -403,6 +404,7 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 5: e = launch_t<256, 128, 2, 2, 3, 32, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
         case 6: e = launch_t<256, 128, 2, 2, 2, 32, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
         case 4: e = launch_t<256, 256, 2, 4, 3, 32, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
+        case 7: e = launch_t<256, 256, 2, 4, 4, 32, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
         default: e = launch_t<128, 128, 2, 2, 2, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;   \
     }
     if (M % 256 || N % 256 || K % 64) return -1;
