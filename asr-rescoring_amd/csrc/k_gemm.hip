@@ -143,11 +143,27 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         }
         // every wave's part of tile kt landed; every wave finished reading tile kt-1
         asm volatile("s_barrier" ::: "memory");
-        if (!(DBG & 1) && kt + NSTAGE - 1 < nk) {
-            int nb = buf + NSTAGE - 1;
-            if (nb >= NSTAGE) nb -= NSTAGE;
-            stage(nb, (kt + NSTAGE - 1) * BK);
+        const bool do_stage = !(DBG & 1) && kt + NSTAGE - 1 < nk;
+        int nb = buf + NSTAGE - 1;
+        if (nb >= NSTAGE) nb -= NSTAGE;
+        const int knext = (kt + NSTAGE - 1) * BK;
+        if constexpr (!(DBG & 4)) {
+            if (do_stage) stage(nb, knext);
         }
+        // DBG&4: the next stage's LDS-DMA pieces are spread over the MFMA clusters
+        auto stage_part = [&](int q) {
+            if constexpr (DBG & 4) {
+                __builtin_amdgcn_sched_barrier(0);
+                if (do_stage) {
+#pragma unroll
+                    for (int p = q * (PPW / 4); p < (q + 1) * (PPW / 4); ++p)
+                        __builtin_amdgcn_global_load_lds(
+                            (const void*)(src[p] + knext),
+                            (__attribute__((address_space(3))) void*)(smem + nb * STAGE + ldsoff[p]), 16, 0, 0);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        };
         const char* sA = smem + buf * STAGE;
         const char* sB = sA + A_BYTES;
         // fragments of k-substep s+1 are read while the MFMAs of substep s issue
@@ -175,13 +191,17 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         load_frags(0, af0, bf0);
         load_frags(1, af1, bf1);
         mfmas(af0, bf0);
+        stage_part(0);
         if constexpr (BK == 64) {
             load_frags(2, af0, bf0);
             mfmas(af1, bf1);
+            stage_part(1);
             load_frags(3, af1, bf1);
             mfmas(af0, bf0);
+            stage_part(2);
         }
         mfmas(af1, bf1);
+        stage_part(3);
         buf = buf + 1 == NSTAGE ? 0 : buf + 1;
     }
 
@@ -410,6 +430,8 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
     if (M % 256 || N % 256 || K % 64) return -1;
     switch (dbg) {
         case 0: RS_DBG(0); break;
+        case 4: RS_DBG(4); break;
+        case 6: RS_DBG(6); break;
         case 1: RS_DBG(1); break;
         case 2: RS_DBG(2); break;
         default: RS_DBG(3); break;
