@@ -151,12 +151,14 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             if (do_stage) stage(nb, knext);
         }
         // DBG&4: the next stage's LDS-DMA pieces are spread over the MFMA clusters
+        constexpr int NSUB = BK / 16;          // k-substeps per stage
+        static_assert(PPW % NSUB == 0, "pieces per substep");
         auto stage_part = [&](int q) {
             if constexpr (DBG & 4) {
                 __builtin_amdgcn_sched_barrier(0);
                 if (do_stage) {
 #pragma unroll
-                    for (int p = q * (PPW / 4); p < (q + 1) * (PPW / 4); ++p)
+                    for (int p = q * (PPW / NSUB); p < (q + 1) * (PPW / NSUB); ++p)
                         __builtin_amdgcn_global_load_lds(
                             (const void*)(src[p] + knext),
                             (__attribute__((address_space(3))) void*)(smem + nb * STAGE + ldsoff[p]), 16, 0, 0);
@@ -201,7 +203,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             stage_part(2);
         }
         mfmas(af1, bf1);
-        stage_part(3);
+        stage_part(NSUB - 1);
         buf = buf + 1 == NSTAGE ? 0 : buf + 1;
     }
 
