@@ -152,13 +152,12 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         }
         // DBG&4: the next stage's LDS-DMA pieces are spread over the MFMA clusters
         constexpr int NSUB = BK / 16;          // k-substeps per stage
-        static_assert(PPW % NSUB == 0, "pieces per substep");
         auto stage_part = [&](int q) {
             if constexpr (DBG & 4) {
                 __builtin_amdgcn_sched_barrier(0);
                 if (do_stage) {
 #pragma unroll
-                    for (int p = q * (PPW / NSUB); p < (q + 1) * (PPW / NSUB); ++p)
+                    for (int p = (q * PPW) / NSUB; p < ((q + 1) * PPW) / NSUB; ++p)
                         __builtin_amdgcn_global_load_lds(
                             (const void*)(src[p] + knext),
                             (__attribute__((address_space(3))) void*)(smem + nb * STAGE + ldsoff[p]), 16, 0, 0);
