@@ -120,11 +120,33 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         }
     };
 
+    // Accumulators start at bias (+ residual): these loads' latency hides behind the whole
+    // K loop and the epilogue only converts / activates / stores.
+    //   acc[i][j][4g + e] <-> C[m0 + wm*WTM + 32i + (lane&31)][n0 + wn*WTN + 32j + 8g + 4(lane>>5) + e]
     f32x16 acc[TM][TN];
+    {
+        const int arow = m0 + wm * WTM + (lane & 31);
+        const int acol = n0 + wn * WTN + 4 * (lane >> 5);
 #pragma unroll
-    for (int i = 0; i < TM; ++i)
+        for (int j = 0; j < TN; ++j)
 #pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16){};
+            for (int g = 0; g < 4; ++g) {
+                const float4 b4 = (DBG & 2) ? make_float4(0.f, 0.f, 0.f, 0.f)
+                                            : *(const float4*)(ep.bias + acol + 32 * j + 8 * g);
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+                    float4 v = b4;
+                    if constexpr (EPI == EPI_RES_F32 && !(DBG & 2)) {
+                        const float4 r4 = *(const float4*)(ep.res + (size_t)(arow + 32 * i) * ep.ldc + acol + 32 * j + 8 * g);
+                        v = make_float4(v.x + r4.x, v.y + r4.y, v.z + r4.z, v.w + r4.w);
+                    }
+                    acc[i][j][4 * g] = v.x;
+                    acc[i][j][4 * g + 1] = v.y;
+                    acc[i][j][4 * g + 2] = v.z;
+                    acc[i][j][4 * g + 3] = v.w;
+                }
+            }
+    }
 
     const int nk = K / BK;
 #pragma unroll
@@ -235,11 +257,10 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     const int col = cbase + j * 32 + 8 * g;
-                    const float4 b4 = *(const float4*)(ep.bias + col);
-                    const float bb[4] = {b4.x, b4.y, b4.z, b4.w};
+
 #pragma unroll
                     for (int e = 0; e < 4; ++e) {
-                        const float x = col + e < ep.n_valid ? acc[i][j][4 * g + e] + bb[e] : -INFINITY;
+                        const float x = col + e < ep.n_valid ? acc[i][j][4 * g + e] : -INFINITY;
                         v[j][4 * g + e] = x;
                         mx = fmaxf(mx, x);
                         if (col + e == lab) ep.label_logit[row] = x;
@@ -267,12 +288,6 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         float* lw = (float*)smem + wave * 32 * LDW;
         const int rr0 = lane >> 3, cc = (lane & 7) * 8;
         const int col = n0 + wn * WTN + cc;
-        float bias[8];
-        {
-            const float4 b0 = *(const float4*)(ep.bias + col), b1 = *(const float4*)(ep.bias + col + 4);
-            bias[0] = b0.x; bias[1] = b0.y; bias[2] = b0.z; bias[3] = b0.w;
-            bias[4] = b1.x; bias[5] = b1.y; bias[6] = b1.z; bias[7] = b1.w;
-        }
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -287,8 +302,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 const int row = m0 + wm * WTM + i * 32 + rr;
                 const float4 u0 = *(const float4*)(lw + rr * LDW + cc);
                 const float4 u1 = *(const float4*)(lw + rr * LDW + cc + 4);
-                float x[8] = {u0.x + bias[0], u0.y + bias[1], u0.z + bias[2], u0.w + bias[3],
-                              u1.x + bias[4], u1.y + bias[5], u1.z + bias[6], u1.w + bias[7]};
+                float x[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
                 if (row < ep.m_valid) {
                     const size_t o = (size_t)row * ep.ldc + col;
                     if constexpr (EPI == EPI_GELU_F16 || EPI == EPI_GELU_F32) {
@@ -317,11 +331,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                             *(half8*)(orow + ep.nlog + col) = h;
                             *(half8*)(orow + 2 * ep.nlog + col) = l;
                         }
-                    } else if constexpr (EPI == EPI_RES_F32) {
-                        const float4 r0 = *(const float4*)(ep.res + o), r1 = *(const float4*)(ep.res + o + 4);
-                        *(float4*)((float*)ep.out + o) = make_float4(x[0] + r0.x, x[1] + r0.y, x[2] + r0.z, x[3] + r0.w);
-                        *(float4*)((float*)ep.out + o + 4) = make_float4(x[4] + r1.x, x[5] + r1.y, x[6] + r1.z, x[7] + r1.w);
-                    } else {  // EPI_BIAS_F32, EPI_GELU_F32
+                    } else {  // EPI_BIAS_F32, EPI_GELU_F32, EPI_RES_F32 (residual already in acc)
                         *(float4*)((float*)ep.out + o) = make_float4(x[0], x[1], x[2], x[3]);
                         *(float4*)((float*)ep.out + o + 4) = make_float4(x[4], x[5], x[6], x[7]);
                     }
