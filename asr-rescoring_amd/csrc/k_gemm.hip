@@ -304,7 +304,8 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 const float4 u1 = *(const float4*)(lw + rr * LDW + cc + 4);
                 float x[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
                 if (row < ep.m_valid) {
-                    const size_t o = (size_t)row * ep.ldc + col;
+                    // DBG&8 (diagnostic): every tile stores into rows 0..255 (L2-resident)
+                    const size_t o = (size_t)((DBG & 8) ? (row & 255) : row) * ep.ldc + col;
                     if constexpr (EPI == EPI_GELU_F16 || EPI == EPI_GELU_F32) {
 #pragma unroll
                         for (int e = 0; e < 8; e += 2) {
@@ -443,6 +444,7 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 0: RS_DBG(0); break;
         case 4: RS_DBG(4); break;
         case 6: RS_DBG(6); break;
+        case 8: RS_DBG(8); break;
         case 1: RS_DBG(1); break;
         case 2: RS_DBG(2); break;
         default: RS_DBG(3); break;
