@@ -215,7 +215,7 @@ attn_full_kernel(const QT* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H
 //                        (k-step s of key tile kt = registers 8s..8s+7, key order
 //                        16s + 8(j>>2) + 4h + (j&3)); V^T comes from LDS, written
 //                        transposed once per key block.
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(64, 4)
 attn_mfma_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
                  f16* __restrict__ ctx, int kx) {
     constexpr int VTS = 72;                       // V^T row stride (halfs): 64 keys + pad
@@ -250,67 +250,54 @@ attn_mfma_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int 
                     for (int e = 0; e < 8; ++e) sVT[(d0 + e) * VTS + kr] = v[e];
                 }
             }
-            // ---- X = K . Q^T  (two key tiles)
-            f32x16 x[2];
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt) {
+            if (!one_block || q0 == 0) __syncthreads();   // sVT written by every lane
+            // ---- one 32-key tile at a time: X = K . Q^T, online softmax, O^T += V^T . P^T
+            for (int kt = 0; kt < 2 && k0 + kt * 32 < T; ++kt) {
                 const int key = k0 + kt * 32 + r;
-                f32x16 a = {};
+                f32x16 x = {};
 #pragma unroll
                 for (int ks = 0; ks < 4; ++ks) {
                     const half8 kf = key < T ? *(const half8*)(base + (size_t)key * ld + H + ks * 16 + hf * 8) : (half8){};
-                    a = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[ks], a, 0, 0, 0);
+                    x = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[ks], x, 0, 0, 0);
                 }
-                x[kt] = a;
-            }
-            // ---- online softmax over keys (registers + the other half-wave)
-            float bm = -INFINITY;
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt)
+                float bm = -INFINITY;
 #pragma unroll
                 for (int j = 0; j < 16; ++j) {
-                    const int key = k0 + kt * 32 + (j & 3) + 8 * (j >> 2) + 4 * hf;
-                    const float v = key < T ? x[kt][j] * scale : -INFINITY;
-                    x[kt][j] = v;
+                    const int kj = k0 + kt * 32 + (j & 3) + 8 * (j >> 2) + 4 * hf;
+                    const float v = kj < T ? x[j] * scale : -INFINITY;
+                    x[j] = v;
                     bm = fmaxf(bm, v);
                 }
-            bm = fmaxf(bm, __shfl_xor(bm, 32));
-            const float mn = fmaxf(m, bm);
-            const float alpha = __expf(m - mn);
-            half8 pf[2][2];                       // [kt][k-step]
-            float ls = 0.f;
-#pragma unroll
-            for (int kt = 0; kt < 2; ++kt)
+                bm = fmaxf(bm, __shfl_xor(bm, 32));
+                const float mn = fmaxf(m, bm);
+                const float alpha = __expf(m - mn);
+                half8 pf[2];                          // k-steps of this key tile
+                float ls = 0.f;
 #pragma unroll
                 for (int sk = 0; sk < 2; ++sk)
 #pragma unroll
                     for (int e = 0; e < 8; ++e) {
-                        const f16 ph = (f16)__expf(x[kt][sk * 8 + e] - mn);
-                        pf[kt][sk][e] = ph;
+                        const f16 ph = (f16)__expf(x[sk * 8 + e] - mn);
+                        pf[sk][e] = ph;
                         ls += (float)ph;
                     }
-            ls += __shfl_xor(ls, 32);
-            l = l * alpha + ls;
-            m = mn;
+                ls += __shfl_xor(ls, 32);
+                l = l * alpha + ls;
+                m = mn;
 #pragma unroll
-            for (int dt = 0; dt < 2; ++dt)
+                for (int dt = 0; dt < 2; ++dt) {
 #pragma unroll
-                for (int j = 0; j < 16; ++j) o[dt][j] *= alpha;
-            if (!one_block || q0 == 0) __syncthreads();   // sVT written by every lane
-            // ---- O^T += V^T . P^T
-#pragma unroll
-            for (int dt = 0; dt < 2; ++dt) {
-                const int d = dt * 32 + r;
-#pragma unroll
-                for (int kt = 0; kt < 2; ++kt)
+                    for (int j = 0; j < 16; ++j) o[dt][j] *= alpha;
+                    const int d = dt * 32 + r;
 #pragma unroll
                     for (int sk = 0; sk < 2; ++sk) {
                         const int kb = kt * 32 + sk * 16 + 4 * hf;
                         const half4 lo = *(const half4*)(sVT + d * VTS + kb);
                         const half4 hi = *(const half4*)(sVT + d * VTS + kb + 8);
                         const half8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf[kt][sk], o[dt], 0, 0, 0);
+                        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf[sk], o[dt], 0, 0, 0);
                     }
+                }
             }
         }
         // ---- store: lane = query, registers = dims (j&3) + 8(j>>2) + 4h of d tile dt
