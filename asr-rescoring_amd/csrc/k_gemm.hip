@@ -303,6 +303,10 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 const float4 u0 = *(const float4*)(lw + rr * LDW + cc);
                 const float4 u1 = *(const float4*)(lw + rr * LDW + cc + 4);
                 float x[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
+                if constexpr (DBG & 16) {       // diagnostic: LDS pass + conversion, no store
+                    asm volatile("" ::"v"(x[0]), "v"(x[3]), "v"(x[7]));
+                    continue;
+                }
                 if (row < ep.m_valid) {
                     // DBG&8 (diagnostic): every tile stores into rows 0..255 (L2-resident)
                     const size_t o = (size_t)((DBG & 8) ? (row & 255) : row) * ep.ldc + col;
@@ -445,6 +449,7 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 4: RS_DBG(4); break;
         case 6: RS_DBG(6); break;
         case 8: RS_DBG(8); break;
+        case 16: RS_DBG(16); break;
         case 1: RS_DBG(1); break;
         case 2: RS_DBG(2); break;
         default: RS_DBG(3); break;

@@ -57,7 +57,7 @@ def main():
                         ref = (A[:4096].float() @ W.float().t() + b).half()
                     err = (out[:4096].float() - ref.float()).abs().max().item()
                     assert err < 0.05 * K ** 0.5, (cfg, err)
-            names = {0: "full", 1: "nostage", 2: "noepi", 3: "neither", 4: "ilv", 6: "ilv-noepi", 8: "l2store"}
+            names = {0: "full", 1: "nostage", 2: "noepi", 3: "neither", 4: "ilv", 6: "ilv-noepi", 8: "l2store", 16: "nostore"}
             print(f"M={M} N={N} K={K} cfg={cfg}: " + "  ".join(f"{names[d]} {v:7.1f}" for d, v in zip(dbgs, res))
                   + " TF/s", flush=True)
 
