@@ -19,6 +19,8 @@
 //    per-lane global SOURCE address and on the ds_read address: conflict-free b128 reads.
 //  * Bijective XCD-aware block remap: consecutive tiles (same A row panel) share an XCD L2.
 #include "common.h"
+#include <stdlib.h>
+#include <string.h>
 
 namespace {
 
@@ -276,6 +278,74 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             if (fh == 0 && row < ep.m_valid)
                 ep.lse_part[(size_t)row * ep.n_parts + slab] = make_float2(mx, sm);
         }
+    } else if constexpr ((DBG & 32) != 0) {
+        // Straight from the accumulators.  fp16 outputs: lane l holds cols 8g..8g+3 and lane
+        // l+32 cols 8g+4..8g+7 of the same row; one v_permlane32_swap per dword pair (g, g+1)
+        // gives lanes 0-31 cols 8g..8g+7 and lanes 32-63 cols 8g+8..8g+15 -> 16-B stores.
+        // fp32 outputs: the lane's 4 columns are already one 16-B store.
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            const int row = rbase + i * 32;
+            const bool ok = row < ep.m_valid;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+                if constexpr (EPI == EPI_BIAS_F16 || EPI == EPI_GELU_F16) {
+#pragma unroll
+                    for (int gp = 0; gp < 2; ++gp) {
+                        float x[8];
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) x[e] = acc[i][j][8 * gp + e];
+                        if constexpr (EPI == EPI_GELU_F16) {
+#pragma unroll
+                            for (int e = 0; e < 8; e += 2) {
+                                const f32x2 gv = gelu2((f32x2){x[e], x[e + 1]});
+                                x[e] = gv.x;
+                                x[e + 1] = gv.y;
+                            }
+                        }
+                        half8 h;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) h[e] = (f16)x[e];
+                        uint4 hv = __builtin_bit_cast(uint4, h);     // .xy group 2gp, .zw group 2gp+1
+                        auto s0 = __builtin_amdgcn_permlane32_swap(hv.x, hv.z, false, false);
+                        auto s1 = __builtin_amdgcn_permlane32_swap(hv.y, hv.w, false, false);
+                        const uint4 sv = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+                        const int col = n0 + wn * WTN + 32 * j + 16 * gp + 8 * fh;
+                        f16* orow = (f16*)ep.out + (size_t)((DBG & 8) ? (row & 255) : row) * ep.ldc;
+                        if (ok) *(uint4*)(orow + col) = sv;
+                        if constexpr (EPI == EPI_GELU_F16) {
+                            if (ep.kx == 3) {
+                                half8 l;
+#pragma unroll
+                                for (int e = 0; e < 8; ++e) l[e] = (f16)(x[e] - (float)h[e]);
+                                uint4 lv = __builtin_bit_cast(uint4, l);
+                                auto t0 = __builtin_amdgcn_permlane32_swap(lv.x, lv.z, false, false);
+                                auto t1 = __builtin_amdgcn_permlane32_swap(lv.y, lv.w, false, false);
+                                if (ok) {
+                                    *(uint4*)(orow + ep.nlog + col) = sv;
+                                    *(uint4*)(orow + 2 * ep.nlog + col) = make_uint4(t0[0], t1[0], t0[1], t1[1]);
+                                }
+                            }
+                        }
+                    }
+                } else {  // EPI_BIAS_F32, EPI_GELU_F32, EPI_RES_F32
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        float x[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+                        if constexpr (EPI == EPI_GELU_F32) {
+#pragma unroll
+                            for (int e = 0; e < 4; e += 2) {
+                                const f32x2 gv = gelu2((f32x2){x[e], x[e + 1]});
+                                x[e] = gv.x;
+                                x[e + 1] = gv.y;
+                            }
+                        }
+                        const size_t o = (size_t)((DBG & 8) ? (row & 255) : row) * ep.ldc + cbase + 32 * j + 8 * g;
+                        if (ok) *(float4*)((float*)ep.out + o) = make_float4(x[0], x[1], x[2], x[3]);
+                    }
+                }
+            }
+        }
     } else {
         // Through LDS: each wave parks one 32-row slice of its accumulators (fp32, row
         // stride WTN+4 floats: conflict-free b128 writes) in a private region, then reads it
@@ -392,7 +462,17 @@ int pick_cfg(int N_pad) {
 template <int EPI>
 hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep,
                       hipStream_t st) {
-    switch (pick_cfg(N_pad)) {
+    // RS_GEMM_EPI=direct: accumulator -> permlane32_swap -> global epilogue (no LDS pass)
+    static const int direct = [] {
+        const char* v = getenv("RS_GEMM_EPI");
+        return v && !strcmp(v, "direct") ? 1 : 0;
+    }();
+    const int cfg = pick_cfg(N_pad);
+    if (direct && EPI != EPI_LSE && (cfg == 0 || cfg == 1)) {
+        if (cfg == 0) return launch_t<256, 256, 2, 4, 2, 64, EPI, 32>(A, W, M_pad, N_pad, K, ep, st);
+        return launch_t<256, 128, 4, 2, 3, 64, EPI, 32>(A, W, M_pad, N_pad, K, ep, st);
+    }
+    switch (cfg) {
         case 0: return launch_t<256, 256, 2, 4, 2, 64, EPI>(A, W, M_pad, N_pad, K, ep, st);
         case 1: return launch_t<256, 128, 4, 2, 3, 64, EPI>(A, W, M_pad, N_pad, K, ep, st);
         case 3: return launch_t<256, 128, 4, 2, 3, 32, EPI>(A, W, M_pad, N_pad, K, ep, st);
@@ -450,6 +530,8 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 6: RS_DBG(6); break;
         case 8: RS_DBG(8); break;
         case 16: RS_DBG(16); break;
+        case 32: RS_DBG(32); break;
+        case 40: RS_DBG(40); break;
         case 1: RS_DBG(1); break;
         case 2: RS_DBG(2); break;
         default: RS_DBG(3); break;

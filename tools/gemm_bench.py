@@ -52,12 +52,12 @@ def main():
                 torch.cuda.synchronize()
                 ms = e0.elapsed_time(e1) / reps
                 res.append(2.0 * M * N * K / (ms * 1e-3) / 1e12)
-                if dbg == 0:
+                if dbg in (0, 32):
                     if ref is None:
                         ref = (A[:4096].float() @ W.float().t() + b).half()
                     err = (out[:4096].float() - ref.float()).abs().max().item()
                     assert err < 0.05 * K ** 0.5, (cfg, err)
-            names = {0: "full", 1: "nostage", 2: "noepi", 3: "neither", 4: "ilv", 6: "ilv-noepi", 8: "l2store", 16: "nostore"}
+            names = {0: "full", 1: "nostage", 2: "noepi", 3: "neither", 4: "ilv", 6: "ilv-noepi", 8: "l2store", 16: "nostore", 32: "direct", 40: "direct-l2"}
             print(f"M={M} N={N} K={K} cfg={cfg}: " + "  ".join(f"{names[d]} {v:7.1f}" for d, v in zip(dbgs, res))
                   + " TF/s", flush=True)
 
