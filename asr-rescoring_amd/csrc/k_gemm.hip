@@ -54,6 +54,14 @@ __device__ __forceinline__ f32x2 gelu2(f32x2 x) {
     return __builtin_elementwise_fma(s * erfz, x, hx);      // 0.5x + sign*0.5*erf*x
 }
 
+// 16-byte epilogue store; DBG&64: non-temporal (streamed past L2, keeps the A panels there)
+template <int DBG>
+__device__ __forceinline__ void st16(uint4* p, uint4 v) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    if constexpr (DBG & 64) __builtin_nontemporal_store((u32x4){v.x, v.y, v.z, v.w}, (u32x4*)p);
+    else *p = v;
+}
+
 // DBG (timing experiments only, rs_debug_gemm): bit0 = no K-loop staging (MFMA + LDS
 // reads on stale tiles), bit1 = no epilogue (accumulators kept alive, nothing stored).
 template <int BM, int BN, int WM, int WN, int NSTAGE, int BK, int EPI, int DBG = 0>
@@ -312,7 +320,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         const uint4 sv = make_uint4(s0[0], s1[0], s0[1], s1[1]);
                         const int col = n0 + wn * WTN + 32 * j + 16 * gp + 8 * fh;
                         f16* orow = (f16*)ep.out + (size_t)((DBG & 8) ? (row & 255) : row) * ep.ldc;
-                        if (ok) *(uint4*)(orow + col) = sv;
+                        if (ok) st16<DBG>((uint4*)(orow + col), sv);
                         if constexpr (EPI == EPI_GELU_F16) {
                             if (ep.kx == 3) {
                                 half8 l;
@@ -322,8 +330,8 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                                 auto t0 = __builtin_amdgcn_permlane32_swap(lv.x, lv.z, false, false);
                                 auto t1 = __builtin_amdgcn_permlane32_swap(lv.y, lv.w, false, false);
                                 if (ok) {
-                                    *(uint4*)(orow + ep.nlog + col) = sv;
-                                    *(uint4*)(orow + 2 * ep.nlog + col) = make_uint4(t0[0], t1[0], t0[1], t1[1]);
+                                    st16<DBG>((uint4*)(orow + ep.nlog + col), sv);
+                                    st16<DBG>((uint4*)(orow + 2 * ep.nlog + col), make_uint4(t0[0], t1[0], t0[1], t1[1]));
                                 }
                             }
                         }
@@ -341,7 +349,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                             }
                         }
                         const size_t o = (size_t)((DBG & 8) ? (row & 255) : row) * ep.ldc + cbase + 32 * j + 8 * g;
-                        if (ok) *(float4*)((float*)ep.out + o) = make_float4(x[0], x[1], x[2], x[3]);
+                        if (ok) st16<DBG>((uint4*)((float*)ep.out + o), __builtin_bit_cast(uint4, make_float4(x[0], x[1], x[2], x[3])));
                     }
                 }
             }
@@ -392,7 +400,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         half8 h;
 #pragma unroll
                         for (int e = 0; e < 8; ++e) h[e] = (f16)x[e];
-                        *(half8*)((f16*)ep.out + o) = h;
+                        st16<DBG>((uint4*)((f16*)ep.out + o), __builtin_bit_cast(uint4, h));
                     } else if constexpr (EPI == EPI_GELU_F16) {
                         f16* orow = (f16*)ep.out + (size_t)row * ep.ldc;
                         half8 h, l;
@@ -401,14 +409,14 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                             h[e] = (f16)x[e];
                             l[e] = (f16)(x[e] - (float)h[e]);
                         }
-                        *(half8*)(orow + col) = h;
+                        st16<DBG>((uint4*)(orow + col), __builtin_bit_cast(uint4, h));
                         if (ep.kx == 3) {
-                            *(half8*)(orow + ep.nlog + col) = h;
-                            *(half8*)(orow + 2 * ep.nlog + col) = l;
+                            st16<DBG>((uint4*)(orow + ep.nlog + col), __builtin_bit_cast(uint4, h));
+                            st16<DBG>((uint4*)(orow + 2 * ep.nlog + col), __builtin_bit_cast(uint4, l));
                         }
                     } else {  // EPI_BIAS_F32, EPI_GELU_F32, EPI_RES_F32 (residual already in acc)
-                        *(float4*)((float*)ep.out + o) = make_float4(x[0], x[1], x[2], x[3]);
-                        *(float4*)((float*)ep.out + o + 4) = make_float4(x[4], x[5], x[6], x[7]);
+                        st16<DBG>((uint4*)((float*)ep.out + o), __builtin_bit_cast(uint4, make_float4(x[0], x[1], x[2], x[3])));
+                        st16<DBG>((uint4*)((float*)ep.out + o + 4), __builtin_bit_cast(uint4, make_float4(x[4], x[5], x[6], x[7])));
                     }
                 }
             }
@@ -532,6 +540,8 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 16: RS_DBG(16); break;
         case 32: RS_DBG(32); break;
         case 40: RS_DBG(40); break;
+        case 64: RS_DBG(64); break;
+        case 96: RS_DBG(96); break;
         case 1: RS_DBG(1); break;
         case 2: RS_DBG(2); break;
         default: RS_DBG(3); break;
