@@ -54,17 +54,20 @@ __device__ __forceinline__ f32x2 gelu2(f32x2 x) {
     return __builtin_elementwise_fma(s * erfz, x, hx);      // 0.5x + sign*0.5*erf*x
 }
 
-// 16-byte epilogue store; DBG&64: non-temporal (streamed past L2, keeps the A panels there)
-template <int DBG>
+// 16-byte epilogue store; VAR&64: non-temporal (streamed past L2, keeps the A panels there)
+template <int VAR>
 __device__ __forceinline__ void st16(uint4* p, uint4 v) {
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    if constexpr (DBG & 64) __builtin_nontemporal_store((u32x4){v.x, v.y, v.z, v.w}, (u32x4*)p);
+    if constexpr (VAR & 64) __builtin_nontemporal_store((u32x4){v.x, v.y, v.z, v.w}, (u32x4*)p);
     else *p = v;
 }
 
-// DBG (timing experiments only, rs_debug_gemm): bit0 = no K-loop staging (MFMA + LDS
-// reads on stale tiles), bit1 = no epilogue (accumulators kept alive, nothing stored).
-template <int BM, int BN, int WM, int WN, int NSTAGE, int BK, int EPI, int DBG = 0>
+// VAR = variant bits.  Production: 64 (LDS epilogue, non-temporal stores; default),
+// 0 (LDS epilogue, plain stores), 32 (direct permlane epilogue).  Timing experiments only
+// (rs_debug_gemm): bit0 = no K-loop staging (MFMA + LDS reads on stale tiles), bit1 = no
+// epilogue (accumulators kept alive, nothing stored), bit2 = staging interleaved with the
+// MFMAs, bit3 = stores aliased onto rows 0..255 (L2-resident), bit4 = no global stores.
+template <int BM, int BN, int WM, int WN, int NSTAGE, int BK, int EPI, int VAR = 0>
 __global__ void __launch_bounds__(WM * WN * 64)
 gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int n_tiles_n,
                 EpiArgs ep) {
@@ -141,12 +144,12 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const float4 b4 = (DBG & 2) ? make_float4(0.f, 0.f, 0.f, 0.f)
+                const float4 b4 = (VAR & 2) ? make_float4(0.f, 0.f, 0.f, 0.f)
                                             : *(const float4*)(ep.bias + acol + 32 * j + 8 * g);
 #pragma unroll
                 for (int i = 0; i < TM; ++i) {
                     float4 v = b4;
-                    if constexpr (EPI == EPI_RES_F32 && !(DBG & 2)) {
+                    if constexpr (EPI == EPI_RES_F32 && !(VAR & 2)) {
                         const float4 r4 = *(const float4*)(ep.res + (size_t)(arow + 32 * i) * ep.ldc + acol + 32 * j + 8 * g);
                         v = make_float4(v.x + r4.x, v.y + r4.y, v.z + r4.z, v.w + r4.w);
                     }
@@ -175,17 +178,17 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         }
         // every wave's part of tile kt landed; every wave finished reading tile kt-1
         asm volatile("s_barrier" ::: "memory");
-        const bool do_stage = !(DBG & 1) && kt + NSTAGE - 1 < nk;
+        const bool do_stage = !(VAR & 1) && kt + NSTAGE - 1 < nk;
         int nb = buf + NSTAGE - 1;
         if (nb >= NSTAGE) nb -= NSTAGE;
         const int knext = (kt + NSTAGE - 1) * BK;
-        if constexpr (!(DBG & 4)) {
+        if constexpr (!(VAR & 4)) {
             if (do_stage) stage(nb, knext);
         }
-        // DBG&4: the next stage's LDS-DMA pieces are spread over the MFMA clusters
+        // VAR&4: the next stage's LDS-DMA pieces are spread over the MFMA clusters
         constexpr int NSUB = BK / 16;          // k-substeps per stage
         auto stage_part = [&](int q) {
-            if constexpr (DBG & 4) {
+            if constexpr (VAR & 4) {
                 __builtin_amdgcn_sched_barrier(0);
                 if (do_stage) {
 #pragma unroll
@@ -238,7 +241,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         buf = buf + 1 == NSTAGE ? 0 : buf + 1;
     }
 
-    if constexpr (DBG & 2) {
+    if constexpr (VAR & 2) {
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -286,7 +289,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             if (fh == 0 && row < ep.m_valid)
                 ep.lse_part[(size_t)row * ep.n_parts + slab] = make_float2(mx, sm);
         }
-    } else if constexpr ((DBG & 32) != 0) {
+    } else if constexpr ((VAR & 32) != 0) {
         // Straight from the accumulators.  fp16 outputs: lane l holds cols 8g..8g+3 and lane
         // l+32 cols 8g+4..8g+7 of the same row; one v_permlane32_swap per dword pair (g, g+1)
         // gives lanes 0-31 cols 8g..8g+7 and lanes 32-63 cols 8g+8..8g+15 -> 16-B stores.
@@ -319,8 +322,8 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         auto s1 = __builtin_amdgcn_permlane32_swap(hv.y, hv.w, false, false);
                         const uint4 sv = make_uint4(s0[0], s1[0], s0[1], s1[1]);
                         const int col = n0 + wn * WTN + 32 * j + 16 * gp + 8 * fh;
-                        f16* orow = (f16*)ep.out + (size_t)((DBG & 8) ? (row & 255) : row) * ep.ldc;
-                        if (ok) st16<DBG>((uint4*)(orow + col), sv);
+                        f16* orow = (f16*)ep.out + (size_t)((VAR & 8) ? (row & 255) : row) * ep.ldc;
+                        if (ok) st16<VAR>((uint4*)(orow + col), sv);
                         if constexpr (EPI == EPI_GELU_F16) {
                             if (ep.kx == 3) {
                                 half8 l;
@@ -330,8 +333,8 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                                 auto t0 = __builtin_amdgcn_permlane32_swap(lv.x, lv.z, false, false);
                                 auto t1 = __builtin_amdgcn_permlane32_swap(lv.y, lv.w, false, false);
                                 if (ok) {
-                                    st16<DBG>((uint4*)(orow + ep.nlog + col), sv);
-                                    st16<DBG>((uint4*)(orow + 2 * ep.nlog + col), make_uint4(t0[0], t1[0], t0[1], t1[1]));
+                                    st16<VAR>((uint4*)(orow + ep.nlog + col), sv);
+                                    st16<VAR>((uint4*)(orow + 2 * ep.nlog + col), make_uint4(t0[0], t1[0], t0[1], t1[1]));
                                 }
                             }
                         }
@@ -348,8 +351,8 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                                 x[e + 1] = gv.y;
                             }
                         }
-                        const size_t o = (size_t)((DBG & 8) ? (row & 255) : row) * ep.ldc + cbase + 32 * j + 8 * g;
-                        if (ok) st16<DBG>((uint4*)((float*)ep.out + o), __builtin_bit_cast(uint4, make_float4(x[0], x[1], x[2], x[3])));
+                        const size_t o = (size_t)((VAR & 8) ? (row & 255) : row) * ep.ldc + cbase + 32 * j + 8 * g;
+                        if (ok) st16<VAR>((uint4*)((float*)ep.out + o), __builtin_bit_cast(uint4, make_float4(x[0], x[1], x[2], x[3])));
                     }
                 }
             }
@@ -381,13 +384,13 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 const float4 u0 = *(const float4*)(lw + rr * LDW + cc);
                 const float4 u1 = *(const float4*)(lw + rr * LDW + cc + 4);
                 float x[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-                if constexpr (DBG & 16) {       // diagnostic: LDS pass + conversion, no store
+                if constexpr (VAR & 16) {       // diagnostic: LDS pass + conversion, no store
                     asm volatile("" ::"v"(x[0]), "v"(x[3]), "v"(x[7]));
                     continue;
                 }
                 if (row < ep.m_valid) {
-                    // DBG&8 (diagnostic): every tile stores into rows 0..255 (L2-resident)
-                    const size_t o = (size_t)((DBG & 8) ? (row & 255) : row) * ep.ldc + col;
+                    // VAR&8 (diagnostic): every tile stores into rows 0..255 (L2-resident)
+                    const size_t o = (size_t)((VAR & 8) ? (row & 255) : row) * ep.ldc + col;
                     if constexpr (EPI == EPI_GELU_F16 || EPI == EPI_GELU_F32) {
 #pragma unroll
                         for (int e = 0; e < 8; e += 2) {
@@ -400,7 +403,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         half8 h;
 #pragma unroll
                         for (int e = 0; e < 8; ++e) h[e] = (f16)x[e];
-                        st16<DBG>((uint4*)((f16*)ep.out + o), __builtin_bit_cast(uint4, h));
+                        st16<VAR>((uint4*)((f16*)ep.out + o), __builtin_bit_cast(uint4, h));
                     } else if constexpr (EPI == EPI_GELU_F16) {
                         f16* orow = (f16*)ep.out + (size_t)row * ep.ldc;
                         half8 h, l;
@@ -409,14 +412,14 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                             h[e] = (f16)x[e];
                             l[e] = (f16)(x[e] - (float)h[e]);
                         }
-                        st16<DBG>((uint4*)(orow + col), __builtin_bit_cast(uint4, h));
+                        st16<VAR>((uint4*)(orow + col), __builtin_bit_cast(uint4, h));
                         if (ep.kx == 3) {
-                            st16<DBG>((uint4*)(orow + ep.nlog + col), __builtin_bit_cast(uint4, h));
-                            st16<DBG>((uint4*)(orow + 2 * ep.nlog + col), __builtin_bit_cast(uint4, l));
+                            st16<VAR>((uint4*)(orow + ep.nlog + col), __builtin_bit_cast(uint4, h));
+                            st16<VAR>((uint4*)(orow + 2 * ep.nlog + col), __builtin_bit_cast(uint4, l));
                         }
                     } else {  // EPI_BIAS_F32, EPI_GELU_F32, EPI_RES_F32 (residual already in acc)
-                        st16<DBG>((uint4*)((float*)ep.out + o), __builtin_bit_cast(uint4, make_float4(x[0], x[1], x[2], x[3])));
-                        st16<DBG>((uint4*)((float*)ep.out + o + 4), __builtin_bit_cast(uint4, make_float4(x[4], x[5], x[6], x[7])));
+                        st16<VAR>((uint4*)((float*)ep.out + o), __builtin_bit_cast(uint4, make_float4(x[0], x[1], x[2], x[3])));
+                        st16<VAR>((uint4*)((float*)ep.out + o + 4), __builtin_bit_cast(uint4, make_float4(x[4], x[5], x[6], x[7])));
                     }
                 }
             }
@@ -424,14 +427,14 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     }
 }
 
-template <int BM, int BN, int WM, int WN, int NSTAGE, int BK, int EPI, int DBG = 0>
+template <int BM, int BN, int WM, int WN, int NSTAGE, int BK, int EPI, int VAR = 0>
 hipError_t launch_t(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep,
                     hipStream_t st) {
     constexpr int smem = NSTAGE * (BM + BN) * BK * 2;
     if (K % BK) return hipErrorInvalidValue;
     static bool attr_set = false;
     if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_f16_kernel<BM, BN, WM, WN, NSTAGE, BK, EPI, DBG>,
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_f16_kernel<BM, BN, WM, WN, NSTAGE, BK, EPI, VAR>,
                                            hipFuncAttributeMaxDynamicSharedMemorySize, smem);
         if (e != hipSuccess) return e;
         attr_set = true;
@@ -441,7 +444,7 @@ hipError_t launch_t(const f16* A, const f16* W, int M_pad, int N_pad, int K, con
     static const int gm_env = getenv("RS_GEMM_GROUP_M") ? atoi(getenv("RS_GEMM_GROUP_M")) : 0;
     EpiArgs e2 = ep;
     e2.group_m = gm_env > 0 ? gm_env : 4;   // 4 row panels per group (measured best of 1/2/4/8/16)
-    hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WM, WN, NSTAGE, BK, EPI, DBG>), dim3(grid), dim3(WM * WN * 64),
+    hipLaunchKernelGGL((gemm_f16_kernel<BM, BN, WM, WN, NSTAGE, BK, EPI, VAR>), dim3(grid), dim3(WM * WN * 64),
                        smem, st, A, W, K, ntn, e2);
     return hipGetLastError();
 }
@@ -470,15 +473,23 @@ int pick_cfg(int N_pad) {
 template <int EPI>
 hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep,
                       hipStream_t st) {
-    // RS_GEMM_EPI=direct: accumulator -> permlane32_swap -> global epilogue (no LDS pass)
-    static const int direct = [] {
+    // RS_GEMM_EPI: "nt" (default) LDS epilogue + non-temporal stores (the output stream does
+    // not evict the A panels from L2: +1..9 % at the BERT shapes, tools/gemm_bench.py);
+    // "lds" plain stores; "direct" accumulator -> permlane32_swap -> global (no LDS pass).
+    static const int mode = [] {
         const char* v = getenv("RS_GEMM_EPI");
-        return v && !strcmp(v, "direct") ? 1 : 0;
+        if (v && !strcmp(v, "direct")) return 32;
+        if (v && !strcmp(v, "lds")) return 0;
+        return 64;
     }();
     const int cfg = pick_cfg(N_pad);
-    if (direct && EPI != EPI_LSE && (cfg == 0 || cfg == 1)) {
-        if (cfg == 0) return launch_t<256, 256, 2, 4, 2, 64, EPI, 32>(A, W, M_pad, N_pad, K, ep, st);
-        return launch_t<256, 128, 4, 2, 3, 64, EPI, 32>(A, W, M_pad, N_pad, K, ep, st);
+    if (EPI != EPI_LSE && (cfg == 0 || cfg == 1) && mode != 0) {
+        if (mode == 32) {
+            if (cfg == 0) return launch_t<256, 256, 2, 4, 2, 64, EPI, 32>(A, W, M_pad, N_pad, K, ep, st);
+            return launch_t<256, 128, 4, 2, 3, 64, EPI, 32>(A, W, M_pad, N_pad, K, ep, st);
+        }
+        if (cfg == 0) return launch_t<256, 256, 2, 4, 2, 64, EPI, 64>(A, W, M_pad, N_pad, K, ep, st);
+        return launch_t<256, 128, 4, 2, 3, 64, EPI, 64>(A, W, M_pad, N_pad, K, ep, st);
     }
     switch (cfg) {
         case 0: return launch_t<256, 256, 2, 4, 2, 64, EPI>(A, W, M_pad, N_pad, K, ep, st);
@@ -511,7 +522,7 @@ hipError_t launch_gemm(int epi, const f16* A, const f16* W, int M_pad, int N_pad
 }
 
 // Timing/diagnostic entry (not part of the scoring path): one GEMM with an explicit tile
-// configuration and DBG bits, C = A[M,K].W[N,K]^T + bias -> fp16 [M, N].
+// configuration and VAR bits, C = A[M,K].W[N,K]^T + bias -> fp16 [M, N].
 extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, const float* bias, void* out,
                              int M, int N, int K, void* stream) {
     EpiArgs ep{};
