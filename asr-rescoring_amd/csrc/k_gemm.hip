@@ -185,6 +185,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         if constexpr (!(VAR & 4)) {
             if (do_stage) stage(nb, knext);
         }
+        if constexpr (VAR & 128) __builtin_amdgcn_sched_barrier(0);
         // VAR&4: the next stage's LDS-DMA pieces are spread over the MFMA clusters
         constexpr int NSUB = BK / 16;          // k-substeps per stage
         auto stage_part = [&](int q) {
@@ -238,6 +239,24 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         }
         mfmas(af1, bf1);
         stage_part(NSUB - 1);
+        if constexpr ((VAR & 128) && !(VAR & 4)) {
+            // Software pipeline the scheduler will not find by itself (it serialises the
+            // fragment reads and the MFMAs that consume them, exposing LDS latency per
+            // substep): substep 0's reads, then substep s+1's reads one per MFMA of substep s.
+            constexpr int NR = TM + TN, NM = TM * TN;
+            static_assert(NM >= NR, "one read per MFMA slot");
+            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+#pragma unroll
+            for (int s = 0; s < NSUB - 1; ++s) {
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+        }
         buf = buf + 1 == NSTAGE ? 0 : buf + 1;
     }
 
@@ -553,6 +572,9 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 40: RS_DBG(40); break;
         case 64: RS_DBG(64); break;
         case 96: RS_DBG(96); break;
+        case 128: RS_DBG(128); break;
+        case 131: RS_DBG(131); break;
+        case 192: RS_DBG(192); break;
         case 1: RS_DBG(1); break;
         case 2: RS_DBG(2); break;
         default: RS_DBG(3); break;
