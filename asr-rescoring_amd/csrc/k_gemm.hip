@@ -185,7 +185,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         if constexpr (!(VAR & 4)) {
             if (do_stage) stage(nb, knext);
         }
-        if constexpr (VAR & 128) __builtin_amdgcn_sched_barrier(0);
+        if constexpr (VAR & 384) __builtin_amdgcn_sched_barrier(0);
         // VAR&4: the next stage's LDS-DMA pieces are spread over the MFMA clusters
         constexpr int NSUB = BK / 16;          // k-substeps per stage
         auto stage_part = [&](int q) {
@@ -239,7 +239,23 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         }
         mfmas(af1, bf1);
         stage_part(NSUB - 1);
-        if constexpr ((VAR & 128) && !(VAR & 4)) {
+        if constexpr ((VAR & 256) && !(VAR & 4)) {
+            // variant: substep s+1's reads front-loaded, two per MFMA, so the last one has
+            // NM - NR/2 MFMAs to land before the (conservative) lgkmcnt(0)
+            constexpr int NR = TM + TN, NM = TM * TN;
+            static_assert(NR % 2 == 0 && NM >= NR / 2, "two reads per MFMA slot");
+            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+#pragma unroll
+            for (int s = 0; s < NSUB - 1; ++s) {
+#pragma unroll
+                for (int r = 0; r < NR / 2; ++r) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, NM - NR / 2, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+        } else if constexpr ((VAR & 128) && !(VAR & 4)) {
             // Software pipeline the scheduler will not find by itself (it serialises the
             // fragment reads and the MFMAs that consume them, exposing LDS latency per
             // substep): substep 0's reads, then substep s+1's reads one per MFMA of substep s.
@@ -575,6 +591,9 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 128: RS_DBG(128); break;
         case 131: RS_DBG(131); break;
         case 192: RS_DBG(192); break;
+        case 256: RS_DBG(256); break;
+        case 320: RS_DBG(320); break;
+        case 259: RS_DBG(259); break;
         case 1: RS_DBG(1); break;
         case 2: RS_DBG(2); break;
         default: RS_DBG(3); break;
