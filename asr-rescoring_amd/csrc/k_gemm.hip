@@ -62,8 +62,9 @@ __device__ __forceinline__ void st16(uint4* p, uint4 v) {
     else *p = v;
 }
 
-// VAR = variant bits.  Production: 64 (LDS epilogue, non-temporal stores; default),
-// 0 (LDS epilogue, plain stores), 32 (direct permlane epilogue).  Timing experiments only
+// VAR = variant bits.  Production: 128 (K loop software-pipelined by sched_group_barrier)
+// and 64 (non-temporal epilogue stores).  Alternatives kept for timing: 256 (front-loaded
+// read schedule), 32 (direct permlane epilogue, no LDS pass).  Timing experiments only
 // (rs_debug_gemm): bit0 = no K-loop staging (MFMA + LDS reads on stale tiles), bit1 = no
 // epilogue (accumulators kept alive, nothing stored), bit2 = staging interleaved with the
 // MFMAs, bit3 = stores aliased onto rows 0..255 (L2-resident), bit4 = no global stores.
@@ -508,33 +509,30 @@ int pick_cfg(int N_pad) {
 template <int EPI>
 hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep,
                       hipStream_t st) {
-    // RS_GEMM_EPI: "nt" (default) LDS epilogue + non-temporal stores (the output stream does
-    // not evict the A panels from L2: +1..9 % at the BERT shapes, tools/gemm_bench.py);
-    // "lds" plain stores; "direct" accumulator -> permlane32_swap -> global (no LDS pass).
-    static const int mode = [] {
-        const char* v = getenv("RS_GEMM_EPI");
-        if (v && !strcmp(v, "direct")) return 32;
-        if (v && !strcmp(v, "lds")) return 0;
-        return 64;
+    // Production variant: software-pipelined K loop (VAR 128) + non-temporal stores (VAR 64)
+    // for the epilogues selected by RS_GEMM_NT: "f16" (default: fp16 outputs stream past L2,
+    // keeping the A panels resident), "all", "none".
+    static const unsigned nt_mask = [] {
+        const char* v = getenv("RS_GEMM_NT");
+        const unsigned f16 = (1u << EPI_BIAS_F16) | (1u << EPI_GELU_F16);
+        if (v && !strcmp(v, "all")) return ~0u;
+        if (v && !strcmp(v, "none")) return 0u;
+        return f16;
     }();
     const int cfg = pick_cfg(N_pad);
-    if (EPI != EPI_LSE && (cfg == 0 || cfg == 1) && mode != 0) {
-        if (mode == 32) {
-            if (cfg == 0) return launch_t<256, 256, 2, 4, 2, 64, EPI, 32>(A, W, M_pad, N_pad, K, ep, st);
-            return launch_t<256, 128, 4, 2, 3, 64, EPI, 32>(A, W, M_pad, N_pad, K, ep, st);
-        }
-        if (cfg == 0) return launch_t<256, 256, 2, 4, 2, 64, EPI, 64>(A, W, M_pad, N_pad, K, ep, st);
-        return launch_t<256, 128, 4, 2, 3, 64, EPI, 64>(A, W, M_pad, N_pad, K, ep, st);
+    if ((nt_mask >> EPI) & 1u) {
+        if (cfg == 0) return launch_t<256, 256, 2, 4, 2, 64, EPI, 192>(A, W, M_pad, N_pad, K, ep, st);
+        if (cfg == 1) return launch_t<256, 128, 4, 2, 3, 64, EPI, 192>(A, W, M_pad, N_pad, K, ep, st);
     }
     switch (cfg) {
-        case 0: return launch_t<256, 256, 2, 4, 2, 64, EPI>(A, W, M_pad, N_pad, K, ep, st);
-        case 1: return launch_t<256, 128, 4, 2, 3, 64, EPI>(A, W, M_pad, N_pad, K, ep, st);
-        case 3: return launch_t<256, 128, 4, 2, 3, 32, EPI>(A, W, M_pad, N_pad, K, ep, st);
-        case 4: return launch_t<256, 256, 2, 4, 3, 32, EPI>(A, W, M_pad, N_pad, K, ep, st);
-        case 5: return launch_t<256, 128, 2, 2, 3, 32, EPI>(A, W, M_pad, N_pad, K, ep, st);
-        case 6: return launch_t<256, 128, 2, 2, 2, 32, EPI>(A, W, M_pad, N_pad, K, ep, st);
-        case 7: return launch_t<256, 256, 2, 4, 4, 32, EPI>(A, W, M_pad, N_pad, K, ep, st);
-        default: return launch_t<128, 128, 2, 2, 2, 64, EPI>(A, W, M_pad, N_pad, K, ep, st);
+        case 0: return launch_t<256, 256, 2, 4, 2, 64, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
+        case 1: return launch_t<256, 128, 4, 2, 3, 64, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
+        case 3: return launch_t<256, 128, 4, 2, 3, 32, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
+        case 4: return launch_t<256, 256, 2, 4, 3, 32, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
+        case 5: return launch_t<256, 128, 2, 2, 3, 32, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
+        case 6: return launch_t<256, 128, 2, 2, 2, 32, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
+        case 7: return launch_t<256, 256, 2, 4, 4, 32, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
+        default: return launch_t<128, 128, 2, 2, 2, 64, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
     }
 }
 

@@ -1,8 +1,8 @@
 set -e
 mkdir -p gpurun_out/ab
 timeout -k 10 400 python -m pytest tests/test_gpu_bert.py -x -q 2>&1 | tail -2
-for r in 1 2; do for m in lds nt; do
-  RS_GEMM_EPI=$m timeout -k 10 200 python bench.py --utts 20 --steps 3 --warmup 1 --cpu-seconds 0 > gpurun_out/ab/$m$r.json 2>/dev/null
+for r in 1 2; do for m in none f16 all; do
+  RS_GEMM_NT=$m timeout -k 10 200 python bench.py --utts 20 --steps 3 --warmup 1 --cpu-seconds 0 > gpurun_out/ab/$m$r.json 2>/dev/null
 done; done
 python - <<'PY'
 import json,glob
