@@ -67,7 +67,8 @@ __device__ __forceinline__ void st16(uint4* p, uint4 v) {
 // read schedule), 32 (direct permlane epilogue, no LDS pass).  Timing experiments only
 // (rs_debug_gemm): bit0 = no K-loop staging (MFMA + LDS reads on stale tiles), bit1 = no
 // epilogue (accumulators kept alive, nothing stored), bit2 = staging interleaved with the
-// MFMAs, bit3 = stores aliased onto rows 0..255 (L2-resident), bit4 = no global stores.
+// MFMAs, bit3 = stores aliased onto rows 0..255 (L2-resident), bit4 = no global stores,
+// bit9 = K-loop DMA never waited for (isolates its latency from its bandwidth cost).
 template <int BM, int BN, int WM, int WN, int NSTAGE, int BK, int EPI, int VAR = 0>
 __global__ void __launch_bounds__(WM * WN * 64)
 gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int n_tiles_n,
@@ -173,7 +174,8 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         // tile kt landed for this wave: all later-issued stages may stay in flight
         {
             const int ahead = min(NSTAGE - 2, nk - 1 - kt);   // stages issued after tile kt
-            if (NSTAGE >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+            if (VAR & 512) {   // diagnostic: DMA issued but never waited for (latency cost)
+            } else if (NSTAGE >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
             else if (NSTAGE >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
@@ -590,6 +592,7 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 131: RS_DBG(131); break;
         case 192: RS_DBG(192); break;
         case 256: RS_DBG(256); break;
+        case 704: RS_DBG(704); break;
         case 320: RS_DBG(320); break;
         case 259: RS_DBG(259); break;
         case 1: RS_DBG(1); break;
