@@ -593,6 +593,8 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 192: RS_DBG(192); break;
         case 256: RS_DBG(256); break;
         case 704: RS_DBG(704); break;
+        case 194: RS_DBG(194); break;
+        case 706: RS_DBG(706); break;
         case 320: RS_DBG(320); break;
         case 259: RS_DBG(259); break;
         case 1: RS_DBG(1); break;

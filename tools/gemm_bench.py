@@ -48,12 +48,12 @@ def main():
                     _time(fn, cfg, dbg, A, W, b, out, M, N, K, reps=1)
                     err = (out[:4096].float() - ref.float()).abs().max().item()
                     assert err < 0.05 * K ** 0.5, (cfg, dbg, err)
-            print(f"M={M} N={N} K={K} cfg={cfg}: " + "  ".join(f"{NAMES[d]} {v:7.1f}" for d, v in zip(dbgs, res))
+            print(f"M={M} N={N} K={K} cfg={cfg}: " + "  ".join(f"{NAMES.get(d, d)} {v:7.1f}" for d, v in zip(dbgs, res))
                   + " TF/s", flush=True)
 
 
 NAMES = {0: "full", 1: "nostage", 2: "noepi", 3: "neither", 4: "ilv", 6: "ilv-noepi", 8: "l2store", 16: "nostore",
-         32: "direct", 40: "direct-l2", 64: "nt", 96: "direct-nt", 128: "pipe", 131: "pipe-neither", 192: "pipe-nt", 256: "fl", 320: "fl-nt", 259: "fl-neither", 704: "pipe-nt-nowait"}
+         32: "direct", 40: "direct-l2", 64: "nt", 96: "direct-nt", 128: "pipe", 131: "pipe-neither", 192: "pipe-nt", 256: "fl", 320: "fl-nt", 259: "fl-neither", 704: "pipe-nt-nowait", 194: "pipe-noepi", 706: "pipe-noepi-nowait"}
 CHECKED = (0, 4, 32, 64, 96, 128, 192, 256, 320)      # variants that store the real result
 
 
