@@ -169,6 +169,77 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         if (s < nk) stage(s, s * BK);
 
     const int frow = lane & 31, fh = lane >> 5;
+    if constexpr (NSTAGE == 2 && (VAR & 1024)) {
+        // Two-buffer ring pipelined across K-steps.  One barrier per K-step, placed after
+        // this wave's reads of the step's last substep have landed and its own DMA pieces
+        // of the next step have arrived: past it, (a) every wave is done reading buffer
+        // `cur`, which is refilled with step kt+2, and (b) step kt+1 is complete, so its
+        // substep-0 fragments are read while the last substep's MFMAs issue.  Inside a
+        // step, substep s+1's reads interleave with substep s's MFMAs (MFMA first, so the
+        // compiler's lgkmcnt wait before it covers only the older reads).
+        constexpr int NSUB = BK / 16, NR = TM + TN, NM = TM * TN;
+        static_assert(NSUB % 2 == 0 && NM >= NR, "pipeline shape");
+        // Fragment addresses: swz(row, 2s + fh) = swz(row, fh) ^ 2s, and fragments 32 rows
+        // apart share the swizzle, so substep s is one XOR of bits 5-6 of a per-lane base and
+        // the fragment/buffer offsets are immediates (no per-substep address registers).
+        const int offA = (wm * WTM + frow) * RB + (swz<BK>(wm * WTM + frow, fh) << 4);
+        const int offB = A_BYTES + (wn * WTN + frow) * RB + (swz<BK>(wn * WTN + frow, fh) << 4);
+        auto load_frags = [&](const char* sbase, int s, half8 (&af)[TM], half8 (&bf)[TN]) {
+            const int xa = offA ^ (s << 5), xb = offB ^ (s << 5);
+#pragma unroll
+            for (int j = 0; j < TN; ++j) bf[j] = *(const half8*)(sbase + xb + j * 32 * RB);
+#pragma unroll
+            for (int i = 0; i < TM; ++i) af[i] = *(const half8*)(sbase + xa + i * 32 * RB);
+        };
+        auto mfmas = [&](const half8 (&af)[TM], const half8 (&bf)[TN]) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+        };
+        auto pattern = [&]() {
+#pragma unroll
+            for (int r = 0; r < NR; ++r) {
+                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
+        };
+        half8 af0[TM], bf0[TN], af1[TM], bf1[TN];
+        if (nk > 1 && !(VAR & 1)) stage(1, BK);
+        if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_barrier" ::: "memory");
+        load_frags(smem, 0, af0, bf0);
+        for (int kt = 0; kt < nk; ++kt) {
+            const int cur = kt & 1;
+            const char* sbase = smem + cur * STAGE;
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s = 0; s + 1 < NSUB; s += 2) {
+                load_frags(sbase, s + 1, af1, bf1);
+                mfmas(af0, bf0);
+                pattern();
+                __builtin_amdgcn_sched_barrier(0);
+                if (s + 2 < NSUB) {
+                    load_frags(sbase, s + 2, af0, bf0);
+                    mfmas(af1, bf1);
+                    pattern();
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            // last substep (fragments in af1/bf1)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (kt + 1 < nk) {
+                if (!(VAR & 512)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                asm volatile("s_barrier" ::: "memory");
+                if (kt + 2 < nk && !(VAR & 1)) stage(cur, (kt + 2) * BK);
+                load_frags(smem + (cur ^ 1) * STAGE, 0, af0, bf0);
+            }
+            mfmas(af1, bf1);
+        }
+    } else {
     int buf = 0;
     for (int kt = 0; kt < nk; ++kt) {
         // tile kt landed for this wave: all later-issued stages may stay in flight
@@ -278,6 +349,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         }
         buf = buf + 1 == NSTAGE ? 0 : buf + 1;
     }
+    }
 
     if constexpr (VAR & 2) {
 #pragma unroll
@@ -295,6 +367,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     const int rbase = m0 + wm * WTM + frow;
     const int cbase = n0 + wn * WTN + 4 * fh;
     if constexpr (EPI == EPI_LSE) {
+        static_assert(WTN == 64, "decoder logsumexp parts are 64-column slabs (n_parts = N/64)");
         // per (row, 64-column wave slab): max and sum exp over the slab + label logit
         const int slab = (n0 + wn * WTN) / WTN;
 #pragma unroll
@@ -400,12 +473,12 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         // stride WTN+4 floats: conflict-free b128 writes) in a private region, then reads it
         // back 8 consecutive columns per lane, so every global store covers whole 128/256-B
         // row segments instead of 16-B pieces of 32 rows.
-        static_assert(WTN == 64, "epilogue assumes 64-column wave tiles");
         constexpr int LDW = WTN + 4;
+        constexpr int LPR = WTN / 8, RPI = 64 / LPR, NIT = 32 / RPI;   // lanes/row, rows/pass
         static_assert(NW * 32 * LDW * 4 <= NSTAGE * STAGE, "epilogue LDS");
         __syncthreads();                                   // the LDS ring is no longer read
         float* lw = (float*)smem + wave * 32 * LDW;
-        const int rr0 = lane >> 3, cc = (lane & 7) * 8;
+        const int rr0 = lane / LPR, cc = (lane % LPR) * 8;
         const int col = n0 + wn * WTN + cc;
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
@@ -416,8 +489,8 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                     *(float4*)(lw + frow * LDW + j * 32 + 8 * g + 4 * fh) =
                         make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
 #pragma unroll
-            for (int it = 0; it < 4; ++it) {
-                const int rr = it * 8 + rr0;
+            for (int it = 0; it < NIT; ++it) {
+                const int rr = it * RPI + rr0;
                 const int row = m0 + wm * WTM + i * 32 + rr;
                 const float4 u0 = *(const float4*)(lw + rr * LDW + cc);
                 const float4 u1 = *(const float4*)(lw + rr * LDW + cc + 4);
@@ -575,6 +648,7 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 6: e = launch_t<256, 128, 2, 2, 2, 32, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
         case 4: e = launch_t<256, 256, 2, 4, 3, 32, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
         case 7: e = launch_t<256, 256, 2, 4, 4, 32, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
+        case 8: e = launch_t<256, 256, 2, 2, 2, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
         default: e = launch_t<128, 128, 2, 2, 2, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;   \
     }
     if (M % 256 || N % 256 || K % 64) return -1;
@@ -593,6 +667,9 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 192: RS_DBG(192); break;
         case 256: RS_DBG(256); break;
         case 704: RS_DBG(704); break;
+        case 1216: RS_DBG(1216); break;
+        case 1218: RS_DBG(1218); break;
+        case 1219: RS_DBG(1219); break;
         case 194: RS_DBG(194); break;
         case 706: RS_DBG(706); break;
         case 320: RS_DBG(320); break;
