@@ -169,7 +169,62 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         if (s < nk) stage(s, s * BK);
 
     const int frow = lane & 31, fh = lane >> 5;
-    if constexpr (NSTAGE == 2 && (VAR & 1024)) {
+    if constexpr (NSTAGE == 2 && WM == 2 && BK == 64 && (VAR & 2048)) {
+        // Ping-pong: the two wave rows (grp = wm; every SIMD holds one wave of each) run one
+        // barrier apart, so while one issues its MFMA cluster the other reads its next
+        // fragments / issues DMA, and the MFMA pipe never waits on LDS latency.
+        // Phase p = one k16 substep (K-step u = p/4, s = p%4):
+        //   load segment:  6 ds_read_b128 of substep s (+ DMA issue / wait, below); s_barrier
+        //   MFMA segment:  lgkmcnt(0); 8 MFMAs;                                   s_barrier
+        // Group 1 starts with one extra barrier (pairs with group 0's first load barrier) and
+        // group 0 ends with one.  Barrier B_j (B_0 = prologue): group 0 load(p) = [B_2p,
+        // B_2p+1), MFMA(p) = [B_2p+1, B_2p+2); group 1 is one barrier later.  Buffer of step
+        // u-1 is free after B_8u+1 (group 1's last reads retire in its MFMA(4u-1)), so the
+        // DMA of step u+1 is issued in group 1's load(4u) / group 0's load(4u+1), and each
+        // wave waits vmcnt(0) in load(4u+3): every piece has landed before B_8u+8, where
+        // group 0 starts reading step u+1.
+        constexpr int NSUB = BK / 16;
+        static_assert(NSUB == 4, "ping-pong schedule assumes BK = 64");
+        const int grp = wm;
+        const int offA = (wm * WTM + frow) * RB + (swz<BK>(wm * WTM + frow, fh) << 4);
+        const int offB = A_BYTES + (wn * WTN + frow) * RB + (swz<BK>(wn * WTN + frow, fh) << 4);
+        half8 af[TM], bf[TN];
+        if (nk > 1 && !(VAR & 1)) stage(1, BK);
+        if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("s_barrier" ::: "memory");                                   // B_0
+        if (grp == 1) asm volatile("s_barrier" ::: "memory");
+        for (int u = 0; u < nk; ++u) {
+            const char* sbase = smem + (u & 1) * STAGE;
+#pragma unroll
+            for (int s = 0; s < NSUB; ++s) {
+                // ---- load segment
+                __builtin_amdgcn_sched_barrier(0);
+                const int xa = offA ^ (s << 5), xb = offB ^ (s << 5);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bf[j] = *(const half8*)(sbase + xb + j * 32 * RB);
+#pragma unroll
+                for (int i = 0; i < TM; ++i) af[i] = *(const half8*)(sbase + xa + i * 32 * RB);
+                if (s == 1 - grp && u >= 1 && u + 1 < nk && !(VAR & 1)) stage((u + 1) & 1, (u + 1) * BK);
+                if (s == 3 && !(VAR & 512)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_barrier" ::: "memory");
+                // ---- MFMA segment
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_sched_barrier(0);
+                if constexpr (VAR & 4096) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+                if constexpr (VAR & 4096) __builtin_amdgcn_s_setprio(0);
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_barrier" ::: "memory");
+            }
+        }
+        if (grp == 0) asm volatile("s_barrier" ::: "memory");
+    } else if constexpr (NSTAGE == 2 && (VAR & 1024)) {
         // Two-buffer ring pipelined across K-steps.  One barrier per K-step, placed after
         // this wave's reads of the step's last substep have landed and its own DMA pieces
         // of the next step have arrived: past it, (a) every wave is done reading buffer
@@ -668,6 +723,10 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 256: RS_DBG(256); break;
         case 704: RS_DBG(704); break;
         case 1216: RS_DBG(1216); break;
+        case 2240: RS_DBG(2240); break;
+        case 6336: RS_DBG(6336); break;
+        case 2242: RS_DBG(2242); break;
+        case 2243: RS_DBG(2243); break;
         case 1218: RS_DBG(1218); break;
         case 1219: RS_DBG(1219); break;
         case 194: RS_DBG(194); break;
