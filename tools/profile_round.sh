@@ -1,0 +1,24 @@
+#!/bin/bash
+# One GPU call: full bench line + rocprofv3 kernel stats of the same workload + separate
+# FETCH_SIZE / WRITE_SIZE PMC passes (MI355X_MICROARCH.md HBM recipe) -> gpurun_out/prof/.
+# usage (on the GPU box, repo root): bash tools/profile_round.sh
+set -eo pipefail
+export TMPDIR=/tmp
+O=gpurun_out/prof
+rm -rf $O && mkdir -p $O
+echo "[prof] bench"
+timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err
+echo "[prof] kernel trace"
+timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- \
+    python bench.py --cpu-seconds 0 > $O/bench_under_rocprof.json 2> $O/kt.err
+echo "[prof] pmc fetch"
+timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o run --output-format csv -- \
+    python bench.py --utts 20 --steps 1 --warmup 0 --cpu-seconds 0 --no-profile > /dev/null 2> $O/fetch.err
+echo "[prof] pmc write"
+timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $O/write -o run --output-format csv -- \
+    python bench.py --utts 20 --steps 1 --warmup 0 --cpu-seconds 0 --no-profile > /dev/null 2> $O/write.err
+python tools/pmc_summary.py "$(dirname "$(find $O/fetch -name '*counter_collection.csv' | head -1)")" \
+    "$(dirname "$(find $O/write -name '*counter_collection.csv' | head -1)")" $O/pmc_gemm_traffic.json > /dev/null
+cp "$(find $O/kt -name '*kernel_stats.csv' | head -1)" $O/kernel_stats.csv
+echo "[prof] done"
+tail -c 2000 $O/bench.json
