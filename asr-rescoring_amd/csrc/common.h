@@ -19,11 +19,16 @@ enum EpiKind {
     EPI_RES_F32 = 3,    // out32 = acc + bias + res32              (BertSelfOutput / BertOutput, pre-LN)
     EPI_LSE = 4,        // per-row partial (max, sum exp) over a 64-column slab + label logit
     EPI_BIAS_F32 = 5,   // out32 = acc + bias                      (QKV in the fp16x3 precision mode)
+    EPI_RESLN_F32 = 6,  // out32 = acc + bias + LN(res32)          (same, residual kept pre-LN:
+                        //   LN rebuilt from res_stats/res_g/res_b; out may alias res)
 };
 
 struct EpiArgs {
     const float* bias;     // [N]
-    const float* res;      // [M, ldc] fp32 residual (EPI_RES_F32)
+    const float* res;      // [M, ldc] fp32 residual (EPI_RES_F32; pre-LN sum for EPI_RESLN_F32)
+    const float2* res_stats;  // [M] (mean, 1/sqrt(var + eps)) of res rows (EPI_RESLN_F32)
+    const float* res_g;    // [N] LayerNorm weight / bias applied to res (EPI_RESLN_F32)
+    const float* res_b;
     void* out;             // [M, ldc]
     int ldc;
     int m_valid;           // rows >= m_valid are not stored
@@ -96,16 +101,27 @@ int gemm_row_align();   // M padding granularity required by launch_gemm
 
 // kx: width factor of the fp16 operand images written (1 or 3, see put_split);
 // qkv32: the QKV projection is fp32 (fp16x3 mode) instead of fp16.
+// LayerNorm output of one element from its row statistics: the single expression every
+// kernel uses, so an LN rebuilt downstream (EPI_RESLN_F32, attention_query) is bit-identical
+// to the one the LN kernel writes.
+__device__ __forceinline__ float ln_apply(float x, float2 st, float g, float b) {
+    return (x - st.x) * st.y * g + b;
+}
+
+// embed_ln writes the pre-LN embedding sum (x32), its row statistics and the fp16 operand
+// image of LN(x); ln_rows writes the operand image, the statistics and (y32 != null) LN(x).
 hipError_t launch_embed_ln(const int* tok, SeqMeta sm, int s0, int s1, int row0, int mask_id,
                            int vocab, const float* word, const float* pos, const float* type0,
-                           const float* g, const float* b, float eps, int H, float* h32, f16* h16,
-                           int kx, hipStream_t st);
+                           const float* g, const float* b, float eps, int H, float* x32,
+                           float2* stats, f16* h16, int kx, hipStream_t st);
 hipError_t launch_ln_rows(const float* x, int rows, const float* g, const float* b, float eps,
-                          int H, float* y32, f16* y16, int kx, hipStream_t st);
+                          int H, float* y32, float2* stats, f16* y16, int kx, hipStream_t st);
 hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0, int s1, int row0,
                                  int H, int heads, f16* ctx, int kx, hipStream_t st);
-hipError_t launch_attention_query(const void* qkv, bool qkv32, const float* h32, SeqMeta sm, int s0,
-                                  int s1, int row0, int H, int heads, f16* ctxq, float* resq, int kx,
+// resq = LN(x32[query row]) (x32 pre-LN, with its row statistics and LN weight / bias)
+hipError_t launch_attention_query(const void* qkv, bool qkv32, const float* x32, const float2* stats,
+                                  const float* g, const float* b, SeqMeta sm, int s0, int s1,
+                                  int row0, int H, int heads, f16* ctxq, float* resq, int kx,
                                   hipStream_t st);
 hipError_t launch_gather_labels(const int* tok, SeqMeta sm, int s0, int s1, int* lab,
                                 hipStream_t st);

@@ -14,14 +14,19 @@
 //  segsum_f64      per-hypothesis PLL, float64, in row order (MLM_PLL/main.py:106-107)
 //
 // Every producer of a GEMM operand writes the fp16 operand image (put_split: [hi] or
-// [hi | hi | lo]) next to the fp32 value the residual path keeps.
+// [hi | hi | lo]).  The residual stream stays PRE-LayerNorm in fp32 (x32) with per-row
+// (mean, rstd): its consumers (the next residual GEMM's accumulator init, attention_query)
+// rebuild LN(x) with ln_apply, so no LN kernel writes an fp32 copy of its output.
 #include "common.h"
 
 namespace {
 
+// LayerNorm of one row held as NV float4 per lane (row = 256*NV floats over one wave).
+// Writes the row statistics (stats != null), LN(x) in fp32 (y32 != null) and the fp16
+// operand image; every output element goes through ln_apply (common.h).
 template <int NV>
-__device__ __forceinline__ void ln_store(float4 (&x)[NV], const float* g, const float* b, float eps,
-                                         int lane, float* y32, f16* y16, int kx) {
+__device__ __forceinline__ void ln_store(const float4 (&x)[NV], const float* g, const float* b, float eps,
+                                         int lane, float* y32, float2* stats, f16* y16, int kx) {
     constexpr int H = NV * 256;
     float s = 0.f;
 #pragma unroll
@@ -30,21 +35,22 @@ __device__ __forceinline__ void ln_store(float4 (&x)[NV], const float* g, const 
     float q = 0.f;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
-        x[v].x -= mean; x[v].y -= mean; x[v].z -= mean; x[v].w -= mean;
-        q += (x[v].x * x[v].x + x[v].y * x[v].y) + (x[v].z * x[v].z + x[v].w * x[v].w);
+        const float4 d = make_float4(x[v].x - mean, x[v].y - mean, x[v].z - mean, x[v].w - mean);
+        q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
     }
-    const float inv = 1.0f / sqrtf(wave_sum(q) * (1.0f / H) + eps);
+    const float2 st = make_float2(mean, 1.0f / sqrtf(wave_sum(q) * (1.0f / H) + eps));
+    if (stats && lane == 0) *stats = st;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         const int c = v * 256 + lane * 4;
         const float4 gg = *(const float4*)(g + c);
         const float4 bb = *(const float4*)(b + c);
         float4 y;
-        y.x = x[v].x * inv * gg.x + bb.x;
-        y.y = x[v].y * inv * gg.y + bb.y;
-        y.z = x[v].z * inv * gg.z + bb.z;
-        y.w = x[v].w * inv * gg.w + bb.w;
-        *(float4*)(y32 + c) = y;
+        y.x = ln_apply(x[v].x, st, gg.x, bb.x);
+        y.y = ln_apply(x[v].y, st, gg.y, bb.y);
+        y.z = ln_apply(x[v].z, st, gg.z, bb.z);
+        y.w = ln_apply(x[v].w, st, gg.w, bb.w);
+        if (y32) *(float4*)(y32 + c) = y;
         put_split4(y16, c, H, kx, y);
     }
 }
@@ -54,8 +60,8 @@ __global__ void __launch_bounds__(256)
 embed_ln_kernel(const int* __restrict__ tok, SeqMeta sm, int s0, int row0, int mask_id, int vocab,
                 const float* __restrict__ word, const float* __restrict__ pos,
                 const float* __restrict__ type0, const float* __restrict__ g,
-                const float* __restrict__ b, float eps, float* __restrict__ h32,
-                f16* __restrict__ h16, int kx) {
+                const float* __restrict__ b, float eps, float* __restrict__ x32,
+                float2* __restrict__ stats, f16* __restrict__ h16, int kx) {
     constexpr int H = NV * 256;
     const int s = s0 + blockIdx.x;
     const int T = sm.len[s], toff = sm.tok_off[s], mp = sm.mask_pos[s];
@@ -75,15 +81,17 @@ embed_ln_kernel(const int* __restrict__ tok, SeqMeta sm, int s0, int row0, int m
             x[v] = make_float4((w.x + ty.x) + p.x, (w.y + ty.y) + p.y, (w.z + ty.z) + p.z, (w.w + ty.w) + p.w);
         }
         const size_t r = (size_t)(rs + t);
-        ln_store<NV>(x, g, b, eps, lane, h32 + r * H, h16 + r * kx * H, kx);
+#pragma unroll
+        for (int v = 0; v < NV; ++v) *(float4*)(x32 + r * H + v * 256 + lane * 4) = x[v];
+        ln_store<NV>(x, g, b, eps, lane, nullptr, stats + r, h16 + r * kx * H, kx);
     }
 }
 
 template <int NV>
 __global__ void __launch_bounds__(256)
 ln_rows_kernel(const float* __restrict__ xin, int rows, const float* __restrict__ g,
-               const float* __restrict__ b, float eps, float* __restrict__ y32, f16* __restrict__ y16,
-               int kx) {
+               const float* __restrict__ b, float eps, float* __restrict__ y32,
+               float2* __restrict__ stats, f16* __restrict__ y16, int kx) {
     constexpr int H = NV * 256;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -91,7 +99,8 @@ ln_rows_kernel(const float* __restrict__ xin, int rows, const float* __restrict_
     float4 x[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) x[v] = *(const float4*)(xin + (size_t)row * H + v * 256 + lane * 4);
-    ln_store<NV>(x, g, b, eps, lane, y32 + (size_t)row * H, y16 + (size_t)row * kx * H, kx);
+    ln_store<NV>(x, g, b, eps, lane, y32 ? y32 + (size_t)row * H : nullptr, stats ? stats + row : nullptr,
+                 y16 + (size_t)row * kx * H, kx);
 }
 
 __device__ __forceinline__ void load8(const f16* p, float (&o)[8]) {
@@ -319,8 +328,10 @@ attn_mfma_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int 
 // for QK^T, lanes over the 64 head dims for P.V.
 template <class QT>
 __global__ void __launch_bounds__(64)
-attn_query_kernel(const QT* __restrict__ qkv, const float* __restrict__ h32, SeqMeta sm, int s0,
-                  int row0, int H, f16* __restrict__ ctxq, float* __restrict__ resq, int kx) {
+attn_query_kernel(const QT* __restrict__ qkv, const float* __restrict__ x32,
+                  const float2* __restrict__ stats, const float* __restrict__ lg,
+                  const float* __restrict__ lb, SeqMeta sm, int s0, int row0, int H,
+                  f16* __restrict__ ctxq, float* __restrict__ resq, int kx) {
     __shared__ float sq[64];
     __shared__ float sp[64];
     const int s = s0 + blockIdx.x, h = blockIdx.y;
@@ -361,7 +372,11 @@ attn_query_kernel(const QT* __restrict__ qkv, const float* __restrict__ h32, Seq
     }
     const int s_loc = s - s0;
     put_split(ctxq + (size_t)s_loc * kx * H, h * 64 + lane, H, kx, acc / l);
-    resq[(size_t)s_loc * H + h * 64 + lane] = h32[(size_t)(rs + qi) * H + h * 64 + lane];
+    {   // residual of the scored row: LN of its pre-LN sum
+        const int c = h * 64 + lane;
+        const size_t r = (size_t)(rs + qi);
+        resq[(size_t)s_loc * H + c] = ln_apply(x32[r * H + c], stats[r], lg[c], lb[c]);
+    }
 }
 
 __global__ void gather_labels_kernel(const int* __restrict__ tok, SeqMeta sm, int s0, int n,
@@ -416,11 +431,11 @@ __global__ void segsum_f64_kernel(const float* __restrict__ row_lp, const int* _
 
 hipError_t launch_embed_ln(const int* tok, SeqMeta sm, int s0, int s1, int row0, int mask_id,
                            int vocab, const float* word, const float* pos, const float* type0,
-                           const float* g, const float* b, float eps, int H, float* h32, f16* h16,
-                           int kx, hipStream_t st) {
+                           const float* g, const float* b, float eps, int H, float* x32,
+                           float2* stats, f16* h16, int kx, hipStream_t st) {
     const int n = s1 - s0;
     if (n <= 0) return hipSuccess;
-#define RS_EMB(NV) hipLaunchKernelGGL(embed_ln_kernel<NV>, dim3(n), dim3(256), 0, st, tok, sm, s0, row0, mask_id, vocab, word, pos, type0, g, b, eps, h32, h16, kx)
+#define RS_EMB(NV) hipLaunchKernelGGL(embed_ln_kernel<NV>, dim3(n), dim3(256), 0, st, tok, sm, s0, row0, mask_id, vocab, word, pos, type0, g, b, eps, x32, stats, h16, kx)
     switch (H) {
         case 256: RS_EMB(1); break;
         case 512: RS_EMB(2); break;
@@ -433,10 +448,10 @@ hipError_t launch_embed_ln(const int* tok, SeqMeta sm, int s0, int s1, int row0,
 }
 
 hipError_t launch_ln_rows(const float* x, int rows, const float* g, const float* b, float eps,
-                          int H, float* y32, f16* y16, int kx, hipStream_t st) {
+                          int H, float* y32, float2* stats, f16* y16, int kx, hipStream_t st) {
     if (rows <= 0) return hipSuccess;
     const dim3 grid((rows + 3) / 4);
-#define RS_LN(NV) hipLaunchKernelGGL(ln_rows_kernel<NV>, grid, dim3(256), 0, st, x, rows, g, b, eps, y32, y16, kx)
+#define RS_LN(NV) hipLaunchKernelGGL(ln_rows_kernel<NV>, grid, dim3(256), 0, st, x, rows, g, b, eps, y32, stats, y16, kx)
     switch (H) {
         case 256: RS_LN(1); break;
         case 512: RS_LN(2); break;
@@ -462,15 +477,16 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
     return hipGetLastError();
 }
 
-hipError_t launch_attention_query(const void* qkv, bool qkv32, const float* h32, SeqMeta sm, int s0,
-                                  int s1, int row0, int H, int heads, f16* ctxq, float* resq, int kx,
+hipError_t launch_attention_query(const void* qkv, bool qkv32, const float* x32, const float2* stats,
+                                  const float* g, const float* b, SeqMeta sm, int s0, int s1,
+                                  int row0, int H, int heads, f16* ctxq, float* resq, int kx,
                                   hipStream_t st) {
     if (s1 <= s0) return hipSuccess;
     const dim3 grid(s1 - s0, heads);
     if (qkv32)
-        hipLaunchKernelGGL(attn_query_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, h32, sm, s0, row0, H, ctxq, resq, kx);
+        hipLaunchKernelGGL(attn_query_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, x32, stats, g, b, sm, s0, row0, H, ctxq, resq, kx);
     else
-        hipLaunchKernelGGL(attn_query_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, h32, sm, s0, row0, H, ctxq, resq, kx);
+        hipLaunchKernelGGL(attn_query_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, x32, stats, g, b, sm, s0, row0, H, ctxq, resq, kx);
     return hipGetLastError();
 }
 

@@ -142,17 +142,33 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     {
         const int arow = m0 + wm * WTM + (lane & 31);
         const int acol = n0 + wn * WTN + 4 * (lane >> 5);
+        float2 rst[TM];                       // EPI_RESLN_F32: LN statistics of the residual rows
+        if constexpr (EPI == EPI_RESLN_F32) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i) rst[i] = ep.res_stats[arow + 32 * i];
+        }
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                const float4 b4 = (VAR & 2) ? make_float4(0.f, 0.f, 0.f, 0.f)
-                                            : *(const float4*)(ep.bias + acol + 32 * j + 8 * g);
+                const int col = acol + 32 * j + 8 * g;
+                const float4 b4 = (VAR & 2) ? make_float4(0.f, 0.f, 0.f, 0.f) : *(const float4*)(ep.bias + col);
+                float4 lg4, lb4;
+                if constexpr (EPI == EPI_RESLN_F32) {
+                    lg4 = *(const float4*)(ep.res_g + col);
+                    lb4 = *(const float4*)(ep.res_b + col);
+                }
 #pragma unroll
                 for (int i = 0; i < TM; ++i) {
                     float4 v = b4;
-                    if constexpr (EPI == EPI_RES_F32 && !(VAR & 2)) {
-                        const float4 r4 = *(const float4*)(ep.res + (size_t)(arow + 32 * i) * ep.ldc + acol + 32 * j + 8 * g);
+                    if constexpr ((EPI == EPI_RES_F32 || EPI == EPI_RESLN_F32) && !(VAR & 2)) {
+                        float4 r4 = *(const float4*)(ep.res + (size_t)(arow + 32 * i) * ep.ldc + col);
+                        if constexpr (EPI == EPI_RESLN_F32) {
+                            r4.x = ln_apply(r4.x, rst[i], lg4.x, lb4.x);
+                            r4.y = ln_apply(r4.y, rst[i], lg4.y, lb4.y);
+                            r4.z = ln_apply(r4.z, rst[i], lg4.z, lb4.z);
+                            r4.w = ln_apply(r4.w, rst[i], lg4.w, lb4.w);
+                        }
                         v = make_float4(v.x + r4.x, v.y + r4.y, v.z + r4.z, v.w + r4.w);
                     }
                     acc[i][j][4 * g] = v.x;
@@ -505,7 +521,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                             }
                         }
                     }
-                } else {  // EPI_BIAS_F32, EPI_GELU_F32, EPI_RES_F32
+                } else {  // EPI_BIAS_F32, EPI_GELU_F32, EPI_RES_F32, EPI_RESLN_F32
 #pragma unroll
                     for (int g = 0; g < 4; ++g) {
                         float x[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
@@ -583,7 +599,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                             st16<VAR>((uint4*)(orow + ep.nlog + col), __builtin_bit_cast(uint4, h));
                             st16<VAR>((uint4*)(orow + 2 * ep.nlog + col), __builtin_bit_cast(uint4, l));
                         }
-                    } else {  // EPI_BIAS_F32, EPI_GELU_F32, EPI_RES_F32 (residual already in acc)
+                    } else {  // fp32 outputs (residual already in acc)
                         st16<VAR>((uint4*)((float*)ep.out + o), __builtin_bit_cast(uint4, make_float4(x[0], x[1], x[2], x[3])));
                         st16<VAR>((uint4*)((float*)ep.out + o + 4), __builtin_bit_cast(uint4, make_float4(x[4], x[5], x[6], x[7])));
                     }
@@ -680,6 +696,7 @@ hipError_t launch_gemm(int epi, const f16* A, const f16* W, int M_pad, int N_pad
         case EPI_RES_F32: return launch_epi<EPI_RES_F32>(A, W, M_pad, N_pad, K, ep, st);
         case EPI_LSE: return launch_epi<EPI_LSE>(A, W, M_pad, N_pad, K, ep, st);
         case EPI_BIAS_F32: return launch_epi<EPI_BIAS_F32>(A, W, M_pad, N_pad, K, ep, st);
+        case EPI_RESLN_F32: return launch_epi<EPI_RESLN_F32>(A, W, M_pad, N_pad, K, ep, st);
     }
     return hipErrorInvalidValue;
 }

@@ -77,7 +77,7 @@ struct rs_model {
     int64_t max_rows = 0;
     int s_cap = 0, r_pad = 0, m_pad = 0;
     int kx = 1;                 // fp16 operand image width (1: fp16, 3: fp16x3)
-    DevBuf h32, h16, t32, qkv, ctx, inter;
+    DevBuf xst, h16, t32, qkv, ctx, inter;   // xst: (mean, rstd) of the pre-LN rows in t32
     DevBuf ctxq, resq, tq32, hq32, hq16, interq, lab, llog, part, rowlp_tmp;
     DevBuf meta, hypoff;
     std::vector<int> pinned_dummy;
@@ -145,7 +145,7 @@ int reserve_impl(rs_model* m, int64_t max_rows) {
     const size_t M = m->m_pad, R = m->r_pad, H = c.hidden, F = c.intermediate;
     HIPTRY(hipSetDevice(m->device));
     const size_t kx = m->kx;
-    HIPTRY(m->h32.ensure(M * H * 4));
+    HIPTRY(m->xst.ensure(M * sizeof(float2)));
     HIPTRY(m->h16.ensure(M * H * 2 * kx));
     HIPTRY(m->t32.ensure(M * H * 4));
     HIPTRY(m->qkv.ensure(M * 3 * H * (kx == 3 ? 4 : 2)));
@@ -167,6 +167,8 @@ int reserve_impl(rs_model* m, int64_t max_rows) {
     HIPTRY(hipMemset(m->ctxq.p, 0, m->ctxq.bytes));
     HIPTRY(hipMemset(m->hq16.p, 0, m->hq16.bytes));
     HIPTRY(hipMemset(m->interq.p, 0, m->interq.bytes));
+    HIPTRY(hipMemset(m->t32.p, 0, m->t32.bytes));    // pad rows of the residual stream stay finite
+    HIPTRY(hipMemset(m->xst.p, 0, m->xst.bytes));
     return RS_OK;
 }
 
@@ -236,16 +238,16 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
     const bool q32 = kx == 3;                 // fp16x3: QKV kept in fp32 for attention
     const int qkv_epi = q32 ? EPI_BIAS_F32 : EPI_BIAS_F16;
     const int rows = c.rows, ns = c.s1 - c.s0;
-    float* h32 = m->h32.as<float>();
+    float2* xst = m->xst.as<float2>();
     f16* h16 = m->h16.as<f16>();
-    float* t32 = m->t32.as<float>();
+    float* t32 = m->t32.as<float>();     // residual stream, pre-LN fp32 (LN rebuilt from xst)
     void* qkv = m->qkv.p;
     f16* ctx = m->ctx.as<f16>();
     f16* inter = m->inter.as<f16>();
     {
         ProfScope ps(m, st, RS_K_OTHER, 0);
         HIPTRY(launch_embed_ln(d_tok, sm, c.s0, c.s1, 0, cf.mask_id, cf.vocab, m->word32, m->pos32,
-                               m->type32, m->eg, m->eb, cf.ln_eps, H, h32, h16, kx, st));
+                               m->type32, m->eg, m->eb, cf.ln_eps, H, t32, xst, h16, kx, st));
     }
     EpiArgs ep{};
     auto gelu_ep = [&](const float* bias, f16* out) {
@@ -253,9 +255,19 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
         e.bias = bias; e.out = out; e.ldc = kx * F; e.kx = kx; e.nlog = F;
         return e;
     };
+    // residual GEMM: t32 <- acc + bias + LN(t32) (in place: a tile reads and writes only its own
+    // rows x columns), LN given by the statistics in xst and the LN parameters (lg, lb)
+    auto resln_ep = [&](const float* bias, const float* lg, const float* lb) {
+        EpiArgs e{};
+        e.bias = bias; e.res = t32; e.res_stats = xst; e.res_g = lg; e.res_b = lb; e.out = t32; e.ldc = H;
+        return e;
+    };
     for (int li = 0; li < cf.layers; ++li) {
         const Layer& L = m->layers[li];
         const bool last = li == cf.layers - 1;
+        // LayerNorm that produced this layer's input (embeddings LN, or the previous BertOutput LN)
+        const float* pg = li ? m->layers[li - 1].g2 : m->eg;
+        const float* pb = li ? m->layers[li - 1].be2 : m->eb;
         ep = EpiArgs{};
         ep.bias = L.bqkv; ep.out = qkv; ep.ldc = 3 * H;
         if (int r = gemm(m, st, RS_K_QKV, qkv_epi, h16, L.wqkv, rows, 3 * H, kx * H, ep, last ? 2 * H : 3 * H)) return r;
@@ -264,14 +276,14 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
                 ProfScope ps(m, st, RS_K_ATTN, 0);
                 HIPTRY(launch_attention_full(qkv, q32, sm, c.s0, c.s1, 0, H, nh, ctx, kx, st));
             }
-            ep = EpiArgs{}; ep.bias = L.bo; ep.res = h32; ep.out = t32; ep.ldc = H;
-            if (int r = gemm(m, st, RS_K_OPROJ, EPI_RES_F32, ctx, L.wo, rows, H, kx * H, ep, H)) return r;
-            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(t32, rows, L.g1, L.be1, cf.ln_eps, H, h32, h16, kx, st)); }
+            ep = resln_ep(L.bo, pg, pb);
+            if (int r = gemm(m, st, RS_K_OPROJ, EPI_RESLN_F32, ctx, L.wo, rows, H, kx * H, ep, H)) return r;
+            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(t32, rows, L.g1, L.be1, cf.ln_eps, H, nullptr, xst, h16, kx, st)); }
             ep = gelu_ep(L.b1, inter);
             if (int r = gemm(m, st, RS_K_FFN1, EPI_GELU_F16, h16, L.w1, rows, F, kx * H, ep, F)) return r;
-            ep = EpiArgs{}; ep.bias = L.b2; ep.res = h32; ep.out = t32; ep.ldc = H;
-            if (int r = gemm(m, st, RS_K_FFN2, EPI_RES_F32, inter, L.w2, rows, H, kx * F, ep, H)) return r;
-            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(t32, rows, L.g2, L.be2, cf.ln_eps, H, h32, h16, kx, st)); }
+            ep = resln_ep(L.b2, L.g1, L.be1);
+            if (int r = gemm(m, st, RS_K_FFN2, EPI_RESLN_F32, inter, L.w2, rows, H, kx * F, ep, H)) return r;
+            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(t32, rows, L.g2, L.be2, cf.ln_eps, H, nullptr, xst, h16, kx, st)); }
         } else {
             // last layer: only the scored row of every sequence (one row per sequence)
             f16* ctxq = m->ctxq.as<f16>();
@@ -282,16 +294,16 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
             f16* interq = m->interq.as<f16>();
             {
                 ProfScope ps(m, st, RS_K_ATTN, 0);
-                HIPTRY(launch_attention_query(qkv, q32, h32, sm, c.s0, c.s1, 0, H, nh, ctxq, resq, kx, st));
+                HIPTRY(launch_attention_query(qkv, q32, t32, xst, pg, pb, sm, c.s0, c.s1, 0, H, nh, ctxq, resq, kx, st));
             }
             ep = EpiArgs{}; ep.bias = L.bo; ep.res = resq; ep.out = tq; ep.ldc = H;
             if (int r = gemm(m, st, RS_K_OPROJ, EPI_RES_F32, ctxq, L.wo, ns, H, kx * H, ep, H)) return r;
-            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(tq, ns, L.g1, L.be1, cf.ln_eps, H, hq32, hq16, kx, st)); }
+            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(tq, ns, L.g1, L.be1, cf.ln_eps, H, hq32, nullptr, hq16, kx, st)); }
             ep = gelu_ep(L.b1, interq);
             if (int r = gemm(m, st, RS_K_FFN1, EPI_GELU_F16, hq16, L.w1, ns, F, kx * H, ep, F)) return r;
             ep = EpiArgs{}; ep.bias = L.b2; ep.res = hq32; ep.out = tq; ep.ldc = H;
             if (int r = gemm(m, st, RS_K_FFN2, EPI_RES_F32, interq, L.w2, ns, H, kx * F, ep, H)) return r;
-            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(tq, ns, L.g2, L.be2, cf.ln_eps, H, hq32, hq16, kx, st)); }
+            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(tq, ns, L.g2, L.be2, cf.ln_eps, H, hq32, nullptr, hq16, kx, st)); }
         }
     }
     float* hq32 = m->hq32.as<float>();
@@ -300,7 +312,7 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
     if (mode == MODE_MLM) {
         ep = EpiArgs{}; ep.bias = m->bt; ep.out = tq; ep.ldc = H;
         if (int r = gemm(m, st, RS_K_DECODER, EPI_GELU_F32, hq16, m->wt, ns, H, kx * H, ep, H)) return r;
-        { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(tq, ns, m->gt, m->bet, cf.ln_eps, H, hq32, hq16, kx, st)); }
+        { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(tq, ns, m->gt, m->bet, cf.ln_eps, H, hq32, nullptr, hq16, kx, st)); }
         int* lab = m->lab.as<int>();
         float* ll = m->llog.as<float>();
         { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_gather_labels(d_tok, sm, c.s0, c.s1, lab, st)); }
@@ -625,7 +637,7 @@ void rs_model_destroy(rs_model* m) {
     (void)hipSetDevice(m->device);
     (void)hipDeviceSynchronize();
     for (void* p : m->allocs) (void)hipFree(p);
-    for (DevBuf* b : {&m->h32, &m->h16, &m->t32, &m->qkv, &m->ctx, &m->inter, &m->ctxq, &m->resq,
+    for (DevBuf* b : {&m->xst, &m->h16, &m->t32, &m->qkv, &m->ctx, &m->inter, &m->ctxq, &m->resq,
                       &m->tq32, &m->hq32, &m->hq16, &m->interq, &m->lab, &m->llog, &m->part,
                       &m->rowlp_tmp, &m->meta, &m->hypoff})
         b->release();
