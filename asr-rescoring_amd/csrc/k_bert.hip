@@ -18,6 +18,8 @@
 // (mean, rstd): its consumers (the next residual GEMM's accumulator init, attention_query)
 // rebuild LN(x) with ln_apply, so no LN kernel writes an fp32 copy of its output.
 #include "common.h"
+#include <stdlib.h>
+#include <string.h>
 
 namespace {
 
@@ -324,6 +326,128 @@ attn_mfma_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int 
     }
 }
 
+// One wave per (sequence, head), MFMA, latency-lean variant:
+//  * K fragments (A operand of X = K.Q^T) go straight from HBM into registers and stay
+//    resident across the query tiles (T <= 64: one key block, loaded once);
+//  * V is staged ROW-major in LDS with ds_write_b128 and its transposed fragments (A operand
+//    of O^T = V^T.P^T) are read with ds_read_b64_tr_b16 (gfx950 hardware transpose): no
+//    scalar transposing writes.  V row stride 96 halfs makes those reads conflict-free
+//    (the 8 (row, 16-column) blocks of a 32-lane half land on disjoint 8-bank ranges);
+//  * all of a key block's global loads are in flight before the first is consumed.
+// Numerics are those of attn_mfma_kernel (fp16 P, fp32 accumulation, online softmax).
+__global__ void __launch_bounds__(64, 3)
+attn_tr_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
+               f16* __restrict__ ctx, int kx) {
+    typedef __fp16 fp16x4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
+    constexpr int VR = 96;
+    __shared__ __attribute__((aligned(16))) f16 sV[64 * VR];
+    const int s = s0 + blockIdx.x, hd = blockIdx.y;
+    const int T = sm.len[s], rs = sm.row[s] - row0;
+    const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5;
+    const int ld = 3 * H;
+    const f16* base = qkv + (size_t)rs * ld + hd * 64;
+    const float scale = 0.125f;                   // head_dim ** -0.5
+    const int nkb = (T + 63) >> 6;
+    // transposed-read role: 16-lane group g reads keys 4(g>>1) + q (+8), dims 16(g&1) + 4p
+    const int g4 = lane >> 4, tq = (lane >> 2) & 3, tp = lane & 3;
+    const int tr_off = (4 * (g4 >> 1) + tq) * VR + 16 * (g4 & 1) + 4 * tp;
+    auto tr_read = [&](const f16* p) {
+        const fp16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) fp16x4*)p);
+        return __builtin_bit_cast(half4, v);
+    };
+
+    half8 kf[2][4];
+    auto load_kv = [&](int k0) {
+        half8 v[8];
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int kr = it * 8 + (lane >> 3), d0 = (lane & 7) * 8;
+            v[it] = k0 + kr < T ? *(const half8*)(base + (size_t)(k0 + kr) * ld + 2 * H + d0) : (half8){};
+        }
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int ks = 0; ks < 4; ++ks) {
+                const int key = k0 + kt * 32 + r;
+                kf[kt][ks] = key < T ? *(const half8*)(base + (size_t)key * ld + H + ks * 16 + hf * 8) : (half8){};
+            }
+        __syncthreads();                          // previous block's V reads are done
+#pragma unroll
+        for (int it = 0; it < 8; ++it)
+            *(half8*)(sV + (it * 8 + (lane >> 3)) * VR + (lane & 7) * 8) = v[it];
+        __syncthreads();
+    };
+
+    for (int q0 = 0; q0 < T; q0 += 32) {
+        const int t = q0 + r;
+        half8 qf[4];
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+            qf[ks] = t < T ? *(const half8*)(base + (size_t)t * ld + ks * 16 + hf * 8) : (half8){};
+        f32x16 o[2] = {(f32x16){}, (f32x16){}};  // O^T[d tile], lane = query
+        float m = -INFINITY, l = 0.f;
+        for (int kb = 0; kb < nkb; ++kb) {
+            const int k0 = kb * 64;
+            if (nkb > 1 || q0 == 0) load_kv(k0);
+#pragma unroll
+            for (int kt = 0; kt < 2; ++kt) {
+                if (k0 + kt * 32 >= T) break;
+                f32x16 x = {};
+#pragma unroll
+                for (int ks = 0; ks < 4; ++ks) x = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf[kt][ks], qf[ks], x, 0, 0, 0);
+                float bm = -INFINITY;
+#pragma unroll
+                for (int j = 0; j < 16; ++j) {
+                    const int kj = k0 + kt * 32 + (j & 3) + 8 * (j >> 2) + 4 * hf;
+                    const float v = kj < T ? x[j] * scale : -INFINITY;
+                    x[j] = v;
+                    bm = fmaxf(bm, v);
+                }
+                bm = fmaxf(bm, __shfl_xor(bm, 32));
+                const float mn = fmaxf(m, bm);
+                const float alpha = __expf(m - mn);
+                half8 pf[2];
+                float ls = 0.f;
+#pragma unroll
+                for (int sk = 0; sk < 2; ++sk)
+#pragma unroll
+                    for (int e = 0; e < 8; ++e) {
+                        const f16 ph = (f16)__expf(x[sk * 8 + e] - mn);
+                        pf[sk][e] = ph;
+                        ls += (float)ph;
+                    }
+                ls += __shfl_xor(ls, 32);
+                l = l * alpha + ls;
+                m = mn;
+#pragma unroll
+                for (int dt = 0; dt < 2; ++dt) {
+#pragma unroll
+                    for (int j = 0; j < 16; ++j) o[dt][j] *= alpha;
+#pragma unroll
+                    for (int sk = 0; sk < 2; ++sk) {
+                        // keys kt*32 + 16 sk + 4 hf + {0..3, 8..11}: the P fragment's key order
+                        const f16* p = sV + (kt * 32 + 16 * sk) * VR + 32 * dt + tr_off;
+                        const half4 lo = tr_read(p), hi = tr_read(p + 8 * VR);
+                        const half8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf[sk], o[dt], 0, 0, 0);
+                    }
+                }
+            }
+        }
+        if (t < T) {
+            const float il = 1.0f / l;
+            f16* orow = ctx + (size_t)(rs + t) * kx * H;
+#pragma unroll
+            for (int dt = 0; dt < 2; ++dt)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+                    put_split4(orow, hd * 64 + dt * 32 + 8 * g + 4 * hf, H, kx,
+                               make_float4(o[dt][4 * g] * il, o[dt][4 * g + 1] * il,
+                                           o[dt][4 * g + 2] * il, o[dt][4 * g + 3] * il));
+        }
+    }
+}
+
 // Last layer: one wave per (sequence, head), only the scored query row.  Lanes over keys
 // for QK^T, lanes over the 64 head dims for P.V.
 template <class QT>
@@ -467,13 +591,21 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
                                  int H, int heads, f16* ctx, int kx, hipStream_t st) {
     if (s1 <= s0) return hipSuccess;
     const dim3 grid(s1 - s0, heads);
-    static const int valu = getenv("RS_ATTN_VALU") ? atoi(getenv("RS_ATTN_VALU")) : 0;
+    // RS_ATTN: "tr" (default, transposed-read MFMA), "mfma" (LDS-transposed V), "valu"
+    static const int kind = [] {
+        const char* v = getenv("RS_ATTN");
+        if (v && !strcmp(v, "valu")) return 2;
+        if (v && !strcmp(v, "mfma")) return 1;
+        return 0;
+    }();
     if (qkv32)
         hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
-    else if (valu)
+    else if (kind == 2)
         hipLaunchKernelGGL(attn_full_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
-    else
+    else if (kind == 1)
         hipLaunchKernelGGL(attn_mfma_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
+    else
+        hipLaunchKernelGGL(attn_tr_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
     return hipGetLastError();
 }
 
