@@ -378,12 +378,20 @@ attn_tr_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
         __syncthreads();
     };
 
+    half8 qn[4];                                  // Q fragments of the next query tile (prefetch)
+    auto load_q = [&](int q0) {
+        const int t = q0 + r;
+#pragma unroll
+        for (int ks = 0; ks < 4; ++ks)
+            qn[ks] = t < T ? *(const half8*)(base + (size_t)t * ld + ks * 16 + hf * 8) : (half8){};
+    };
+    load_q(0);
     for (int q0 = 0; q0 < T; q0 += 32) {
         const int t = q0 + r;
         half8 qf[4];
 #pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-            qf[ks] = t < T ? *(const half8*)(base + (size_t)t * ld + ks * 16 + hf * 8) : (half8){};
+        for (int ks = 0; ks < 4; ++ks) qf[ks] = qn[ks];
+        if (q0 + 32 < T) load_q(q0 + 32);
         f32x16 o[2] = {(f32x16){}, (f32x16){}};  // O^T[d tile], lane = query
         float m = -INFINITY, l = 0.f;
         for (int kb = 0; kb < nkb; ++kb) {
