@@ -741,6 +741,9 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 704: RS_DBG(704); break;
         case 1216: RS_DBG(1216); break;
         case 2240: RS_DBG(2240); break;
+        case 208: RS_DBG(208); break;
+        case 200: RS_DBG(200); break;
+        case 160: RS_DBG(160); break;
         case 6336: RS_DBG(6336); break;
         case 2242: RS_DBG(2242); break;
         case 2243: RS_DBG(2243); break;
