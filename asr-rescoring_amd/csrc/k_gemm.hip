@@ -609,6 +609,237 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Persistent variant for the fp16-output epilogues (fused QKV, BertIntermediate) in the
+// fp16 precision mode (kx = 1).  256x256 tiles, 8 waves (2x4), BK 64, two LDS buffers and
+// the software-pipelined K loop of gemm_f16_kernel; one workgroup per CU walks the tiles
+// t = blockIdx.x, + gridDim.x, ... (gridDim.x a multiple of 8, so a tile keeps the XCD its
+// block runs on and the same bijective XCD remap applies to t).
+// Per tile transition: barrier -> the NEXT tile's stage 0 (buffer 0) and bias are issued ->
+// this tile's epilogue (bias/GELU applied in registers, fp16, transposed through a per-wave
+// slab in buffer 1, whole 128-B row segments stored non-temporally).  The next tile then
+// waits vmcnt(NSTORE): its stage 0 and bias, not the stores (the stores are unconditional,
+// rows < M_pad are all allocated, so NSTORE is exact).  The bias loads are inline asm so the
+// compiler's own (loop-merged, conservative) wait does not drain the stores; the wait asm
+// takes the bias registers as operands, so nothing reads them before it.
+template <int EPI, int VAR>
+__global__ void __launch_bounds__(512)
+gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int n_tiles_n,
+                    int n_tiles, EpiArgs ep) {
+    constexpr int BM = 256, BN = 256, WN = 4, BK = 64, NW = 8;
+    constexpr int A_BYTES = BM * BK * 2, STAGE = (BM + BN) * BK * 2;
+    constexpr int WTM = 128, WTN = 64, TM = 4, TN = 2;
+    constexpr int RB = BK * 2, CPR = BK / 8, RPP = 1024 / RB;
+    constexpr int A_PIECES = BM / RPP, PIECES = (BM + BN) / RPP, PPW = PIECES / NW;
+    constexpr int LDH = WTN + 8;                  // epilogue slab row, halfs (16-B aligned rows)
+    constexpr int NSTORE = TM * 4;                // 16-B stores per wave per tile
+    constexpr int NSUB = BK / 16, NR = TM + TN, NM = TM * TN;
+    static_assert(EPI == EPI_BIAS_F16 || EPI == EPI_GELU_F16, "fp16-output epilogues only");
+    static_assert(NW * 32 * LDH * 2 <= STAGE, "epilogue slab fits in one buffer");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN, wn = wave % WN;
+    const int frow = lane & 31, fh = lane >> 5;
+    const int nk = K / BK;
+
+    int t = blockIdx.x;
+    if (t >= n_tiles) return;
+    auto tile_of = [&](int tt, int& m0, int& n0) {
+        const int xcd = tt & 7, pos = tt >> 3, q = n_tiles >> 3, r = n_tiles & 7;
+        const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+        const int GM = ep.group_m, n_tiles_m = n_tiles / n_tiles_n, per_group = GM * n_tiles_n;
+        const int g = wgid / per_group, loc = wgid - g * per_group;
+        const int gm = min(GM, n_tiles_m - g * GM);
+        const int tn = loc / gm;
+        m0 = (g * GM + (loc - tn * gm)) * BM;
+        n0 = tn * BN;
+    };
+    // Pieces p < 4 of a wave are A rows (p*8 + wave)*8 + lane/8, pieces p >= 4 the same rows
+    // of W: 64 rows apart with a p-independent swizzle ((row>>1)&7 depends on wave and lane
+    // only), so two per-lane bases and a scalar stride address all eight.
+    static_assert(A_PIECES == 4 * NW && PIECES == 8 * NW && RPP == 8, "piece layout");
+    const int lrow = lane / CPR, pc = lane % CPR;
+    const int prow = wave * RPP + lrow;                 // row of piece 0 (and of piece 4 in W)
+    const int pswz = swz<BK>(prow, pc) * 8;
+    const size_t pstride = (size_t)64 * K;              // elements between pieces p and p+1
+    const f16* srcA;
+    const f16* srcW;
+    auto set_src = [&](int m0, int n0) {
+        srcA = A + (size_t)(m0 + prow) * K + pswz;
+        srcW = W + (size_t)(n0 + prow) * K + pswz;
+    };
+    auto stage = [&](int buf, int k0) {
+#pragma unroll
+        for (int p = 0; p < PPW; ++p) {
+            const f16* g = (p < 4 ? srcA + p * pstride : srcW + (p - 4) * pstride) + k0;
+            __builtin_amdgcn_global_load_lds((const void*)g,
+                                             (__attribute__((address_space(3))) void*)(smem + buf * STAGE + (p * NW + wave) * 1024),
+                                             16, 0, 0);
+        }
+    };
+    typedef float f32x4 __attribute__((ext_vector_type(4)));
+    f32x4 bz[TN][4];                              // bias of the tile about to start
+    auto load_bias = [&](int n0) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float* bp = ep.bias + n0 + wn * WTN + 4 * fh + 32 * j + 8 * g;
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bz[j][g]) : "v"(bp) : "memory");
+            }
+    };
+#define RS_PERSIST_WAIT(N)                                                                         \
+    asm volatile("s_waitcnt vmcnt(" #N ")"                                                         \
+                 : "+v"(bz[0][0]), "+v"(bz[0][1]), "+v"(bz[0][2]), "+v"(bz[0][3]), "+v"(bz[1][0]),  \
+                   "+v"(bz[1][1]), "+v"(bz[1][2]), "+v"(bz[1][3])                                   \
+                 :                                                                                  \
+                 : "memory")
+
+    int m0, n0;
+    tile_of(t, m0, n0);
+    set_src(m0, n0);
+    stage(0, 0);
+    load_bias(n0);
+    RS_PERSIST_WAIT(0);
+    const int offA = (wm * WTM + frow) * RB + (swz<BK>(wm * WTM + frow, fh) << 4);
+    const int offB = A_BYTES + (wn * WTN + frow) * RB + (swz<BK>(wn * WTN + frow, fh) << 4);
+    for (;;) {
+        f32x16 acc[TM][TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    acc[i][j][4 * g] = bz[j][g].x;
+                    acc[i][j][4 * g + 1] = bz[j][g].y;
+                    acc[i][j][4 * g + 2] = bz[j][g].z;
+                    acc[i][j][4 * g + 3] = bz[j][g].w;
+                }
+        // ---- K loop: stage kt landed (this tile's stage 0 was waited with the bias)
+        for (int kt = 0; kt < nk; ++kt) {
+            if (kt > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_barrier" ::: "memory");
+            if (kt + 1 < nk) stage((kt + 1) & 1, (kt + 1) * BK);
+            __builtin_amdgcn_sched_barrier(0);
+            const char* sb = smem + (kt & 1) * STAGE;
+            half8 af0[TM], bf0[TN], af1[TM], bf1[TN];
+            auto load_frags = [&](int s, half8 (&af)[TM], half8 (&bf)[TN]) {
+                const int xa = offA ^ (s << 5), xb = offB ^ (s << 5);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) bf[j] = *(const half8*)(sb + xb + j * 32 * RB);
+#pragma unroll
+                for (int i = 0; i < TM; ++i) af[i] = *(const half8*)(sb + xa + i * 32 * RB);
+            };
+            auto mfmas = [&](const half8 (&af)[TM], const half8 (&bf)[TN]) {
+#pragma unroll
+                for (int i = 0; i < TM; ++i)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+            };
+            load_frags(0, af0, bf0);
+            load_frags(1, af1, bf1);
+            mfmas(af0, bf0);
+            load_frags(2, af0, bf0);
+            mfmas(af1, bf1);
+            load_frags(3, af1, bf1);
+            mfmas(af0, bf0);
+            mfmas(af1, bf1);
+            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+#pragma unroll
+            for (int s = 0; s < NSUB - 1; ++s) {
+#pragma unroll
+                for (int r = 0; r < NR; ++r) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+        }
+        // ---- transition: next tile's stage 0 + bias, then this tile's epilogue
+        asm volatile("s_barrier" ::: "memory");      // every wave is done reading the ring
+        // epilogue part 1: bias/GELU, fp16, transposed through the wave's slab (buffer 1) into
+        // whole-row registers; no LDS access follows the next tile's DMA issue below
+        f16* slab = (f16*)(smem + STAGE) + wave * 32 * LDH;
+        const int rr0 = lane >> 3, cc = (lane & 7) * 8;
+        uint4 ov[TM][4];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    float x[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+                    if constexpr (EPI == EPI_GELU_F16) {
+                        const f32x2 a = gelu2((f32x2){x[0], x[1]}), b = gelu2((f32x2){x[2], x[3]});
+                        x[0] = a.x; x[1] = a.y; x[2] = b.x; x[3] = b.y;
+                    }
+                    const half4 h = {(f16)x[0], (f16)x[1], (f16)x[2], (f16)x[3]};
+                    *(half4*)(slab + frow * LDH + 32 * j + 8 * g + 4 * fh) = h;
+                }
+#pragma unroll
+            for (int it = 0; it < 4; ++it) ov[i][it] = *(const uint4*)(slab + (it * 8 + rr0) * LDH + cc);
+        }
+        // part 2: the next tile's stage 0 (buffer 0) and bias
+        const int cm0 = m0, cn0 = n0;
+        t += gridDim.x;
+        const bool more = t < n_tiles;
+        if (more) {
+            tile_of(t, m0, n0);
+            set_src(m0, n0);
+            stage(0, 0);
+            load_bias(n0);
+        }
+        // part 3: this tile's stores (whole 128-B row segments, non-temporal)
+        f16* obase = (f16*)ep.out + (size_t)(cm0 + wm * WTM + rr0) * ep.ldc + cn0 + wn * WTN + cc;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int it = 0; it < 4; ++it)
+                st16<64>((uint4*)(obase + (size_t)(i * 32 + it * 8) * ep.ldc), ov[i][it]);
+        if (!more) break;
+        RS_PERSIST_WAIT(16);
+        static_assert(NSTORE == 16, "RS_PERSIST_WAIT count");
+    }
+#undef RS_PERSIST_WAIT
+}
+
+int n_cus() {
+    static int n = [] {
+        int dev = 0, v = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+        return v > 0 ? v : 256;
+    }();
+    return n;
+}
+
+template <int EPI, int VAR = 0>
+hipError_t launch_persist(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep,
+                          hipStream_t st) {
+    constexpr int smem = 2 * 512 * 64 * 2;
+    if (K % 64 || M_pad % 256 || N_pad % 256) return hipErrorInvalidValue;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_persist_kernel<EPI, VAR>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    const int ntn = N_pad / 256, n_tiles = (M_pad / 256) * ntn;
+    const int cus = n_cus() / 8 * 8;
+    const int grid = n_tiles <= cus ? n_tiles : cus;
+    static const int gm_env = getenv("RS_GEMM_GROUP_M") ? atoi(getenv("RS_GEMM_GROUP_M")) : 0;
+    EpiArgs e2 = ep;
+    e2.group_m = gm_env > 0 ? gm_env : 4;
+    hipLaunchKernelGGL((gemm_persist_kernel<EPI, VAR>), dim3(grid), dim3(512), smem, st, A, W, K, ntn, n_tiles, e2);
+    return hipGetLastError();
+}
+
 template <int BM, int BN, int WM, int WN, int NSTAGE, int BK, int EPI, int VAR = 0>
 hipError_t launch_t(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep,
                     hipStream_t st) {
@@ -666,6 +897,12 @@ hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
         return f16;
     }();
     const int cfg = pick_cfg(N_pad);
+    // RS_GEMM_PERSIST=0 disables the persistent kernel (fp16-output epilogues, kx = 1)
+    static const int persist = getenv("RS_GEMM_PERSIST") ? atoi(getenv("RS_GEMM_PERSIST")) : 1;
+    if constexpr (EPI == EPI_BIAS_F16 || EPI == EPI_GELU_F16) {
+        if (persist && cfg == 0 && (EPI == EPI_BIAS_F16 || ep.kx == 1))
+            return launch_persist<EPI>(A, W, M_pad, N_pad, K, ep, st);
+    }
     if ((nt_mask >> EPI) & 1u) {
         if (cfg == 0) return launch_t<256, 256, 2, 4, 2, 64, EPI, 192>(A, W, M_pad, N_pad, K, ep, st);
         if (cfg == 1) return launch_t<256, 128, 4, 2, 3, 64, EPI, 192>(A, W, M_pad, N_pad, K, ep, st);
@@ -724,6 +961,10 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         default: e = launch_t<128, 128, 2, 2, 2, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;   \
     }
     if (M % 256 || N % 256 || K % 64) return -1;
+    if (cfg == 9) {   // persistent fp16-output kernel
+        e = launch_persist<EPI_BIAS_F16>(a, w, M, N, K, ep, st);
+        return e == hipSuccess ? 0 : -2;
+    }
     switch (dbg) {
         case 0: RS_DBG(0); break;
         case 4: RS_DBG(4); break;
