@@ -657,3 +657,22 @@ hipError_t launch_segsum_f64(const float* row_lp, const int* hyp_seq_off, int n_
     hipLaunchKernelGGL(segsum_f64_kernel, dim3((n_hyp + 255) / 256), dim3(256), 0, st, row_lp, hyp_seq_off, n_hyp, out);
     return hipGetLastError();
 }
+
+// Timing/diagnostic entry (not part of the scoring path): one attention launch over
+// sequences [0, n_seq) with explicit kernel kind (0 tr, 1 mfma, 2 valu); len / row device
+// int32 arrays; qkv fp16 [rows, 3H]; ctx fp16 [rows, H].
+extern "C" int rs_debug_attention(int kind, const void* qkv, const int* len, const int* row, int n_seq,
+                                  int H, int heads, void* ctx, void* stream) {
+    SeqMeta sm{};
+    sm.len = len;
+    sm.row = row;
+    const dim3 grid(n_seq, heads);
+    hipStream_t st = (hipStream_t)stream;
+    if (kind == 0)
+        hipLaunchKernelGGL(attn_tr_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
+    else if (kind == 1)
+        hipLaunchKernelGGL(attn_mfma_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
+    else
+        hipLaunchKernelGGL(attn_full_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
