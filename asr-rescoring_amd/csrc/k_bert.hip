@@ -658,6 +658,26 @@ hipError_t launch_segsum_f64(const float* row_lp, const int* hyp_seq_off, int n_
     return hipGetLastError();
 }
 
+// Diagnostic: the memory skeleton of attn_tr_kernel (same Q/K/V reads per (sequence, head)
+// wave, ctx written) with no math — the access pattern's own cost.
+__global__ void __launch_bounds__(64)
+attn_memskel_kernel(const f16* __restrict__ qkv, SeqMeta sm, int H, f16* __restrict__ ctx, int heads_per_block) {
+    const int s = blockIdx.x;
+    const int T = sm.len[s], rs = sm.row[s];
+    const int lane = threadIdx.x & 63, hd = blockIdx.y * heads_per_block + (threadIdx.x >> 6);
+    const int ld = 3 * H;
+    const f16* base = qkv + (size_t)rs * ld + hd * 64;
+    for (int r0 = 0; r0 < T; r0 += 8) {
+        const int t = r0 + (lane >> 3), d0 = (lane & 7) * 8;
+        if (t < T) {
+            const half8 q = *(const half8*)(base + (size_t)t * ld + d0);
+            const half8 k = *(const half8*)(base + (size_t)t * ld + H + d0);
+            const half8 v = *(const half8*)(base + (size_t)t * ld + 2 * H + d0);
+            *(half8*)(ctx + (size_t)(rs + t) * H + hd * 64 + d0) = q + k + v;
+        }
+    }
+}
+
 // Timing/diagnostic entry (not part of the scoring path): one attention launch over
 // sequences [0, n_seq) with explicit kernel kind (0 tr, 1 mfma, 2 valu); len / row device
 // int32 arrays; qkv fp16 [rows, 3H]; ctx fp16 [rows, H].
@@ -672,7 +692,11 @@ extern "C" int rs_debug_attention(int kind, const void* qkv, const int* len, con
         hipLaunchKernelGGL(attn_tr_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
     else if (kind == 1)
         hipLaunchKernelGGL(attn_mfma_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
-    else
+    else if (kind == 2)
         hipLaunchKernelGGL(attn_full_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
+    else if (kind == 3)
+        hipLaunchKernelGGL(attn_memskel_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, H, (f16*)ctx, 1);
+    else   // kind 4: memory skeleton, 4 heads per 256-thread block
+        hipLaunchKernelGGL(attn_memskel_kernel, dim3(n_seq, heads / 4), dim3(256), 0, st, (const f16*)qkv, sm, H, (f16*)ctx, 4);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
