@@ -660,7 +660,7 @@ hipError_t launch_segsum_f64(const float* row_lp, const int* hyp_seq_off, int n_
 
 // Diagnostic: the memory skeleton of attn_tr_kernel (same Q/K/V reads per (sequence, head)
 // wave, ctx written) with no math — the access pattern's own cost.
-__global__ void __launch_bounds__(64)
+__global__ void __launch_bounds__(256)
 attn_memskel_kernel(const f16* __restrict__ qkv, SeqMeta sm, int H, f16* __restrict__ ctx, int heads_per_block) {
     const int s = blockIdx.x;
     const int T = sm.len[s], rs = sm.row[s];
