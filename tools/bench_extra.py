@@ -1,0 +1,118 @@
+"""Secondary measurements of the SURVEY §8d configurations (not the headline bench line).
+
+  c2  RescoreBert: U=1000 x N=50 synthetic hypotheses -> CLS scores (fp16x3 default and fp16),
+      hypothesis forwards/s and canonical TFLOP/s (5.425 GFLOP per forward at T=34).
+  c4  MLM_PLL on the real-length variant (alfred test length histogram, N=100); a 1/10
+      subsample of the 7176 test utterances (full C4 is ~10.5 M forwards).
+  c5  RMBR CER utility: U=7176 x N=100 real-length hypotheses -> all-pairs edit distances
+      (DP cells/s), MBR scores for k = 2..10, plus the 101-weight AM/LM fusion sweep.
+
+Prints one JSON line per configuration.  usage: python tools/bench_extra.py [c2,c4,c5]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import __graft_entry__  # noqa: E402
+
+__graft_entry__._import_pkg()
+from asr_rescoring_amd import data as D  # noqa: E402
+from asr_rescoring_amd import rerank  # noqa: E402
+from asr_rescoring_amd.weights import BERT_BASE, make_weights  # noqa: E402
+
+
+def _lengths():
+    lc = json.load(open(os.path.join(REPO, "tests", "golden", "alfred_test_lengths.json")))["length_counts"]
+    return np.repeat(np.arange(len(lc)), lc).astype(np.int64)
+
+
+def _timed(fn, steps=2, warmup=1):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def rescorebert_flops(T, s=BERT_BASE):
+    H, F, nl = s.hidden, s.intermediate, s.layers
+    dense = 2 * (4 * H * H + 2 * H * F)
+    return float((nl - 1) * (T * dense + 4 * T * T * H) + 4 * T * H * H
+                 + (2 * H * H + 4 * T * H + 2 * H * H + 4 * H * F) + 2 * H)
+
+
+def c2():
+    from asr_rescoring_amd.scorer import RescoreBertScorer
+    w = make_weights(BERT_BASE, seed=1234, with_cls_linear=True, with_pooler=True)
+    nb = D.synthetic_nbest(1000, 50, seed=1)
+    lens = np.diff(nb.hyp_off)
+    fl = float(sum(rescorebert_flops(int(T)) for T in lens))
+    d_tok = torch.from_numpy(nb.tokens).cuda()
+    out = []
+    for prec in ("fp16x3", "fp16"):
+        sc = RescoreBertScorer(w, BERT_BASE, device=0, max_rows=131072, precision=prec)
+        dt = _timed(lambda: sc.score_nbest(d_tok, nb.hyp_off))
+        sc.close()
+        out.append({"workload": "C2 RescoreBert U=1000 N=50", "precision": prec, "value": round(nb.n_hyp / dt, 1),
+                    "unit": "hypothesis fwd/s", "ms_per_step": round(dt * 1e3, 2),
+                    "achieved_tflops_canonical": round(fl / dt / 1e12, 1)})
+    return out
+
+
+def c4():
+    from asr_rescoring_amd.scorer import PLLScorer
+    w = make_weights(BERT_BASE, seed=1234)
+    sc = PLLScorer(w, BERT_BASE, device=0, max_rows=131072)
+    nb = D.synthetic_nbest(718, 100, seed=1, lengths=_lengths())
+    d_tok = torch.from_numpy(nb.tokens).cuda()
+    dt = _timed(lambda: sc.score_nbest(d_tok, nb.hyp_off), steps=1)
+    sc.close()
+    lens = np.diff(nb.hyp_off)
+    return [{"workload": "C4 MLM_PLL real-length (718 of 7176 utts) N=100", "value": round(nb.n_forwards() / dt, 1),
+             "unit": "masked fwd/s", "forwards": nb.n_forwards(), "mean_T": round(float(np.average(lens, weights=lens - 2)), 2),
+             "ms_per_step": round(dt * 1e3, 1)}]
+
+
+def c5():
+    nb = D.synthetic_nbest(7176, 100, seed=1, lengths=_lengths(), vocab=5000)
+    lens = nb.hyp_len().astype(np.int64)
+    cells = 0
+    for u in range(nb.n_utt):
+        l = lens[nb.utt_off[u]:nb.utt_off[u + 1]]
+        s = int(l.sum())
+        cells += s * s - int((l * l).sum())          # ordered pairs i != j
+    holder = {}
+
+    def pair():
+        holder["ed"], holder["moff"] = rerank.pairwise_edit(nb, 0)
+    dt_pair = _timed(pair)
+    ed, moff = holder["ed"], holder["moff"]
+    dt_mbr = _timed(lambda: [rerank.mbr_scores(nb, k, ed, moff, 0) for k in range(2, 11)])
+    lm = -np.abs(np.random.default_rng(2).normal(40, 10, nb.n_hyp))
+    grid = rerank.weight_grid("norm")
+    am_d, lm_d = torch.from_numpy(nb.am).cuda(), torch.from_numpy(lm).cuda()
+    dt_fuse = _timed(lambda: rerank.fuse_rerank(am_d, lm_d, nb.hyp_len(), nb.utt_off, grid, "norm", 100, 0))
+    return [{"workload": "C5 RMBR CER utility U=7176 N=100 real-length", "value": round(cells / dt_pair / 1e9, 2),
+             "unit": "G DP cells/s (all ordered pairs)", "pairs": int(sum(int(n) * (int(n) - 1) for n in np.diff(nb.utt_off))),
+             "ms_pairwise": round(dt_pair * 1e3, 2), "ms_mbr_k2_10": round(dt_mbr * 1e3, 2),
+             "ms_fusion_sweep_101w": round(dt_fuse * 1e3, 2)}]
+
+
+def main():
+    which = sys.argv[1].split(",") if len(sys.argv) > 1 else ["c2", "c4", "c5"]
+    for name in which:
+        for rec in {"c2": c2, "c4": c4, "c5": c5}[name]():
+            print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()

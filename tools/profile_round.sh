@@ -17,6 +17,12 @@ timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o run --output-format 
 echo "[prof] pmc write"
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $O/write -o run --output-format csv -- \
     python bench.py --utts 20 --steps 1 --warmup 0 --cpu-seconds 0 --no-profile > /dev/null 2> $O/write.err
+echo "[prof] pmc mfma"
+timeout -k 10 600 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d $O/mfma -o run --output-format csv -- \
+    python bench.py --utts 20 --steps 1 --warmup 0 --cpu-seconds 0 --no-profile > /dev/null 2> $O/mfma.err
+python tools/pmc_mfma.py "$(dirname "$(find $O/mfma -name '*counter_collection.csv' | head -1)")" $O/pmc_mfma.json > /dev/null
+echo "[prof] extra configs"
+timeout -k 10 900 python tools/bench_extra.py > $O/bench_extra.jsonl 2> $O/extra.err
 python tools/pmc_summary.py "$(dirname "$(find $O/fetch -name '*counter_collection.csv' | head -1)")" \
     "$(dirname "$(find $O/write -name '*counter_collection.csv' | head -1)")" $O/pmc_gemm_traffic.json > /dev/null
 cp "$(find $O/kt -name '*kernel_stats.csv' | head -1)" $O/kernel_stats.csv
