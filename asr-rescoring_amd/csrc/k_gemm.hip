@@ -907,6 +907,13 @@ hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
         if (cfg == 0) return launch_t<256, 256, 2, 4, 2, 64, EPI, 192>(A, W, M_pad, N_pad, K, ep, st);
         if (cfg == 1) return launch_t<256, 128, 4, 2, 3, 64, EPI, 192>(A, W, M_pad, N_pad, K, ep, st);
     }
+    // RS_GEMM_RESEPI=direct: residual GEMMs store fp32 straight from the accumulators
+    static const int res_direct = [] {
+        const char* v = getenv("RS_GEMM_RESEPI");
+        return v && !strcmp(v, "direct") ? 1 : 0;
+    }();
+    if (EPI == EPI_RESLN_F32 && res_direct && cfg == 0)
+        return launch_t<256, 256, 2, 4, 2, 64, EPI, 160>(A, W, M_pad, N_pad, K, ep, st);
     switch (cfg) {
         case 0: return launch_t<256, 256, 2, 4, 2, 64, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
         case 1: return launch_t<256, 128, 4, 2, 3, 64, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
