@@ -59,6 +59,12 @@ _SIGS = {
     "rs_fuse_rerank": (ctypes.c_int, [P, P, P, P, I32, I32, P, I32, I32, P, P]),
     "rs_corpus_edits": (ctypes.c_int, [P, P, P, I32, I32, P, P]),
     "rs_ref_edit": (ctypes.c_int, [P, P, P, P, P, I32, P, P]),
+    "rs_vocab_load": (P, [ctypes.c_char_p]),
+    "rs_vocab_size": (ctypes.c_int, [P]),
+    "rs_vocab_free": (None, [P]),
+    "rs_tokenize_batch": (I64, [P, ctypes.POINTER(ctypes.c_char_p), I32, I32, P, I64, P]),
+    "rs_json_write_scores": (ctypes.c_int, [ctypes.c_char_p, I32, ctypes.POINTER(ctypes.c_char_p), P,
+                                            ctypes.POINTER(ctypes.c_char_p), P]),
 }
 
 EXPORTED = tuple(_SIGS)

@@ -10,7 +10,8 @@ so weights come from ``checkpoint_path`` (an HF-keyed state_dict, loaded with
 ``torch.load(weights_only=True)`` or safetensors) or, for testing, from the seeded
 generator when ``random_init_seed`` is set.  The tokenizer is ``BertTokenizer``-like
 per-character for CJK (``data.CharTokenizer``) built from the data, unless ``model.vocab``
-names a ``vocab.txt``.  Extra keys: ``precision`` (fp16 / fp16x3), ``max_rows``,
+names a ``vocab.txt`` — then the native BertTokenizer-compatible ``frontend.NativeTokenizer``
+(and score JSON is written by the native ``frontend.json_saving``).  Extra keys: ``precision`` (fp16 / fp16x3), ``max_rows``,
 ``mode`` (rescore fusion formula: norm / legacy / am_norm).
 """
 from __future__ import annotations
@@ -25,7 +26,13 @@ import numpy as np
 
 from . import data as D
 from .config import ArgParser, get
-from .weights import BERT_BASE, BertShape, load_state_dict_file, make_weights
+from .weights import BERT_BASE, load_state_dict_file, make_weights
+
+
+def json_saving(path, data):
+    """util/saving.py:14-16; native writer (frontend.json_saving) for score files."""
+    from .frontend import json_saving as native
+    native(path, data)
 
 
 def _load(path):
@@ -35,10 +42,7 @@ def _load(path):
 def _weights(cfg, kind: str):
     ck = get(cfg, "checkpoint_path")
     if ck and os.path.exists(ck):
-        w = load_state_dict_file(ck)
-        if kind == "cls":    # RescoreBert state_dict: bert.* + linear.*
-            return w
-        return w
+        return load_state_dict_file(ck)   # HF keys (bert.* [+ linear.* for RescoreBert])
     seed = get(cfg, "random_init_seed")
     if seed is None:
         raise FileNotFoundError(f"checkpoint_path {ck!r} not found (set random_init_seed to score with "
@@ -46,22 +50,11 @@ def _weights(cfg, kind: str):
     return make_weights(BERT_BASE, seed=int(seed), with_cls_linear=(kind == "cls"), with_pooler=(kind == "cls"))
 
 
-class VocabTokenizer(D.CharTokenizer):
-    """BertTokenizer-compatible ids from a vocab.txt (one token per line, id = line index);
-    CJK text is split per character as BertTokenizer does."""
-
-    def __init__(self, vocab_path: str):
-        self.vocab = {l.rstrip("\n"): i for i, l in enumerate(open(vocab_path, encoding="utf-8"))}
-
-    def convert_tokens_to_ids(self, toks):
-        unk = self.vocab.get("[UNK]", D.UNK_ID)
-        return [self.vocab.get(t, unk) for t in toks]
-
-
 def _tokenizer(cfg, texts: List[str]):
     v = get(cfg, "model.vocab")
     if v and os.path.exists(v):
-        return VocabTokenizer(v)
+        from .frontend import NativeTokenizer          # BertTokenizer-compatible, native
+        return NativeTokenizer(v)
     chars = sorted({c for t in texts for c in t})
     return D.CharTokenizer(chars)
 
@@ -111,7 +104,7 @@ def mlm_pll(cfg) -> Dict[str, str]:
         else:
             continue
         path = cfg.output_path + f"{split}_lm.json"          # MLM_PLL/main.py:203 naming
-        D.json_saving(path, output_score)
+        json_saving(path, output_score)
         out_files[split] = path
     scorer.close()
     return out_files
@@ -138,7 +131,7 @@ def rescorebert(cfg) -> Dict[str, str]:
         for (u, h), s in zip(keys, scores):
             out[u][h] = float(s)
         path = os.path.join(cfg.output_path, f"{split}_lm.json")
-        D.json_saving(path, out)
+        json_saving(path, out)
         out_files[split] = path
     sc.close()
     return out_files
@@ -169,7 +162,6 @@ def rescore(cfg) -> Dict[str, float]:
     print("best_weight: ", best_w)
     print("dev cer: ", best_cer)
     test_nb, test_lm = split_nb("test")
-    import torch
     arg = rerank.fuse_rerank(test_nb.am, test_lm, test_nb.hyp_len(), test_nb.utt_off, [best_w], mode, n_best,
                              device=_dev(cfg))
     ed = rerank.ref_edits(test_nb, device=_dev(cfg))
@@ -177,7 +169,6 @@ def rescore(cfg) -> Dict[str, float]:
     test_cer = float(edits) / sum(len(r) for r in test_nb.refs)
     log.info("test cer: " + str(test_cer))
     print("test cer: ", test_cer)
-    _ = torch
     return {"best_weight": best_w, "dev_cer": best_cer, "test_cer": test_cer}
 
 
@@ -255,5 +246,3 @@ def main(argv=None):
 if __name__ == "__main__":
     sys.exit(main())
 
-
-_ = BertShape

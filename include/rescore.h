@@ -163,6 +163,31 @@ int rs_ref_edit(const int32_t* d_chars, const int32_t* d_str_off, const int32_t*
                 const int32_t* d_ref_chars, const int32_t* d_ref_off, int32_t n_utt,
                 int32_t* d_ed_ref, void* stream);
 
+/* ---- Native host front end (host-only, no GPU) ------------------------
+ * Replaces the tokenizer calls of MLM_PLL/preprocess.py:9-30 (BertTokenizer.tokenize +
+ * convert_tokens_to_ids per hypothesis text) and RescoreBert/preprocess.py:8-55, and the
+ * score writer util/saving.py:14-16. */
+
+/* Load a BERT vocab.txt (one token per line, id = line index, later duplicates win).
+ * Returns an opaque handle or NULL (rs_last_error-style message not set: path unreadable). */
+void* rs_vocab_load(const char* path);
+int rs_vocab_size(const void* vocab);
+void rs_vocab_free(void* vocab);
+
+/* BertTokenizer(vocab, do_lower_case=True).tokenize + convert_tokens_to_ids for n NFC UTF-8
+ * texts, optionally wrapped in [CLS] .. [SEP] (add_special != 0): the ragged token layout
+ * rs_pll_score / rs_cls_score consume.  ids int32 [cap], off int64 [n+1].  Returns the total
+ * id count (> cap: only the first cap ids were written; call again with a larger buffer),
+ * or < 0 on bad arguments. */
+int64_t rs_tokenize_batch(const void* vocab, const char* const* texts, int32_t n, int32_t add_special,
+                          int32_t* ids, int64_t cap, int64_t* off);
+
+/* {utt_id: {hyp_id: score}} written byte-identical to json.dump(obj, f, indent=4,
+ * ensure_ascii=False) (util/saving.py:14-16); hyp_off int32 [n_utt+1] indexes hyp_ids and
+ * scores (float64, Python repr formatting).  Returns 0 or -1 (file not writable). */
+int rs_json_write_scores(const char* path, int32_t n_utt, const char* const* utt_ids,
+                         const int32_t* hyp_off, const char* const* hyp_ids, const double* scores);
+
 #ifdef __cplusplus
 }
 #endif
