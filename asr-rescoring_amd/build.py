@@ -51,7 +51,7 @@ def build_library(verbose: bool = False) -> str:
         objs = list(ex.map(_compile, srcs))
     if _needs(LIB, objs):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
-        r = subprocess.run(cmd, capture_output=True, text=True)
+        r = subprocess.run(cmd + ["-lpthread"], capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
     if verbose:

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <fstream>
 #include <string>
+#include <thread>
 #include <unordered_map>
 #include <vector>
 
@@ -334,16 +335,36 @@ int64_t rs_tokenize_batch(const void* vocab, const char* const* texts, int n, in
                           int32_t* ids, int64_t cap, int64_t* off) {
     if (!vocab || n < 0 || (n > 0 && (!texts || !off))) return -1;
     const Vocab& v = *(const Vocab*)vocab;
-    std::vector<int> tmp;
+    // independent texts: contiguous slices on up to 16 host threads, concatenated in order
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int nt = (int)std::min<unsigned>(std::min(hw, 16u), (unsigned)std::max(1, n / 2048));
+    std::vector<std::vector<int>> part(nt);
+    std::vector<std::vector<int64_t>> plen(nt);
+    auto work = [&](int w) {
+        const int b = (int)((int64_t)n * w / nt), e = (int)((int64_t)n * (w + 1) / nt);
+        std::vector<int> tmp;
+        for (int h = b; h < e; ++h) {
+            tmp.clear();
+            tokenize(v, texts[h], strlen(texts[h]), add_special != 0, tmp);
+            part[w].insert(part[w].end(), tmp.begin(), tmp.end());
+            plen[w].push_back((int64_t)tmp.size());
+        }
+    };
+    std::vector<std::thread> th;
+    for (int w = 1; w < nt; ++w) th.emplace_back(work, w);
+    work(0);
+    for (auto& t : th) t.join();
     int64_t total = 0;
+    int h = 0;
     off[0] = 0;
-    for (int h = 0; h < n; ++h) {
-        tmp.clear();
-        tokenize(v, texts[h], strlen(texts[h]), add_special != 0, tmp);
-        for (size_t k = 0; k < tmp.size(); ++k)
-            if (ids && total + (int64_t)k < cap) ids[total + k] = tmp[k];
-        total += (int64_t)tmp.size();
-        off[h + 1] = total;
+    for (int w = 0; w < nt; ++w) {
+        for (int64_t k = 0; k < (int64_t)part[w].size(); ++k)
+            if (ids && total + k < cap) ids[total + k] = part[w][k];
+        for (int64_t L : plen[w]) {
+            off[h + 1] = off[h] + L;
+            ++h;
+        }
+        total += (int64_t)part[w].size();
     }
     return total;
 }
