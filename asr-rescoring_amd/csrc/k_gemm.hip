@@ -968,8 +968,9 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         default: e = launch_t<128, 128, 2, 2, 2, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;   \
     }
     if (M % 256 || N % 256 || K % 64) return -1;
-    if (cfg == 9) {   // persistent fp16-output kernel
-        e = launch_persist<EPI_BIAS_F16>(a, w, M, N, K, ep, st);
+    if (cfg == 9 || cfg == 11) {   // persistent fp16-output kernel (11: GELU epilogue)
+        e = cfg == 9 ? launch_persist<EPI_BIAS_F16>(a, w, M, N, K, ep, st)
+                     : launch_persist<EPI_GELU_F16>(a, w, M, N, K, ep, st);
         return e == hipSuccess ? 0 : -2;
     }
     switch (dbg) {

@@ -44,7 +44,11 @@ def main():
             if ref is None:
                 ref = (A[:4096].float() @ W.float().t() + b).half()
             for dbg in dbgs:
-                if dbg in CHECKED:
+                if cfg == 11:      # GELU epilogue: compare against gelu(ref)
+                    _time(fn, cfg, dbg, A, W, b, out, M, N, K, reps=1)
+                    g = torch.nn.functional.gelu(ref.float()).half()
+                    assert (out[:4096].float() - g.float()).abs().max().item() < 0.05 * K ** 0.5
+                elif dbg in CHECKED:
                     _time(fn, cfg, dbg, A, W, b, out, M, N, K, reps=1)
                     err = (out[:4096].float() - ref.float()).abs().max().item()
                     assert err < 0.05 * K ** 0.5, (cfg, dbg, err)
