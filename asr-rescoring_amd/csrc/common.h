@@ -78,11 +78,6 @@ struct SeqMeta {
     const int* row;        // first token row of the sequence (global row index)
 };
 
-__device__ __forceinline__ float gelu_erf(float x) {
-    // transformers GELUActivation = nn.functional.gelu (exact erf form)
-    return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
-}
-
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);

@@ -46,8 +46,8 @@ def main():
             for dbg in dbgs:
                 if cfg == 11:      # GELU epilogue: compare against gelu(ref)
                     _time(fn, cfg, dbg, A, W, b, out, M, N, K, reps=1)
-                    g = torch.nn.functional.gelu(ref.float()).half()
-                    assert (out[:4096].float() - g.float()).abs().max().item() < 0.05 * K ** 0.5
+                    gl = torch.nn.functional.gelu(ref.float()).half()
+                    assert (out[:4096].float() - gl.float()).abs().max().item() < 0.05 * K ** 0.5
                 elif dbg in CHECKED:
                     _time(fn, cfg, dbg, A, W, b, out, M, N, K, reps=1)
                     err = (out[:4096].float() - ref.float()).abs().max().item()
