@@ -76,6 +76,8 @@ struct SeqMeta {
     const int* query;      // row whose last-layer state is scored
     const int* label;      // label id at query, -1 = take tokens[tok_off + query]
     const int* row;        // first token row of the sequence (global row index)
+    const int* urow_h;     // layer-0 dedup: first unique row of the sequence's hypothesis (chunk-local)
+    const int* urow_m;     // layer-0 dedup: the sequence's [MASK] unique row (chunk-local)
 };
 
 __device__ __forceinline__ float wave_sum(float v) {
@@ -111,8 +113,14 @@ hipError_t launch_embed_ln(const int* tok, SeqMeta sm, int s0, int s1, int row0,
                            float2* stats, f16* h16, int kx, hipStream_t st);
 hipError_t launch_ln_rows(const float* x, int rows, const float* g, const float* b, float eps,
                           int H, float* y32, float2* stats, f16* y16, int kx, hipStream_t st);
+// Unique layer-0 rows (dedup): for every hypothesis of the chunk its T rows, and every
+// sequence's [MASK] row, as the fp16 operand image of LN(embedding) (rows of SeqMeta.urow_*)
+hipError_t launch_embed_unique(const int* tok, SeqMeta sm, int s0, int s1, int mask_id, int vocab,
+                               const float* word, const float* pos, const float* type0, const float* g,
+                               const float* b, float eps, int H, f16* h16u, int kx, hipStream_t st);
+// dedup: qkv holds unique rows; sequence s, position t reads row (t == mask_pos ? urow_m : urow_h + t)
 hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0, int s1, int row0,
-                                 int H, int heads, f16* ctx, int kx, hipStream_t st);
+                                 int H, int heads, f16* ctx, int kx, hipStream_t st, bool dedup = false);
 // resq = LN(x32[query row]) (x32 pre-LN, with its row statistics and LN weight / bias)
 hipError_t launch_attention_query(const void* qkv, bool qkv32, const float* x32, const float2* stats,
                                   const float* g, const float* b, SeqMeta sm, int s0, int s1,

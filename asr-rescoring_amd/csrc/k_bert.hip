@@ -53,7 +53,51 @@ __device__ __forceinline__ void ln_store(const float4 (&x)[NV], const float* g, 
         y.z = ln_apply(x[v].z, st, gg.z, bb.z);
         y.w = ln_apply(x[v].w, st, gg.w, bb.w);
         if (y32) *(float4*)(y32 + c) = y;
-        put_split4(y16, c, H, kx, y);
+        if (y16) put_split4(y16, c, H, kx, y);
+    }
+}
+
+// Embedding sum of position t of a sequence (token t, or [MASK] when t == mp): the one
+// expression both the copy-row and the unique-row kernels use (bit-identical rows).
+template <int NV>
+__device__ __forceinline__ void embed_row(const int* tok, int toff, int t, int mp, int mask_id, int vocab,
+                                          const float* word, const float* pos, const float* type0, int lane,
+                                          float4 (&x)[NV]) {
+    constexpr int H = NV * 256;
+    int id = (t == mp) ? mask_id : tok[toff + t];
+    id = min(max(id, 0), vocab - 1);              // out-of-range ids are clamped, never read OOB
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int c = v * 256 + lane * 4;
+        const float4 w = *(const float4*)(word + (size_t)id * H + c);
+        const float4 ty = *(const float4*)(type0 + c);
+        const float4 p = *(const float4*)(pos + (size_t)t * H + c);
+        // transformers order: (inputs_embeds + token_type) + position
+        x[v] = make_float4((w.x + ty.x) + p.x, (w.y + ty.y) + p.y, (w.z + ty.z) + p.z, (w.w + ty.w) + p.w);
+    }
+}
+
+// Layer-0 dedup: block s writes the [MASK] unique row of sequence s, and — when s is the
+// first copy of its hypothesis in the chunk — the hypothesis' T unmasked unique rows.
+template <int NV>
+__global__ void __launch_bounds__(256)
+embed_unique_kernel(const int* __restrict__ tok, SeqMeta sm, int s0, int mask_id, int vocab,
+                    const float* __restrict__ word, const float* __restrict__ pos,
+                    const float* __restrict__ type0, const float* __restrict__ g,
+                    const float* __restrict__ b, float eps, f16* __restrict__ h16u, int kx) {
+    constexpr int H = NV * 256;
+    const int s = s0 + blockIdx.x;
+    const int T = sm.len[s], toff = sm.tok_off[s], mp = sm.mask_pos[s];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const bool first = blockIdx.x == 0 || sm.urow_h[s - 1] != sm.urow_h[s];
+    const int n = first ? T + 1 : 1;
+    for (int k = wave; k < n; k += 4) {
+        const bool masked = k == T || !first;
+        const int t = masked ? mp : k;
+        const size_t r = masked ? (size_t)sm.urow_m[s] : (size_t)(sm.urow_h[s] + k);
+        float4 x[NV];
+        embed_row<NV>(tok, toff, t, masked ? t : -1, mask_id, vocab, word, pos, type0, lane, x);
+        ln_store<NV>(x, g, b, eps, lane, nullptr, nullptr, h16u + r * kx * H, kx);
     }
 }
 
@@ -70,22 +114,12 @@ embed_ln_kernel(const int* __restrict__ tok, SeqMeta sm, int s0, int row0, int m
     const int rs = sm.row[s] - row0;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int t = wave; t < T; t += 4) {
-        int id = (t == mp) ? mask_id : tok[toff + t];
-        id = min(max(id, 0), vocab - 1);          // out-of-range ids are clamped, never read OOB
         float4 x[NV];
-#pragma unroll
-        for (int v = 0; v < NV; ++v) {
-            const int c = v * 256 + lane * 4;
-            const float4 w = *(const float4*)(word + (size_t)id * H + c);
-            const float4 ty = *(const float4*)(type0 + c);
-            const float4 p = *(const float4*)(pos + (size_t)t * H + c);
-            // transformers order: (inputs_embeds + token_type) + position
-            x[v] = make_float4((w.x + ty.x) + p.x, (w.y + ty.y) + p.y, (w.z + ty.z) + p.z, (w.w + ty.w) + p.w);
-        }
+        embed_row<NV>(tok, toff, t, mp, mask_id, vocab, word, pos, type0, lane, x);
         const size_t r = (size_t)(rs + t);
 #pragma unroll
         for (int v = 0; v < NV; ++v) *(float4*)(x32 + r * H + v * 256 + lane * 4) = x[v];
-        ln_store<NV>(x, g, b, eps, lane, nullptr, stats + r, h16 + r * kx * H, kx);
+        ln_store<NV>(x, g, b, eps, lane, nullptr, stats + r, h16 ? h16 + r * kx * H : nullptr, kx);
     }
 }
 
@@ -335,6 +369,9 @@ attn_mfma_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int 
 //    (the 8 (row, 16-column) blocks of a 32-lane half land on disjoint 8-bank ranges);
 //  * all of a key block's global loads are in flight before the first is consumed.
 // Numerics are those of attn_mfma_kernel (fp16 P, fp32 accumulation, online softmax).
+// DEDUP (layer 0): qkv holds the chunk's unique rows; position t of sequence s reads row
+// urow_m[s] when t is its masked position, urow_h[s] + t otherwise.
+template <bool DEDUP>
 __global__ void __launch_bounds__(64, 3)
 attn_tr_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
                f16* __restrict__ ctx, int kx) {
@@ -345,7 +382,15 @@ attn_tr_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
     const int T = sm.len[s], rs = sm.row[s] - row0;
     const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5;
     const int ld = 3 * H;
-    const f16* base = qkv + (size_t)rs * ld + hd * 64;
+    const int ub = DEDUP ? sm.urow_h[s] : rs;
+    const int mp = DEDUP ? sm.mask_pos[s] : -1, um = DEDUP ? sm.urow_m[s] : 0;
+    const f16* base = qkv + (size_t)ub * ld + hd * 64;
+    const f16* mbase = qkv + (size_t)um * ld + hd * 64;
+    // row of position t (the masked copy's [MASK] row lives apart from its hypothesis' rows)
+    auto rowp = [&](int t) -> const f16* {
+        if constexpr (DEDUP) return t == mp ? mbase : base + (size_t)t * ld;
+        else return base + (size_t)t * ld;
+    };
     const float scale = 0.125f;                   // head_dim ** -0.5
     const int nkb = (T + 63) >> 6;
     // transposed-read role: 16-lane group g reads keys 4(g>>1) + q (+8), dims 16(g&1) + 4p
@@ -362,14 +407,14 @@ attn_tr_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
 #pragma unroll
         for (int it = 0; it < 8; ++it) {
             const int kr = it * 8 + (lane >> 3), d0 = (lane & 7) * 8;
-            v[it] = k0 + kr < T ? *(const half8*)(base + (size_t)(k0 + kr) * ld + 2 * H + d0) : (half8){};
+            v[it] = k0 + kr < T ? *(const half8*)(rowp(k0 + kr) + 2 * H + d0) : (half8){};
         }
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
             for (int ks = 0; ks < 4; ++ks) {
                 const int key = k0 + kt * 32 + r;
-                kf[kt][ks] = key < T ? *(const half8*)(base + (size_t)key * ld + H + ks * 16 + hf * 8) : (half8){};
+                kf[kt][ks] = key < T ? *(const half8*)(rowp(key) + H + ks * 16 + hf * 8) : (half8){};
             }
         __syncthreads();                          // previous block's V reads are done
 #pragma unroll
@@ -383,7 +428,7 @@ attn_tr_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
         const int t = q0 + r;
 #pragma unroll
         for (int ks = 0; ks < 4; ++ks)
-            qn[ks] = t < T ? *(const half8*)(base + (size_t)t * ld + ks * 16 + hf * 8) : (half8){};
+            qn[ks] = t < T ? *(const half8*)(rowp(t) + ks * 16 + hf * 8) : (half8){};
     };
     load_q(0);
     for (int q0 = 0; q0 < T; q0 += 32) {
@@ -579,6 +624,23 @@ hipError_t launch_embed_ln(const int* tok, SeqMeta sm, int s0, int s1, int row0,
     return hipGetLastError();
 }
 
+hipError_t launch_embed_unique(const int* tok, SeqMeta sm, int s0, int s1, int mask_id, int vocab,
+                               const float* word, const float* pos, const float* type0, const float* g,
+                               const float* b, float eps, int H, f16* h16u, int kx, hipStream_t st) {
+    const int n = s1 - s0;
+    if (n <= 0) return hipSuccess;
+#define RS_EMBU(NV) hipLaunchKernelGGL(embed_unique_kernel<NV>, dim3(n), dim3(256), 0, st, tok, sm, s0, mask_id, vocab, word, pos, type0, g, b, eps, h16u, kx)
+    switch (H) {
+        case 256: RS_EMBU(1); break;
+        case 512: RS_EMBU(2); break;
+        case 768: RS_EMBU(3); break;
+        case 1024: RS_EMBU(4); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef RS_EMBU
+    return hipGetLastError();
+}
+
 hipError_t launch_ln_rows(const float* x, int rows, const float* g, const float* b, float eps,
                           int H, float* y32, float2* stats, f16* y16, int kx, hipStream_t st) {
     if (rows <= 0) return hipSuccess;
@@ -596,9 +658,14 @@ hipError_t launch_ln_rows(const float* x, int rows, const float* g, const float*
 }
 
 hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0, int s1, int row0,
-                                 int H, int heads, f16* ctx, int kx, hipStream_t st) {
+                                 int H, int heads, f16* ctx, int kx, hipStream_t st, bool dedup) {
     if (s1 <= s0) return hipSuccess;
     const dim3 grid(s1 - s0, heads);
+    if (dedup) {                                  // fp16 QKV, kx == 1 only (host gates it)
+        if (qkv32 || kx != 1 || H % 64) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(attn_tr_kernel<true>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
+        return hipGetLastError();
+    }
     // RS_ATTN: "tr" (default, transposed-read MFMA), "mfma" (LDS-transposed V), "valu"
     static const int kind = [] {
         const char* v = getenv("RS_ATTN");
@@ -613,7 +680,7 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
     else if (kind == 1)
         hipLaunchKernelGGL(attn_mfma_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
     else
-        hipLaunchKernelGGL(attn_tr_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
+        hipLaunchKernelGGL(attn_tr_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
     return hipGetLastError();
 }
 
@@ -689,7 +756,7 @@ extern "C" int rs_debug_attention(int kind, const void* qkv, const int* len, con
     const dim3 grid(n_seq, heads);
     hipStream_t st = (hipStream_t)stream;
     if (kind == 0)
-        hipLaunchKernelGGL(attn_tr_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
+        hipLaunchKernelGGL(attn_tr_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
     else if (kind == 1)
         hipLaunchKernelGGL(attn_mfma_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
     else if (kind == 2)

@@ -57,6 +57,7 @@ struct Layer {
 
 struct Chunk {
     int s0, s1, rows;
+    int urows = 0;     // layer-0 unique rows (dedup mode), 0 = dedup off for this chunk
 };
 
 }  // namespace
@@ -238,6 +239,7 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
     const bool q32 = kx == 3;                 // fp16x3: QKV kept in fp32 for attention
     const int qkv_epi = q32 ? EPI_BIAS_F32 : EPI_BIAS_F16;
     const int rows = c.rows, ns = c.s1 - c.s0;
+    const bool dedup = c.urows > 0;           // layer-0 Q/K/V over unique rows (MLM, fp16, kx == 1)
     float2* xst = m->xst.as<float2>();
     f16* h16 = m->h16.as<f16>();
     float* t32 = m->t32.as<float>();     // residual stream, pre-LN fp32 (LN rebuilt from xst)
@@ -246,8 +248,13 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
     f16* inter = m->inter.as<f16>();
     {
         ProfScope ps(m, st, RS_K_OTHER, 0);
+        // dedup: the per-copy pass keeps only the fp32 residual + LN statistics; the layer-0
+        // GEMM operand is built over the chunk's unique rows (plan_unique_rows)
         HIPTRY(launch_embed_ln(d_tok, sm, c.s0, c.s1, 0, cf.mask_id, cf.vocab, m->word32, m->pos32,
-                               m->type32, m->eg, m->eb, cf.ln_eps, H, t32, xst, h16, kx, st));
+                               m->type32, m->eg, m->eb, cf.ln_eps, H, t32, xst, dedup ? nullptr : h16, kx, st));
+        if (dedup)
+            HIPTRY(launch_embed_unique(d_tok, sm, c.s0, c.s1, cf.mask_id, cf.vocab, m->word32, m->pos32,
+                                       m->type32, m->eg, m->eb, cf.ln_eps, H, h16, kx, st));
     }
     EpiArgs ep{};
     auto gelu_ep = [&](const float* bias, f16* out) {
@@ -270,11 +277,13 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
         const float* pb = li ? m->layers[li - 1].be2 : m->eb;
         ep = EpiArgs{};
         ep.bias = L.bqkv; ep.out = qkv; ep.ldc = 3 * H;
-        if (int r = gemm(m, st, RS_K_QKV, qkv_epi, h16, L.wqkv, rows, 3 * H, kx * H, ep, last ? 2 * H : 3 * H)) return r;
+        const bool uq = dedup && li == 0;
+        if (int r = gemm(m, st, RS_K_QKV, qkv_epi, h16, L.wqkv, uq ? c.urows : rows, 3 * H, kx * H, ep,
+                         last ? 2 * H : 3 * H)) return r;
         if (!last) {
             {
                 ProfScope ps(m, st, RS_K_ATTN, 0);
-                HIPTRY(launch_attention_full(qkv, q32, sm, c.s0, c.s1, 0, H, nh, ctx, kx, st));
+                HIPTRY(launch_attention_full(qkv, q32, sm, c.s0, c.s1, 0, H, nh, ctx, kx, st, uq));
             }
             ep = resln_ep(L.bo, pg, pb);
             if (int r = gemm(m, st, RS_K_OPROJ, EPI_RESLN_F32, ctx, L.wo, rows, H, kx * H, ep, H)) return r;
@@ -330,13 +339,32 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
 
 // Host-side sequence list (structure of arrays) for one call.
 struct SeqList {
-    std::vector<int> tok_off, len, mask, query, label, row;
+    std::vector<int> tok_off, len, mask, query, label, row, urow_h, urow_m;
     void push(int to, int T, int mp, int q, int lb) {
         tok_off.push_back(to); len.push_back(T); mask.push_back(mp); query.push_back(q);
-        label.push_back(lb); row.push_back(0);
+        label.push_back(lb); row.push_back(0); urow_h.push_back(0); urow_m.push_back(0);
     }
     size_t size() const { return len.size(); }
 };
+
+// Layer-0 dedup (MLM_PLL): the masked copies of one hypothesis share every layer-0 input row
+// except the masked one, so the layer-0 QKV projection runs over UNIQUE rows: per hypothesis
+// (within a chunk) its T original rows, then one [MASK] row per copy.  urow_h[s] = first
+// unique row of the hypothesis, urow_m[s] = the copy's masked row (chunk-local).  Returns the
+// chunk's unique-row count, or 0 when a sequence has no mask position (dedup not applicable).
+int plan_unique_rows(SeqList& sl, int s0, int s1) {
+    int u = 0, base = 0;
+    for (int s = s0; s < s1; ++s) {
+        if (sl.mask[s] < 0) return 0;
+        if (s == s0 || sl.tok_off[s] != sl.tok_off[s - 1] || sl.len[s] != sl.len[s - 1]) {
+            base = u;
+            u += sl.len[s];
+        }
+        sl.urow_h[s] = base;
+        sl.urow_m[s] = u++;
+    }
+    return u;
+}
 
 // Chunks the sequence list, uploads metadata, runs every chunk.  out_rows: one float per
 // sequence.  Extra int arrays (e.g. hypothesis -> sequence offsets) ride in the same upload.
@@ -365,10 +393,15 @@ int run_all(rs_model* m, hipStream_t st, const int* d_tok, SeqList& sl, int mode
         rows += T;
     }
     if (S) chunks.push_back({s0, (int)S, rows});
+    // layer-0 dedup: MLM mode, fp16 operands, >= 2 layers (layer 0 is not the query-only layer)
+    const char* dedup_s = getenv("RS_DEDUP");      // read per call (tests flip it)
+    const int dedup_env = dedup_s ? atoi(dedup_s) : 1;
+    if (dedup_env && mode == MODE_MLM && m->kx == 1 && m->cfg.layers >= 2)
+        for (Chunk& c : chunks) c.urows = plan_unique_rows(sl, c.s0, c.s1);
 
     // one upload of all metadata through a pinned staging buffer
     const size_t n_extra = extra ? extra->size() : 0;
-    const size_t n_int = 6 * S + n_extra;
+    const size_t n_int = 8 * S + n_extra;
     if (m->upload_done) HIPTRY(hipEventSynchronize(m->upload_done));
     if (n_int > m->pinned_cap) {
         if (m->pinned) (void)hipHostFree(m->pinned);
@@ -378,17 +411,18 @@ int run_all(rs_model* m, hipStream_t st, const int* d_tok, SeqList& sl, int mode
         m->pinned_cap = n_int;
     }
     int* p = m->pinned;
-    const std::vector<int>* cols[6] = {&sl.tok_off, &sl.len, &sl.mask, &sl.query, &sl.label, &sl.row};
-    for (int k = 0; k < 6; ++k) std::memcpy(p + k * S, cols[k]->data(), S * 4);
-    if (n_extra) std::memcpy(p + 6 * S, extra->data(), n_extra * 4);
+    const std::vector<int>* cols[8] = {&sl.tok_off, &sl.len, &sl.mask, &sl.query, &sl.label, &sl.row,
+                                       &sl.urow_h, &sl.urow_m};
+    for (int k = 0; k < 8; ++k) std::memcpy(p + k * S, cols[k]->data(), S * 4);
+    if (n_extra) std::memcpy(p + 8 * S, extra->data(), n_extra * 4);
     HIPTRY(m->meta.ensure(std::max<size_t>(n_int, 1) * 4));
     HIPTRY(hipMemcpyAsync(m->meta.p, p, n_int * 4, hipMemcpyHostToDevice, st));
     if (!m->upload_done) HIPTRY(hipEventCreateWithFlags(&m->upload_done, hipEventDisableTiming));
     HIPTRY(hipEventRecord(m->upload_done, st));
     int* d = m->meta.as<int>();
     if (d_label) HIPTRY(hipMemcpyAsync(d + 4 * S, d_label, S * 4, hipMemcpyDeviceToDevice, st));
-    SeqMeta sm{d, d + S, d + 2 * S, d + 3 * S, d + 4 * S, d + 5 * S};
-    if (d_extra) *d_extra = d + 6 * S;
+    SeqMeta sm{d, d + S, d + 2 * S, d + 3 * S, d + 4 * S, d + 5 * S, d + 6 * S, d + 7 * S};
+    if (d_extra) *d_extra = d + 8 * S;
     for (const Chunk& c : chunks)
         if (int r = run_chunk(m, st, d_tok, sm, c, mode, out_rows)) return r;
     return RS_OK;

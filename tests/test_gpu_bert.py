@@ -190,3 +190,22 @@ def test_oracle_parity_base_synthetic(pll_base, w_base):
     _, ref = pll_reference_pattern(TorchBert(w_base, BERT_BASE), nb.tokens, nb.hyp_off, batch_size=64,
                                    full_head=False)
     assert rel_err(got, ref).max() < REL
+
+
+@pytest.mark.parametrize("max_rows", [512, 65536])
+def test_layer0_dedup_is_exact(w_tiny, w_base, max_rows, monkeypatch):
+    """Layer-0 Q/K/V over unique rows (RS_DEDUP=1, default) vs over every masked copy
+    (RS_DEDUP=0): the same rows go through the same GEMM, so scores are bitwise equal.
+    max_rows=512 splits hypotheses across chunks (a hypothesis' rows re-planned per chunk)."""
+    from asr_rescoring_amd.scorer import PLLScorer
+    for w, cfg, seed in ((w_tiny, BERT_TINY, 5), (w_base, BERT_BASE, 6)):
+        nb = D.synthetic_nbest(5, 4, seed=seed, vocab=cfg.vocab, len_lo=1, len_hi=70)
+        s = PLLScorer(w, cfg, device=0, max_rows=max_rows)
+        try:
+            monkeypatch.setenv("RS_DEDUP", "1")
+            a = s.score(nb)
+            monkeypatch.setenv("RS_DEDUP", "0")
+            b = s.score(nb)
+        finally:
+            s.close()
+        assert np.array_equal(a, b), np.abs(a - b).max()
