@@ -16,7 +16,7 @@ import torch  # noqa: F401  (must load torch's HIP runtime before librescore.so)
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "librescore.so")
 
-RS_HEAD_MLM, RS_HEAD_CLS = 1, 2
+RS_HEAD_MLM, RS_HEAD_CLS, RS_HEAD_EMB = 1, 2, 4
 RS_FUSE = {"norm": 0, "legacy": 1, "am_norm": 2}
 KINDS = ["qkv", "oproj", "ffn1", "ffn2", "decoder", "attn", "other"]
 
@@ -56,6 +56,9 @@ _SIGS = {
     "rs_model_destroy": (None, [P]),
     "rs_pairwise_edit": (ctypes.c_int, [P, P, P, P, I32, I32, P, P]),
     "rs_mbr_scores": (ctypes.c_int, [P, P, P, P, I32, I32, P, P, P]),
+    "rs_mbr_scores_bs": (ctypes.c_int, [P, P, P, I32, I32, I32, P, P, P]),
+    "rs_token_embed": (ctypes.c_int, [P, P, P, I32, P, P]),
+    "rs_bertscore_recall": (ctypes.c_int, [P, P, P, P, I32, P, P]),
     "rs_fuse_rerank": (ctypes.c_int, [P, P, P, P, I32, I32, P, I32, I32, P, P]),
     "rs_corpus_edits": (ctypes.c_int, [P, P, P, I32, I32, P, P]),
     "rs_ref_edit": (ctypes.c_int, [P, P, P, P, P, I32, P, P]),

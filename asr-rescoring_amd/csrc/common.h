@@ -118,6 +118,13 @@ hipError_t launch_ln_rows(const float* x, int rows, const float* g, const float*
 hipError_t launch_embed_unique(const int* tok, SeqMeta sm, int s0, int s1, int mask_id, int vocab,
                                const float* word, const float* pos, const float* type0, const float* g,
                                const float* b, float eps, int H, f16* h16u, int kx, hipStream_t st);
+// BERTScore recall matrix (k_bertscore.hip); items = (utterance, j0, j1, -) ref-column runs
+hipError_t launch_bertscore_recall(const f16* emb, int H, const int* hyp_off, const int* utt_off,
+                                   const long long* mat_off, const int4* items, int n_items, float* rmat,
+                                   hipStream_t st);
+// Last hidden state, L2-normalised per token, fp16 at out[(tok_off + t) * H] (BERTScore)
+hipError_t launch_embed_out(const float* x32, const float2* stats, const float* g, const float* b,
+                            SeqMeta sm, int s0, int s1, int row0, int H, f16* out, hipStream_t st);
 // dedup: qkv holds unique rows; sequence s, position t reads row (t == mask_pos ? urow_m : urow_h + t)
 hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0, int s1, int row0,
                                  int H, int heads, f16* ctx, int kx, hipStream_t st, bool dedup = false);

@@ -641,6 +641,59 @@ hipError_t launch_embed_unique(const int* tok, SeqMeta sm, int s0, int s1, int m
     return hipGetLastError();
 }
 
+// BERTScore embeddings (bert_score bert_encode + greedy_cos_idf's row normalisation):
+// e = LN(x) of the last layer, rebuilt from the pre-LN stream, then e / ||e||_2 in fp32,
+// stored fp16 at the token's position in the caller's ragged token layout.
+template <int NV>
+__global__ void __launch_bounds__(256)
+embed_out_kernel(const float* __restrict__ x32, const float2* __restrict__ stats,
+                 const float* __restrict__ g, const float* __restrict__ b, SeqMeta sm, int s0,
+                 int row0, f16* __restrict__ out) {
+    constexpr int H = NV * 256;
+    const int s = s0 + blockIdx.x;
+    const int T = sm.len[s], rs = sm.row[s] - row0, toff = sm.tok_off[s];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int t = wave; t < T; t += 4) {
+        const size_t r = (size_t)(rs + t);
+        const float2 st = stats[r];
+        float4 y[NV];
+        float q = 0.f;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const int c = v * 256 + lane * 4;
+            const float4 x = *(const float4*)(x32 + r * H + c);
+            const float4 gg = *(const float4*)(g + c), bb = *(const float4*)(b + c);
+            y[v] = make_float4(ln_apply(x.x, st, gg.x, bb.x), ln_apply(x.y, st, gg.y, bb.y),
+                               ln_apply(x.z, st, gg.z, bb.z), ln_apply(x.w, st, gg.w, bb.w));
+            q += y[v].x * y[v].x + y[v].y * y[v].y + y[v].z * y[v].z + y[v].w * y[v].w;
+        }
+        const float nrm = sqrtf(wave_sum(q));
+        f16* o = out + (size_t)(toff + t) * H;
+#pragma unroll
+        for (int v = 0; v < NV; ++v) {
+            const int c = v * 256 + lane * 4;
+            const half4 h = {(f16)(y[v].x / nrm), (f16)(y[v].y / nrm), (f16)(y[v].z / nrm), (f16)(y[v].w / nrm)};
+            *(half4*)(o + c) = h;
+        }
+    }
+}
+
+hipError_t launch_embed_out(const float* x32, const float2* stats, const float* g, const float* b,
+                            SeqMeta sm, int s0, int s1, int row0, int H, f16* out, hipStream_t st) {
+    const int n = s1 - s0;
+    if (n <= 0) return hipSuccess;
+#define RS_EO(NV) hipLaunchKernelGGL(embed_out_kernel<NV>, dim3(n), dim3(256), 0, st, x32, stats, g, b, sm, s0, row0, out)
+    switch (H) {
+        case 256: RS_EO(1); break;
+        case 512: RS_EO(2); break;
+        case 768: RS_EO(3); break;
+        case 1024: RS_EO(4); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef RS_EO
+    return hipGetLastError();
+}
+
 hipError_t launch_ln_rows(const float* x, int rows, const float* g, const float* b, float eps,
                           int H, float* y32, float2* stats, f16* y16, int kx, hipStream_t st) {
     if (rows <= 0) return hipSuccess;

@@ -171,6 +171,34 @@ __global__ void mbr_scores_kernel(const int* __restrict__ ed, const long long* _
     argmax[u] = bi;
 }
 
+// RMBR mbr_decode with the BERTScore utility: sim(i, j) = P/R/F of cand hyp_i against
+// ref hyp_j from the recall matrix (P(i|j) = R(j|i)), summed like the CER utility.
+#pragma clang fp contract(off)
+__global__ void mbr_scores_bs_kernel(const float* __restrict__ rmat, const long long* __restrict__ mat_off,
+                                     const int* __restrict__ utt_off, int n_utt, int k, int which,
+                                     float* __restrict__ scores, int* __restrict__ argmax) {
+    const int u = blockIdx.x * blockDim.x + threadIdx.x;
+    if (u >= n_utt) return;
+    const int n = utt_off[u + 1] - utt_off[u];
+    const long long mo = mat_off[u];
+    float best = 0.f;
+    int bi = 0;
+    for (int i = 0; i < k; ++i) {
+        auto get = [&](int t) -> float {
+            const int j = t < i ? t : t + 1;
+            const float r = rmat[mo + (long long)i * n + j], p = rmat[mo + (long long)j * n + i];
+            if (which == RS_BS_R) return r;
+            if (which == RS_BS_P) return p;
+            const float f = __fdiv_rn(__fmul_rn(__fmul_rn(2.0f, p), r), __fadd_rn(p, r));
+            return f != f ? 0.f : f;              // bert_score: F.masked_fill(isnan(F), 0)
+        };
+        const float sc = torch_sum_f32(k - 1, get);
+        scores[(long long)u * k + i] = sc;
+        if (i == 0 || sc > best) { best = sc; bi = i; }
+    }
+    argmax[u] = bi;
+}
+
 #pragma clang fp contract(off)
 __global__ void fuse_rerank_kernel(const double* __restrict__ am, const double* __restrict__ lm,
                                    const int* __restrict__ len, const int* __restrict__ utt_off,
@@ -251,6 +279,15 @@ int rs_mbr_scores(const int32_t* d_ed, const int64_t* d_mat_off, const int32_t* 
     if (n_utt == 0) return RS_OK;
     hipLaunchKernelGGL(mbr_scores_kernel, dim3((n_utt + 63) / 64), dim3(64), 0, (hipStream_t)stream, d_ed,
                        (const long long*)d_mat_off, d_utt_off, d_len, n_utt, k, d_scores, d_argmax);
+    return hipGetLastError() == hipSuccess ? RS_OK : RS_EHIP;
+}
+
+int rs_mbr_scores_bs(const float* d_rmat, const int64_t* d_mat_off, const int32_t* d_utt_off, int32_t n_utt,
+                     int32_t k, int32_t which, float* d_scores, int32_t* d_argmax, void* stream) {
+    if (n_utt < 0 || k < 1 || k > 512 || which < RS_BS_P || which > RS_BS_F) return RS_EARG;
+    if (n_utt == 0) return RS_OK;
+    hipLaunchKernelGGL(mbr_scores_bs_kernel, dim3((n_utt + 63) / 64), dim3(64), 0, (hipStream_t)stream, d_rmat,
+                       (const long long*)d_mat_off, d_utt_off, n_utt, k, which, d_scores, d_argmax);
     return hipGetLastError() == hipSuccess ? RS_OK : RS_EHIP;
 }
 

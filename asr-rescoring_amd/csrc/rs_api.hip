@@ -81,6 +81,11 @@ struct rs_model {
     DevBuf xst, h16, t32, qkv, ctx, inter;   // xst: (mean, rstd) of the pre-LN rows in t32
     DevBuf ctxq, resq, tq32, hq32, hq16, interq, lab, llog, part, rowlp_tmp;
     DevBuf meta, hypoff;
+    f16* emb_dst = nullptr;     // MODE_EMB output (rs_token_embed / rs_bertscore_recall)
+    DevBuf emb, plan;           // rs_bertscore_recall: token embeddings, work-item plan
+    int* pinned_plan = nullptr;
+    size_t pinned_plan_cap = 0;
+    hipEvent_t plan_done = nullptr;
     std::vector<int> pinned_dummy;
     int* pinned = nullptr;
     size_t pinned_cap = 0;
@@ -229,7 +234,7 @@ int gemm(rs_model* m, hipStream_t st, int kind, int epi, const f16* A, const f16
     return RS_OK;
 }
 
-enum Mode { MODE_MLM = 0, MODE_CLS = 1 };
+enum Mode { MODE_MLM = 0, MODE_CLS = 1, MODE_EMB = 2 };
 
 // Runs the encoder + head over sequences [c.s0, c.s1) (one chunk).
 int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, const Chunk& c,
@@ -271,7 +276,7 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
     };
     for (int li = 0; li < cf.layers; ++li) {
         const Layer& L = m->layers[li];
-        const bool last = li == cf.layers - 1;
+        const bool last = mode != MODE_EMB && li == cf.layers - 1;   // query-row-only layer
         // LayerNorm that produced this layer's input (embeddings LN, or the previous BertOutput LN)
         const float* pg = li ? m->layers[li - 1].g2 : m->eg;
         const float* pb = li ? m->layers[li - 1].be2 : m->eb;
@@ -314,6 +319,12 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
             if (int r = gemm(m, st, RS_K_FFN2, EPI_RES_F32, interq, L.w2, ns, H, kx * F, ep, H)) return r;
             { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(tq, ns, L.g2, L.be2, cf.ln_eps, H, hq32, nullptr, hq16, kx, st)); }
         }
+    }
+    if (mode == MODE_EMB) {
+        const Layer& L = m->layers[cf.layers - 1];
+        ProfScope ps(m, st, RS_K_OTHER, 0);
+        HIPTRY(launch_embed_out(t32, xst, L.g2, L.be2, sm, c.s0, c.s1, 0, H, m->emb_dst, st));
+        return RS_OK;
     }
     float* hq32 = m->hq32.as<float>();
     f16* hq16 = m->hq16.as<f16>();
@@ -459,7 +470,7 @@ int rs_model_create(const rs_bert_cfg* cfg, int device, rs_model** out) {
     if (c.heads <= 0 || c.hidden / c.heads != 64 || c.hidden % c.heads) return fail(RS_EUNSUP, "head_dim must be 64");
     if (c.intermediate <= 0 || c.intermediate % 128) return fail(RS_EUNSUP, "intermediate must be a multiple of 128");
     if (c.layers < 1 || c.vocab < 1 || c.max_pos < 3 || c.type_vocab < 1) return fail(RS_EARG, "bad config");
-    if (!(c.heads_mask & (RS_HEAD_MLM | RS_HEAD_CLS))) return fail(RS_EARG, "heads_mask selects no head");
+    if (!(c.heads_mask & (RS_HEAD_MLM | RS_HEAD_CLS | RS_HEAD_EMB))) return fail(RS_EARG, "heads_mask selects no head");
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n)
         return fail(RS_EHIP, "no such HIP device");
@@ -649,6 +660,85 @@ int rs_cls_score(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, in
     return run_all(m, (hipStream_t)stream, d_tok, sl, MODE_CLS, d_out, nullptr, nullptr);
 }
 
+int rs_token_embed(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, int32_t n_hyp,
+                   void* d_emb, void* stream) {
+    if (!m || !h_hyp_off || n_hyp < 0 || (n_hyp > 0 && (!d_tok || !d_emb))) return fail(RS_EARG, "null argument");
+    if (n_hyp == 0) return RS_OK;
+    SeqList sl;
+    for (int h = 0; h < n_hyp; ++h) {
+        const int o = h_hyp_off[h], T = h_hyp_off[h + 1] - o;
+        if (o < 0 || T < 1) return fail(RS_EARG, "hypothesis " + std::to_string(h) + " is empty");
+        sl.push(o, T, -1, 0, 0);
+    }
+    m->emb_dst = (f16*)d_emb;
+    const int r = run_all(m, (hipStream_t)stream, d_tok, sl, MODE_EMB, nullptr, nullptr, nullptr);
+    m->emb_dst = nullptr;
+    return r;
+}
+
+int rs_bertscore_recall(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off,
+                        const int32_t* h_utt_off, int32_t n_utt, float* d_rmat, void* stream) {
+    if (!m || !h_hyp_off || !h_utt_off || n_utt < 0 || (n_utt > 0 && (!d_tok || !d_rmat)))
+        return fail(RS_EARG, "null argument");
+    if (n_utt == 0) return RS_OK;
+    if (h_utt_off[0] != 0) return fail(RS_EARG, "utt_off[0] must be 0");
+    const int n_hyp = h_utt_off[n_utt];
+    for (int u = 0; u < n_utt; ++u)
+        if (h_utt_off[u + 1] < h_utt_off[u]) return fail(RS_EARG, "utt_off not ascending");
+    if (h_hyp_off[0] != 0) return fail(RS_EARG, "hyp_off[0] must be 0");
+    for (int h = 0; h < n_hyp; ++h)
+        if (h_hyp_off[h + 1] - h_hyp_off[h] < 2)
+            return fail(RS_EARG, "hypothesis " + std::to_string(h) + " has fewer than 2 tokens ([CLS] [SEP])");
+    hipStream_t st = (hipStream_t)stream;
+    HIPTRY(hipSetDevice(m->device));
+    const int H = m->cfg.hidden;
+    const size_t n_tok = (size_t)h_hyp_off[n_hyp];
+    HIPTRY(m->emb.ensure(std::max<size_t>(n_tok, 1) * H * 2));
+    if (int r = rs_token_embed(m, d_tok, h_hyp_off, n_hyp, m->emb.p, stream)) return r;
+    // plan: runs of whole ref hypotheses fitting one 64-column tile (a longer one alone)
+    std::vector<int> items;
+    std::vector<long long> moff(n_utt + 1, 0);
+    for (int u = 0; u < n_utt; ++u) {
+        const int h0 = h_utt_off[u], n = h_utt_off[u + 1] - h0;
+        moff[u + 1] = moff[u] + (long long)n * n;
+        for (int j = 0; j < n;) {
+            int j1 = j + 1, cols = h_hyp_off[h0 + j + 1] - h_hyp_off[h0 + j];
+            while (cols <= 64 && j1 < n && cols + h_hyp_off[h0 + j1 + 1] - h_hyp_off[h0 + j1] <= 64) {
+                cols += h_hyp_off[h0 + j1 + 1] - h_hyp_off[h0 + j1];
+                ++j1;
+            }
+            items.insert(items.end(), {u, j, j1, 0});
+            j = j1;
+        }
+    }
+    const int n_items = (int)(items.size() / 4);
+    // one upload: items | mat_off (int64) | hyp_off | utt_off
+    const size_t w_items = items.size(), w_moff = 2 * (size_t)(n_utt + 1);
+    const size_t n_int = w_items + w_moff + (size_t)(n_hyp + 1) + (size_t)(n_utt + 1);
+    if (m->plan_done) HIPTRY(hipEventSynchronize(m->plan_done));
+    if (n_int > m->pinned_plan_cap) {
+        if (m->pinned_plan) (void)hipHostFree(m->pinned_plan);
+        m->pinned_plan = nullptr;
+        m->pinned_plan_cap = 0;
+        HIPTRY(hipHostMalloc((void**)&m->pinned_plan, n_int * 4, hipHostMallocDefault));
+        m->pinned_plan_cap = n_int;
+    }
+    int* p = m->pinned_plan;
+    std::memcpy(p, items.data(), w_items * 4);
+    std::memcpy(p + w_items, moff.data(), w_moff * 4);
+    std::memcpy(p + w_items + w_moff, h_hyp_off, (size_t)(n_hyp + 1) * 4);
+    std::memcpy(p + w_items + w_moff + n_hyp + 1, h_utt_off, (size_t)(n_utt + 1) * 4);
+    HIPTRY(m->plan.ensure(n_int * 4));
+    HIPTRY(hipMemcpyAsync(m->plan.p, p, n_int * 4, hipMemcpyHostToDevice, st));
+    if (!m->plan_done) HIPTRY(hipEventCreateWithFlags(&m->plan_done, hipEventDisableTiming));
+    HIPTRY(hipEventRecord(m->plan_done, st));
+    int* d = m->plan.as<int>();
+    ProfScope ps(m, st, RS_K_OTHER, 0);
+    HIPTRY(launch_bertscore_recall(m->emb.as<f16>(), H, d + w_items + w_moff, d + w_items + w_moff + n_hyp + 1,
+                                   (const long long*)(d + w_items), (const int4*)d, n_items, d_rmat, st));
+    return RS_OK;
+}
+
 int rs_profile_enable(rs_model* m, int on) {
     if (!m) return fail(RS_EARG, "null model");
     prof_collect(m);
@@ -673,9 +763,11 @@ void rs_model_destroy(rs_model* m) {
     for (void* p : m->allocs) (void)hipFree(p);
     for (DevBuf* b : {&m->xst, &m->h16, &m->t32, &m->qkv, &m->ctx, &m->inter, &m->ctxq, &m->resq,
                       &m->tq32, &m->hq32, &m->hq16, &m->interq, &m->lab, &m->llog, &m->part,
-                      &m->rowlp_tmp, &m->meta, &m->hypoff})
+                      &m->rowlp_tmp, &m->meta, &m->hypoff, &m->emb, &m->plan})
         b->release();
     if (m->pinned) (void)hipHostFree(m->pinned);
+    if (m->pinned_plan) (void)hipHostFree(m->pinned_plan);
+    if (m->plan_done) (void)hipEventDestroy(m->plan_done);
     if (m->upload_done) (void)hipEventDestroy(m->upload_done);
     for (hipEvent_t e : m->ev_pool) (void)hipEventDestroy(e);
     delete m;

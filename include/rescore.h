@@ -37,6 +37,11 @@ extern "C" {
 
 #define RS_HEAD_MLM 1     /* BertForMaskedLM head: cls.predictions.* (MLM_PLL) */
 #define RS_HEAD_CLS 2     /* RescoreBert head: linear.weight [1,H], linear.bias [1] */
+#define RS_HEAD_EMB 4     /* encoder only: token embeddings (BERTScore, bert_score.utils.bert_encode) */
+
+#define RS_BS_P 0         /* BERTScore component used as the MBR utility */
+#define RS_BS_R 1
+#define RS_BS_F 2
 
 #define RS_FUSE_NORM 0    /* (1-w)*am/len + w*lm/len      rescore.py:51 */
 #define RS_FUSE_LEGACY 1  /* (1-w)*am + w*lm              rescore_result/MLM_PLL/rescore.log:28 */
@@ -134,6 +139,30 @@ void rs_model_destroy(rs_model* m);
 int rs_pairwise_edit(const int32_t* d_chars, const int32_t* d_str_off, const int32_t* d_utt_off,
                      const int64_t* d_mat_off, int32_t n_utt, int32_t max_n, int32_t* d_ed,
                      void* stream);
+
+/* Token embeddings of the BERTScore utility (RMBR/utility_functions.py:9-22 ->
+ * bert_score.utils.get_bert_embedding / bert_encode with the model truncated to cfg.layers
+ * layers — bert_score uses 8 for bert-base-chinese — and greedy_cos_idf's per-token L2
+ * normalisation): d_emb fp16 [hyp_off[n_hyp], hidden], row = token position in d_tok
+ * (h_hyp_off: host int32 [n_hyp+1], hypotheses as [CLS] w.. [SEP]). */
+int rs_token_embed(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, int32_t n_hyp,
+                   void* d_emb, void* stream);
+
+/* bert_score.score(cands=[hyp_i], refs=[hyp_j], idf=False) for every ordered pair of each
+ * utterance's hypotheses, as the recall matrix
+ *   d_rmat[mat_off(u) + i*n_u + j] = R(cand = hyp_i, ref = hyp_j),
+ *   mat_off(u) = sum_{v<u} n_v^2 (n_u = h_utt_off[u+1] - h_utt_off[u]);
+ * P(i|j) = R(j|i), F = 2PR/(P+R).  R = mean over ref j's tokens except [CLS]/[SEP] of the max
+ * cosine over all of cand i's tokens; 0 when either hypothesis is empty (T == 2).
+ * h_hyp_off[0] == 0, h_utt_off[0] == 0 (host arrays); every hypothesis has T >= 2. */
+int rs_bertscore_recall(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off,
+                        const int32_t* h_utt_off, int32_t n_utt, float* d_rmat, void* stream);
+
+/* RMBR mbr_decode (RMBR/mbr.py:5-28) with the BERTScore utility component `which`
+ * (RS_BS_P/R/F) of cand hyp_i against ref hyp_j, from the rs_bertscore_recall matrix;
+ * summation and argmax as rs_mbr_scores. */
+int rs_mbr_scores_bs(const float* d_rmat, const int64_t* d_mat_off, const int32_t* d_utt_off, int32_t n_utt,
+                     int32_t k, int32_t which, float* d_scores, int32_t* d_argmax, void* stream);
 
 /* RMBR mbr_decode scores for top-k (RMBR/mbr.py:17-22):
  *   score[u][i] = float32 torch-CPU-order sum over j != i (j < k) of

@@ -6,8 +6,10 @@
       subsample of the 7176 test utterances (full C4 is ~10.5 M forwards).
   c5  RMBR CER utility: U=7176 x N=100 real-length hypotheses -> all-pairs edit distances
       (DP cells/s), MBR scores for k = 2..10, plus the 101-weight AM/LM fusion sweep.
+  c5bs RMBR BERTScore utility at the C5 shape: 8-layer bert-base token embeddings + the
+      all-pairs greedy-cosine recall matrix, MBR for k = 2..10.
 
-Prints one JSON line per configuration.  usage: python tools/bench_extra.py [c2,c4,c5]
+Prints one JSON line per configuration.  usage: python tools/bench_extra.py [c2,c4,c5,c5bs]
 """
 import json
 import os
@@ -107,10 +109,41 @@ def c5():
              "ms_fusion_sweep_101w": round(dt_fuse * 1e3, 2)}]
 
 
+def c5bs():
+    """BERTScore utility at the C5 shape: bert-base (8 of 12 layers, bert_score's truncation)
+    embeddings of every hypothesis token + the greedy-cosine recall matrix of all ordered pairs."""
+    from asr_rescoring_amd import bertscore as BS
+    w = make_weights(BERT_BASE, seed=1234)
+    nb = D.synthetic_nbest(7176, 100, seed=1, lengths=_lengths())
+    sc = BS.BertScorer(w, BERT_BASE, num_layers=8, device=0, max_rows=131072)
+    d_tok = torch.from_numpy(nb.tokens).cuda()
+    rows = int(nb.hyp_off[-1])
+    T = np.diff(nb.hyp_off).astype(np.int64)
+    sT = np.add.reduceat(T, nb.utt_off[:-1]).astype(np.float64)
+    H = BERT_BASE.hidden
+    enc_fl = float(rows) * 8 * 2 * (4 * H * H + 2 * H * BERT_BASE.intermediate) + 8 * 4 * float((T * T).sum()) * H
+    sim_fl = 2.0 * H * float((sT * sT).sum())
+    dt_emb = _timed(lambda: sc.embed(d_tok, nb.hyp_off))
+    holder = {}
+
+    def rec():
+        holder["r"] = sc.recall_matrix(d_tok, nb.hyp_off, nb.utt_off)
+    dt_all = _timed(rec)
+    rmat, moff = holder["r"]
+    dt_mbr = _timed(lambda: [BS.mbr_scores(rmat, moff, nb.utt_off, k, "R") for k in range(2, 11)])
+    sc.close()
+    dt_sim = max(dt_all - dt_emb, 1e-9)
+    return [{"workload": "C5 RMBR BERTScore utility U=7176 N=100 real-length, bert-base 8 layers",
+             "value": round(int(moff[-1]) / dt_all / 1e6, 2), "unit": "M ordered pairs/s (embeddings included)",
+             "tokens": rows, "ms_total": round(dt_all * 1e3, 1), "ms_embed": round(dt_emb * 1e3, 1),
+             "ms_recall_kernel": round(dt_sim * 1e3, 1), "embed_tflops": round(enc_fl / dt_emb / 1e12, 1),
+             "recall_tflops_algorithmic": round(sim_fl / dt_sim / 1e12, 1), "ms_mbr_k2_10": round(dt_mbr * 1e3, 2)}]
+
+
 def main():
-    which = sys.argv[1].split(",") if len(sys.argv) > 1 else ["c2", "c4", "c5"]
+    which = sys.argv[1].split(",") if len(sys.argv) > 1 else ["c2", "c4", "c5", "c5bs"]
     for name in which:
-        for rec in {"c2": c2, "c4": c4, "c5": c5}[name]():
+        for rec in {"c2": c2, "c4": c4, "c5": c5, "c5bs": c5bs}[name]():
             print(json.dumps(rec), flush=True)
 
 
