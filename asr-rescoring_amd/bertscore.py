@@ -129,12 +129,15 @@ def mbr_decode(scorer: BertScorer, nb: NBest, k: int, which: str = "R") -> Tuple
     return mbr_scores(rmat, moff, nb.utt_off, k, which)
 
 
-def find_best_length(scorer: BertScorer, nb: NBest, n_best: int, which: str = "R"
-                     ) -> Tuple[float, int, np.ndarray]:
-    """RMBR/main.py:15-35 with the BERTScore utility: (best_cer, best_length, best scores)."""
+def find_best_length(scorer: BertScorer, nb: NBest, n_best: int, which: str = "R",
+                     nb_chars: NBest | None = None) -> Tuple[float, int, np.ndarray]:
+    """RMBR/main.py:15-35 with the BERTScore utility: (best_cer, best_length, best scores).
+    ``nb`` holds the model's token ids; ``nb_chars`` (same hypotheses, character symbols)
+    is what the CER is measured on — ``nb`` itself when omitted."""
     rmat, moff = scorer.recall_matrix(nb.tokens, nb.hyp_off, nb.utt_off)
-    ed_ref = ref_edits(nb, scorer.device)
-    total = sum(len(r) for r in nb.refs)
+    nc = nb_chars if nb_chars is not None else nb
+    ed_ref = ref_edits(nc, scorer.device)
+    total = sum(len(r) for r in nc.refs)
     best_cer, best_len, best_sc = float("inf"), 2, None
     for k in range(2, n_best + 1):
         am, sc = mbr_scores(rmat, moff, nb.utt_off, k, which)

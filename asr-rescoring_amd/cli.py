@@ -3,7 +3,7 @@
   python -m asr_rescoring_amd.cli mlm_pll     --config score.yaml    # MLM_PLL/main.py (task: scoring)
   python -m asr_rescoring_amd.cli rescorebert --config MD_score.yaml # RescoreBert/main.py (task: scoring)
   python -m asr_rescoring_amd.cli rescore     --config rescore.yaml  # rescore.py
-  python -m asr_rescoring_amd.cli rmbr        --config CER.yaml      # RMBR/main.py (utility: cer)
+  python -m asr_rescoring_amd.cli rmbr        --config CER.yaml      # RMBR/main.py (utility: cer / bertscore)
 
 Differences forced by the offline image (no model hub): ``model.bert`` cannot be fetched,
 so weights come from ``checkpoint_path`` (an HF-keyed state_dict, loaded with
@@ -173,23 +173,48 @@ def rescore(cfg) -> Dict[str, float]:
 
 
 def rmbr(cfg) -> Dict[str, float]:
-    """RMBR/main.py:38-108 with utility_function: cer."""
+    """RMBR/main.py:38-108; utility_function: cer (RMBR/utility_functions.py:28-33) or
+    bertscore (:9-22, bert_score restated on the HIP path: ``bertscore.BertScorer``, weights
+    from checkpoint_path / random_init_seed, ``bertscore_layers`` (8), ``bertscore_component``
+    (P / R / F, default R))."""
     from . import rerank
-    if get(cfg, "utility_function", "cer") != "cer":
-        raise NotImplementedError("only the CER utility runs offline (bert_score is not available)")
+    util = str(get(cfg, "utility_function", "cer")).lower().replace("_", "")
+    if util not in ("cer", "bertscore"):
+        raise ValueError(f"unknown utility_function {util!r} (cer, bertscore)")
     os.makedirs(cfg.output_path, exist_ok=True)
     log = _logger(os.path.join(cfg.output_path, "mbr.log"))
     n_best, max_utt = cfg.n_best, get(cfg, "max_utt", 1 << 30)
+    scorer = tok = None
+    if util == "bertscore":
+        from . import bertscore as BS
+        scorer = BS.BertScorer(_weights(cfg, "mlm"), BERT_BASE, num_layers=get(cfg, "bertscore_layers", 8),
+                               device=_dev(cfg), max_rows=get(cfg, "max_rows", 65536),
+                               precision=get(cfg, "precision", "fp16"))
+        which = str(get(cfg, "bertscore_component", "R")).upper()
 
     def split_nb(prefix):
+        nonlocal tok
         feats, paths = getattr(cfg, f"{prefix}_feature"), getattr(cfg, f"{prefix}_feature_path")
         refs = _load(paths[feats.index("ref_text")])
         hyps = _load(paths[feats.index("hyps_text")])
-        return D.from_texts(hyps, refs, None, n_best=n_best, max_utt=max_utt)
+        nb = D.from_texts(hyps, refs, None, n_best=n_best, max_utt=max_utt)
+        if scorer is None:
+            return nb, None
+        if tok is None:
+            tok = _tokenizer(cfg, [t for h in hyps.values() for t in h.values()])
+        return nb, _nbest_tokens(hyps, tok, max_utt, n_best)[0]
 
-    dev = split_nb("dev")
+    def decode(nb, nb_tok, k):
+        if scorer is None:
+            return rerank.mbr_decode(nb, k, device=_dev(cfg))
+        return BS.mbr_decode(scorer, nb_tok, k, which)
+
+    dev, dev_tok = split_nb("dev")
     log.info("Running MBR on dev set to find best length ...")
-    best_cer, best_len, best_sc = rerank.find_best_length(dev, n_best, device=_dev(cfg))
+    if scorer is None:
+        best_cer, best_len, best_sc = rerank.find_best_length(dev, n_best, device=_dev(cfg))
+    else:
+        best_cer, best_len, best_sc = BS.find_best_length(scorer, dev_tok, n_best, which, nb_chars=dev)
     log.info(f"best_cer: {best_cer}")
     log.info(f"best_length: {best_len}")
     print("best_cer: ", best_cer)
@@ -197,9 +222,9 @@ def rmbr(cfg) -> Dict[str, float]:
     res = {"best_cer": best_cer, "best_length": best_len}
     for split, nb, sc in (("dev", dev, best_sc), ("test", None, None)):
         if split == "test":
-            nb = split_nb("test")
+            nb, nb_tok = split_nb("test")
             log.info("Running MBR on test set ...")
-            idx, sc = rerank.mbr_decode(nb, best_len, device=_dev(cfg))
+            idx, sc = decode(nb, nb_tok, best_len)
             import torch
             ed = rerank.ref_edits(nb, device=_dev(cfg))
             arg = torch.from_numpy(idx.astype(np.int32)).to(ed.device)[None, :]
@@ -213,6 +238,8 @@ def rmbr(cfg) -> Dict[str, float]:
             for (hid, _), v in zip(hyps.items(), row):
                 out[uid][hid] = v
         D.json_saving(os.path.join(cfg.output_path, f"{split}_MBR.json"), out)
+    if scorer is not None:
+        scorer.close()
     return res
 
 

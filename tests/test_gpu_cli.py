@@ -67,3 +67,30 @@ def test_cli_c1_pipeline(c1):
     assert res2["best_length"] == bl and res2["best_cer"] == bc
     mbr = json.load(open(d / "mbr_out" / "test_MBR.json", encoding="utf-8"))
     assert list(mbr) == g["utt_ids"]
+
+
+def test_cli_rmbr_bertscore(c1):
+    """RMBR with utility_function: bertscore (8-layer bert-base, seeded weights) on the C1
+    texts: dev_MBR.json scores at the chosen length equal the oracle's bert_score MBR."""
+    from asr_rescoring_amd import cli
+    from asr_rescoring_amd.frontend import NativeTokenizer
+    from asr_rescoring_amd.weights import BERT_BASE, make_weights
+    from oracle import bertscore_ref as B
+    g, d = c1
+    res = cli.rmbr(cli.ArgParser().parse(["--config", _cfg(d, "BertScore.yaml", {
+        "device": "cuda:0", "utility_function": "bertscore", "random_init_seed": 1234,
+        "model": {"bert": "bert-base-chinese", "vocab": str(d / "vocab.txt")},
+        "dev_feature": ["ref_text", "hyps_text"], "test_feature": ["ref_text", "hyps_text"],
+        "dev_feature_path": [str(d / "ref_text.json"), str(d / "hyps_text.json")],
+        "test_feature_path": [str(d / "ref_text.json"), str(d / "hyps_text.json")],
+        "dev_output_format": str(d / "hyps_score.json"), "test_output_format": str(d / "hyps_score.json"),
+        "output_path": str(d / "mbr_bs_out"), "max_utt": 99999999, "n_best": 10})]))
+    assert 2 <= res["best_length"] <= 10 and 0.0 <= res["best_cer"] <= 1.0
+    tok = NativeTokenizer(str(d / "vocab.txt"))
+    utts = [[[101] + tok.encode(t) + [102] for t in list(g["hyps_text"][u].values())[:10]] for u in g["utt_ids"]]
+    model = B.truncated_model(make_weights(BERT_BASE, seed=1234), BERT_BASE, 8)
+    k = res["best_length"]
+    _, want = B.mbr_decode(k, B.utility_matrices(model, utts, "R"))
+    mbr = json.load(open(d / "mbr_bs_out" / "dev_MBR.json", encoding="utf-8"))
+    got = np.array([list(mbr[u].values())[:k] for u in g["utt_ids"]], np.float32)
+    assert np.allclose(got, want, rtol=1e-3, atol=1e-5)
