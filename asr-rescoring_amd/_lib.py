@@ -30,6 +30,13 @@ class RsBertCfg(ctypes.Structure):
 
 
 RS_PREC = {"fp16": 0, "fp16x3": 1}
+RS_LOSS = {"MD": 0, "MD_MWER": 1, "MD_MWED": 2}
+
+
+class RsTrainOpts(ctypes.Structure):
+    _fields_ = [("loss", ctypes.c_int32), ("lambda_", ctypes.c_float), ("lr", ctypes.c_float),
+                ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float),
+                ("weight_decay", ctypes.c_float), ("update", ctypes.c_int32)]
 
 
 class RescoreError(RuntimeError):
@@ -58,6 +65,13 @@ _SIGS = {
     "rs_mbr_scores": (ctypes.c_int, [P, P, P, P, I32, I32, P, P, P]),
     "rs_mbr_scores_bs": (ctypes.c_int, [P, P, P, I32, I32, I32, P, P, P]),
     "rs_token_embed": (ctypes.c_int, [P, P, P, I32, P, P]),
+    "rs_trainer_create": (ctypes.c_int, [ctypes.POINTER(RsBertCfg), ctypes.c_int, ctypes.POINTER(P)]),
+    "rs_trainer_set_tensor": (ctypes.c_int, [P, ctypes.c_char_p, P, ctypes.c_int, ctypes.POINTER(I64), ctypes.c_int]),
+    "rs_trainer_finalize": (ctypes.c_int, [P]),
+    "rs_train_step_cls": (ctypes.c_int, [P, P, P, I32, P, I32, P, P, P, ctypes.POINTER(RsTrainOpts), P, P, P]),
+    "rs_trainer_get_tensor": (ctypes.c_int, [P, ctypes.c_char_p, P, I64]),
+    "rs_trainer_get_grad": (ctypes.c_int, [P, ctypes.c_char_p, P, I64]),
+    "rs_trainer_destroy": (None, [P]),
     "rs_bertscore_recall": (ctypes.c_int, [P, P, P, P, I32, P, P]),
     "rs_fuse_rerank": (ctypes.c_int, [P, P, P, P, I32, I32, P, I32, I32, P, P]),
     "rs_corpus_edits": (ctypes.c_int, [P, P, P, I32, I32, P, P]),

@@ -51,7 +51,8 @@ def build_library(verbose: bool = False) -> str:
         objs = list(ex.map(_compile, srcs))
     if _needs(LIB, objs):
         cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
-        r = subprocess.run(cmd + ["-lpthread"], capture_output=True, text=True)
+        # rocBLAS: fp32 GEMMs of the trainer (its soname matches the copy torch loads first)
+        r = subprocess.run(cmd + ["-L/opt/rocm/lib", "-lrocblas", "-lpthread"], capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
     if verbose:

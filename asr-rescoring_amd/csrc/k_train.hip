@@ -1,0 +1,585 @@
+// Training kernels (RescoreBert distillation training, backward through
+// the BERT encoder).  fp32 throughout — the reference trains in fp32 — with every reduction
+// in a fixed order (no float atomics): a training step is bitwise reproducible.
+// GEMMs are plain (transposed) fp32 GEMMs and go to rocBLAS (train_api.hip); everything
+// else is here.  One wave per token row for row-wise ops; column reductions in two stages
+// (64-row partials, then an ordered sum).
+#include "common.h"
+#include "train.h"
+
+namespace {
+
+constexpr float kInvSqrt2 = 0.70710678118654752f;
+constexpr float kInvSqrt2Pi = 0.39894228040143268f;
+
+template <int NV>
+__device__ __forceinline__ void ln_fwd_row(const float4 (&x)[NV], const float* g, const float* b, float eps,
+                                           int lane, float2* st, float* h) {
+    constexpr int H = NV * 256;
+    float s = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) s += (x[v].x + x[v].y) + (x[v].z + x[v].w);
+    const float mean = wave_sum(s) / (float)H;
+    float q = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const float a = x[v].x - mean, bb = x[v].y - mean, c = x[v].z - mean, d = x[v].w - mean;
+        q += (a * a + bb * bb) + (c * c + d * d);
+    }
+    const float rstd = 1.0f / sqrtf(wave_sum(q) / (float)H + eps);
+    if (lane == 0) *st = make_float2(mean, rstd);
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int c = v * 256 + lane * 4;
+        const float4 gg = *(const float4*)(g + c), bb = *(const float4*)(b + c);
+        *(float4*)(h + c) = make_float4((x[v].x - mean) * rstd * gg.x + bb.x, (x[v].y - mean) * rstd * gg.y + bb.y,
+                                        (x[v].z - mean) * rstd * gg.z + bb.z, (x[v].w - mean) * rstd * gg.w + bb.w);
+    }
+}
+
+// x0 = word[tok] + type[0] + pos[t]; h0 = LN(x0)
+template <int NV>
+__global__ void __launch_bounds__(256)
+tr_embed_ln_kernel(const int* __restrict__ row_tok, const int* __restrict__ row_pos, int M, int vocab,
+                   const float* __restrict__ word, const float* __restrict__ pos, const float* __restrict__ type0,
+                   const float* __restrict__ g, const float* __restrict__ b, float eps, float* __restrict__ x0,
+                   float2* __restrict__ st, float* __restrict__ h0) {
+    constexpr int H = NV * 256;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= M) return;
+    const int id = min(max(row_tok[row], 0), vocab - 1), t = row_pos[row];
+    float4 x[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int c = v * 256 + lane * 4;
+        const float4 w = *(const float4*)(word + (size_t)id * H + c);
+        const float4 ty = *(const float4*)(type0 + c);
+        const float4 p = *(const float4*)(pos + (size_t)t * H + c);
+        x[v] = make_float4((w.x + ty.x) + p.x, (w.y + ty.y) + p.y, (w.z + ty.z) + p.z, (w.w + ty.w) + p.w);
+        *(float4*)(x0 + (size_t)row * H + c) = x[v];
+    }
+    ln_fwd_row<NV>(x, g, b, eps, lane, st + row, h0 + (size_t)row * H);
+}
+
+// y <- (y + bias) + res (pre-LN, saved), h = LN(y)
+template <int NV>
+__global__ void __launch_bounds__(256)
+tr_bias_res_ln_kernel(float* __restrict__ y, const float* __restrict__ bias, const float* __restrict__ res,
+                      int M, const float* __restrict__ g, const float* __restrict__ b, float eps,
+                      float2* __restrict__ st, float* __restrict__ h) {
+    constexpr int H = NV * 256;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= M) return;
+    float4 x[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int c = v * 256 + lane * 4;
+        const float4 a = *(const float4*)(y + (size_t)row * H + c);
+        const float4 bb = *(const float4*)(bias + c);
+        const float4 r = *(const float4*)(res + (size_t)row * H + c);
+        x[v] = make_float4((a.x + bb.x) + r.x, (a.y + bb.y) + r.y, (a.z + bb.z) + r.z, (a.w + bb.w) + r.w);
+        *(float4*)(y + (size_t)row * H + c) = x[v];
+    }
+    ln_fwd_row<NV>(x, g, b, eps, lane, st + row, h + (size_t)row * H);
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * kInvSqrt2)); }
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+    return 0.5f * (1.0f + erff(x * kInvSqrt2)) + x * kInvSqrt2Pi * __expf(-0.5f * x * x);
+}
+
+// pre <- pre + bias; act = gelu(pre)   (N % 4 == 0)
+__global__ void tr_bias_gelu_kernel(float* __restrict__ pre, const float* __restrict__ bias, float* __restrict__ act,
+                                    long long n4, int N) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+        const int c = (int)((i * 4) % N);
+        float4 v = ((float4*)pre)[i];
+        const float4 bb = *(const float4*)(bias + c);
+        v = make_float4(v.x + bb.x, v.y + bb.y, v.z + bb.z, v.w + bb.w);
+        ((float4*)pre)[i] = v;
+        ((float4*)act)[i] = make_float4(gelu_erf(v.x), gelu_erf(v.y), gelu_erf(v.z), gelu_erf(v.w));
+    }
+}
+
+// dact <- dact * gelu'(pre)
+__global__ void tr_gelu_bwd_kernel(float* __restrict__ d, const float* __restrict__ pre, long long n4) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+        float4 v = ((float4*)d)[i];
+        const float4 p = ((const float4*)pre)[i];
+        ((float4*)d)[i] = make_float4(v.x * gelu_erf_grad(p.x), v.y * gelu_erf_grad(p.y), v.z * gelu_erf_grad(p.z),
+                                      v.w * gelu_erf_grad(p.w));
+    }
+}
+
+__global__ void tr_bias_kernel(float* __restrict__ y, const float* __restrict__ bias, long long n4, int N) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+        const int c = (int)((i * 4) % N);
+        float4 v = ((float4*)y)[i];
+        const float4 bb = *(const float4*)(bias + c);
+        ((float4*)y)[i] = make_float4(v.x + bb.x, v.y + bb.y, v.z + bb.z, v.w + bb.w);
+    }
+}
+
+// Self-attention forward, one 64-thread block per (sequence, head), thread per query row.
+// K and V of the head staged in LDS; P (softmax probabilities) saved for the backward.
+// Eager transformers order: scores = (q . k) * scale; softmax = exp(s - max) / sum.
+__global__ void __launch_bounds__(64)
+tr_attn_fwd_kernel(const float* __restrict__ qkv, const int* __restrict__ seq_off,
+                   const long long* __restrict__ pofs, int H, int heads, float* __restrict__ P,
+                   float* __restrict__ ctx) {
+    extern __shared__ __attribute__((aligned(16))) float sm_a[];
+    const int s = blockIdx.x, hd = blockIdx.y, tid = threadIdx.x;
+    const int r0 = seq_off[s], T = seq_off[s + 1] - r0;
+    const int ld = 3 * H;
+    float* sK = sm_a;                 // [T][64]
+    float* sV = sm_a + T * 64;        // [T][64]
+    for (int q = tid; q < T * 16; q += 64) {
+        const int j = q >> 4, c = (q & 15) * 4;
+        const float* rowp = qkv + (size_t)(r0 + j) * ld + hd * 64 + c;
+        *(float4*)(sK + j * 64 + c) = *(const float4*)(rowp + H);
+        *(float4*)(sV + j * 64 + c) = *(const float4*)(rowp + 2 * H);
+    }
+    __syncthreads();
+    float* Ph = P + pofs[s] + (long long)hd * T * T;
+    for (int i = tid; i < T; i += 64) {
+        float qv[64];
+        const float* qp = qkv + (size_t)(r0 + i) * ld + hd * 64;
+#pragma unroll
+        for (int c = 0; c < 64; c += 4) {
+            const float4 v = *(const float4*)(qp + c);
+            qv[c] = v.x; qv[c + 1] = v.y; qv[c + 2] = v.z; qv[c + 3] = v.w;
+        }
+        float m = -INFINITY;
+        for (int j = 0; j < T; ++j) {
+            float d = 0.f;
+#pragma unroll
+            for (int c = 0; c < 64; ++c) d += qv[c] * sK[j * 64 + c];
+            d *= 0.125f;
+            Ph[(long long)i * T + j] = d;
+            m = fmaxf(m, d);
+        }
+        float sum = 0.f;
+        for (int j = 0; j < T; ++j) {
+            const float e = __expf(Ph[(long long)i * T + j] - m);
+            Ph[(long long)i * T + j] = e;
+            sum += e;
+        }
+        float o[64];
+#pragma unroll
+        for (int c = 0; c < 64; ++c) o[c] = 0.f;
+        for (int j = 0; j < T; ++j) {
+            const float p = Ph[(long long)i * T + j] / sum;
+            Ph[(long long)i * T + j] = p;
+#pragma unroll
+            for (int c = 0; c < 64; ++c) o[c] += p * sV[j * 64 + c];
+        }
+        float* op = ctx + (size_t)(r0 + i) * H + hd * 64;
+#pragma unroll
+        for (int c = 0; c < 64; c += 4) *(float4*)(op + c) = make_float4(o[c], o[c + 1], o[c + 2], o[c + 3]);
+    }
+}
+
+// Attention backward per (sequence, head): dP = dctx V^T, dS = P (dP - rowsum(P dP)),
+// dq = scale dS K, dk = scale dS^T Q, dv = P^T dctx.  dS lives in LDS.
+__global__ void __launch_bounds__(64)
+tr_attn_bwd_kernel(const float* __restrict__ qkv, const float* __restrict__ P, const float* __restrict__ dctx,
+                   const int* __restrict__ seq_off, const long long* __restrict__ pofs, int H, int heads,
+                   float* __restrict__ dqkv) {
+    extern __shared__ __attribute__((aligned(16))) float sm_a[];
+    const int s = blockIdx.x, hd = blockIdx.y, tid = threadIdx.x;
+    const int r0 = seq_off[s], T = seq_off[s + 1] - r0;
+    const int ld = 3 * H;
+    float* sA = sm_a;                 // [T][64]: K (phase 1), Q (phase 2)
+    float* sB = sm_a + T * 64;        // [T][64]: V (phase 1), dctx (phase 2)
+    float* sS = sm_a + 2 * T * 64;    // [T][T]: dS
+    for (int q = tid; q < T * 16; q += 64) {
+        const int j = q >> 4, c = (q & 15) * 4;
+        const float* rowp = qkv + (size_t)(r0 + j) * ld + hd * 64 + c;
+        *(float4*)(sA + j * 64 + c) = *(const float4*)(rowp + H);
+        *(float4*)(sB + j * 64 + c) = *(const float4*)(rowp + 2 * H);
+    }
+    __syncthreads();
+    const float* Ph = P + pofs[s] + (long long)hd * T * T;
+    for (int i = tid; i < T; i += 64) {
+        float g[64];
+        const float* gp = dctx + (size_t)(r0 + i) * H + hd * 64;
+#pragma unroll
+        for (int c = 0; c < 64; c += 4) {
+            const float4 v = *(const float4*)(gp + c);
+            g[c] = v.x; g[c + 1] = v.y; g[c + 2] = v.z; g[c + 3] = v.w;
+        }
+        float rd = 0.f;
+        for (int j = 0; j < T; ++j) {
+            float d = 0.f;
+#pragma unroll
+            for (int c = 0; c < 64; ++c) d += g[c] * sB[j * 64 + c];
+            sS[i * T + j] = d;
+            rd += Ph[(long long)i * T + j] * d;
+        }
+        float dq[64];
+#pragma unroll
+        for (int c = 0; c < 64; ++c) dq[c] = 0.f;
+        for (int j = 0; j < T; ++j) {
+            const float ds = Ph[(long long)i * T + j] * (sS[i * T + j] - rd);
+            sS[i * T + j] = ds;
+#pragma unroll
+            for (int c = 0; c < 64; ++c) dq[c] += ds * sA[j * 64 + c];
+        }
+        float* o = dqkv + (size_t)(r0 + i) * ld + hd * 64;
+#pragma unroll
+        for (int c = 0; c < 64; c += 4)
+            *(float4*)(o + c) = make_float4(dq[c] * 0.125f, dq[c + 1] * 0.125f, dq[c + 2] * 0.125f, dq[c + 3] * 0.125f);
+    }
+    __syncthreads();
+    for (int q = tid; q < T * 16; q += 64) {
+        const int j = q >> 4, c = (q & 15) * 4;
+        *(float4*)(sA + j * 64 + c) = *(const float4*)(qkv + (size_t)(r0 + j) * ld + hd * 64 + c);
+        *(float4*)(sB + j * 64 + c) = *(const float4*)(dctx + (size_t)(r0 + j) * H + hd * 64 + c);
+    }
+    __syncthreads();
+    for (int j = tid; j < T; j += 64) {
+        float dk[64], dv[64];
+#pragma unroll
+        for (int c = 0; c < 64; ++c) dk[c] = 0.f, dv[c] = 0.f;
+        for (int i = 0; i < T; ++i) {
+            const float ds = sS[i * T + j], p = Ph[(long long)i * T + j];
+#pragma unroll
+            for (int c = 0; c < 64; ++c) {
+                dk[c] += ds * sA[i * 64 + c];
+                dv[c] += p * sB[i * 64 + c];
+            }
+        }
+        float* o = dqkv + (size_t)(r0 + j) * ld + hd * 64;
+#pragma unroll
+        for (int c = 0; c < 64; c += 4) {
+            *(float4*)(o + H + c) = make_float4(dk[c] * 0.125f, dk[c + 1] * 0.125f, dk[c + 2] * 0.125f, dk[c + 3] * 0.125f);
+            *(float4*)(o + 2 * H + c) = make_float4(dv[c], dv[c + 1], dv[c + 2], dv[c + 3]);
+        }
+    }
+}
+
+// LayerNorm backward for one row: dx = rstd (g dy - mean(g dy) - xhat mean(g dy xhat)).
+// dx may alias dy.
+template <int NV>
+__global__ void __launch_bounds__(256)
+tr_ln_bwd_kernel(const float* dy, const float* __restrict__ x, const float2* __restrict__ st,
+                 const float* __restrict__ g, float* dx, int M) {
+    constexpr int H = NV * 256;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (row >= M) return;
+    const float2 s = st[row];
+    float4 gd[NV], xh[NV];
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int c = v * 256 + lane * 4;
+        const float4 d = *(const float4*)(dy + (size_t)row * H + c);
+        const float4 xx = *(const float4*)(x + (size_t)row * H + c);
+        const float4 gg = *(const float4*)(g + c);
+        gd[v] = make_float4(gg.x * d.x, gg.y * d.y, gg.z * d.z, gg.w * d.w);
+        xh[v] = make_float4((xx.x - s.x) * s.y, (xx.y - s.x) * s.y, (xx.z - s.x) * s.y, (xx.w - s.x) * s.y);
+        a += (gd[v].x + gd[v].y) + (gd[v].z + gd[v].w);
+        b += (gd[v].x * xh[v].x + gd[v].y * xh[v].y) + (gd[v].z * xh[v].z + gd[v].w * xh[v].w);
+    }
+    const float c1 = wave_sum(a) / (float)H, c2 = wave_sum(b) / (float)H;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int c = v * 256 + lane * 4;
+        *(float4*)(dx + (size_t)row * H + c) =
+            make_float4(s.y * (gd[v].x - c1 - xh[v].x * c2), s.y * (gd[v].y - c1 - xh[v].y * c2),
+                        s.y * (gd[v].z - c1 - xh[v].z * c2), s.y * (gd[v].w - c1 - xh[v].w * c2));
+    }
+}
+
+// Column reductions, stage 1: partial[rb][c] over rows [64 rb, 64 rb + 64) in row order.
+//   mode 0: sum dy            (bias grads)
+//   mode 1: sum dy * xhat     (LN gamma; xhat from x and (mean, rstd))
+constexpr int kRB = 64;
+__global__ void tr_colsum_partial_kernel(const float* __restrict__ dy, const float* __restrict__ x,
+                                         const float2* __restrict__ st, int M, int N, int mode,
+                                         float* __restrict__ part) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x, rb = blockIdx.y;
+    if (c >= N) return;
+    const int r1 = min(M, (rb + 1) * kRB);
+    float acc = 0.f;
+    for (int r = rb * kRB; r < r1; ++r) {
+        const float d = dy[(size_t)r * N + c];
+        if (mode == 0) acc += d;
+        else {
+            const float2 s = st[r];
+            acc += d * ((x[(size_t)r * N + c] - s.x) * s.y);
+        }
+    }
+    part[(size_t)rb * N + c] = acc;
+}
+
+// stage 2: out[c] (+)= sum over row blocks in order
+__global__ void tr_colsum_final_kernel(const float* __restrict__ part, int nrb, int N, float* __restrict__ out,
+                                       int accumulate) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= N) return;
+    float acc = 0.f;
+    for (int rb = 0; rb < nrb; ++rb) acc += part[(size_t)rb * N + c];
+    out[c] = accumulate ? out[c] + acc : acc;
+}
+
+// word-embedding gradient: block per distinct token, its rows summed in row order
+__global__ void tr_word_grad_kernel(const float* __restrict__ dx0, const int* __restrict__ utok,
+                                    const int* __restrict__ toff, const int* __restrict__ rows, int H,
+                                    float* __restrict__ dword) {
+    const int u = blockIdx.x;
+    const int tk = utok[u], a = toff[u], b = toff[u + 1];
+    for (int c = threadIdx.x; c < H; c += blockDim.x) {
+        float acc = 0.f;
+        for (int k = a; k < b; ++k) acc += dx0[(size_t)rows[k] * H + c];
+        dword[(size_t)tk * H + c] += acc;
+    }
+}
+
+// position-embedding gradient: block per position, sequences in order
+__global__ void tr_pos_grad_kernel(const float* __restrict__ dx0, const int* __restrict__ seq_off, int S, int H,
+                                   float* __restrict__ dpos) {
+    const int p = blockIdx.x;
+    for (int c = threadIdx.x; c < H; c += blockDim.x) {
+        float acc = 0.f;
+        for (int s = 0; s < S; ++s)
+            if (seq_off[s + 1] - seq_off[s] > p) acc += dx0[(size_t)(seq_off[s] + p) * H + c];
+        dpos[(size_t)p * H + c] += acc;
+    }
+}
+
+// RescoreBert head (RescoreBert/model.py:19-20): score_s = h[CLS_s] . w + b
+__global__ void tr_cls_fwd_kernel(const float* __restrict__ h, const int* __restrict__ seq_off, int S, int H,
+                                  const float* __restrict__ w, const float* __restrict__ b, float* __restrict__ out) {
+    const int s = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (s >= S) return;
+    const float* hr = h + (size_t)seq_off[s] * H;
+    float acc = 0.f;
+    for (int c = lane; c < H; c += 64) acc += hr[c] * w[c];
+    acc = wave_sum(acc);
+    if (lane == 0) out[s] = acc + b[0];
+}
+
+// head backward: dh[CLS_s] = dscore_s w (dh zeroed by the caller); dw = sum_s dscore_s h[CLS_s]
+// (block per 256 columns, sequences in order); db = sum_s dscore_s
+__global__ void tr_cls_bwd_kernel(const float* __restrict__ dsc, const float* __restrict__ h,
+                                  const int* __restrict__ seq_off, int S, int H, const float* __restrict__ w,
+                                  float* __restrict__ dh, float* __restrict__ dw, float* __restrict__ db) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c < H) {
+        float acc = 0.f;
+        for (int s = 0; s < S; ++s) {
+            const float d = dsc[s];
+            acc += d * h[(size_t)seq_off[s] * H + c];
+            dh[(size_t)seq_off[s] * H + c] = d * w[c];
+        }
+        dw[c] += acc;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        float acc = 0.f;
+        for (int s = 0; s < S; ++s) acc += dsc[s];
+        db[0] += acc;
+    }
+}
+
+// Distillation losses (single block; utterances strided over threads, totals summed by
+// thread 0 in order).  See train.h for the definitions.
+__global__ void tr_loss_kernel(const float* __restrict__ sc, const float* __restrict__ tgt,
+                               const float* __restrict__ am, const float* __restrict__ err,
+                               const int* __restrict__ utt_off, int n_utt, int n_hyp, int kind, float lam,
+                               float* __restrict__ dsc, float* __restrict__ uloss, float* __restrict__ loss) {
+    const float inv_n = 1.0f / (float)n_hyp;
+    for (int h = threadIdx.x; h < n_hyp; h += blockDim.x) dsc[h] = 2.0f * (sc[h] - tgt[h]) * inv_n;
+    __syncthreads();
+    const float inv_u = 1.0f / (float)max(n_utt, 1);
+    if (kind != RS_LOSS_MD) {
+        for (int u = threadIdx.x; u < n_utt; u += blockDim.x) {
+            const int a = utt_off[u], b = utt_off[u + 1];
+            float l = 0.f;
+            if (b > a) {
+                float m = -INFINITY, eb = 0.f;
+                for (int i = a; i < b; ++i) { m = fmaxf(m, am[i] + sc[i]); eb += err[i]; }
+                eb /= (float)(b - a);
+                if (kind == RS_LOSS_MWER) {
+                    float z = 0.f;
+                    for (int i = a; i < b; ++i) z += __expf(am[i] + sc[i] - m);
+                    for (int i = a; i < b; ++i) l += __expf(am[i] + sc[i] - m) / z * (err[i] - eb);
+                    for (int i = a; i < b; ++i) {
+                        const float p = __expf(am[i] + sc[i] - m) / z;
+                        dsc[i] += lam * inv_u * p * ((err[i] - eb) - l);
+                    }
+                } else {                              // MWED
+                    float cs = 0.f, es = 0.f, me = -INFINITY;
+                    for (int i = a; i < b; ++i) { cs += am[i] + sc[i]; es -= err[i]; me = fmaxf(me, -err[i]); }
+                    const float tau = (es != 0.f && cs / es > 0.f) ? cs / es : 1.0f;
+                    float zs = 0.f, ze = 0.f, ms = -INFINITY;
+                    for (int i = a; i < b; ++i) ms = fmaxf(ms, (am[i] + sc[i]) / tau);
+                    for (int i = a; i < b; ++i) { zs += __expf((am[i] + sc[i]) / tau - ms); ze += __expf(-err[i] - me); }
+                    for (int i = a; i < b; ++i) {
+                        const float de = __expf(-err[i] - me) / ze;
+                        const float lds = (am[i] + sc[i]) / tau - ms - __logf(zs);
+                        l -= de * lds;
+                        dsc[i] += lam * inv_u * (__expf(lds) - de) / tau;
+                    }
+                }
+            }
+            uloss[u] = l;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float md = 0.f;
+        for (int h = 0; h < n_hyp; ++h) md += (sc[h] - tgt[h]) * (sc[h] - tgt[h]);
+        float x = 0.f;
+        if (kind != RS_LOSS_MD)
+            for (int u = 0; u < n_utt; ++u) x += uloss[u];
+        loss[0] = md * inv_n + lam * x * inv_u;
+    }
+}
+
+// torch.optim.AdamW step (decoupled decay, bias-corrected, exp_avg via lerp)
+__global__ void tr_adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                float* __restrict__ v, long long n, float decay, float b1w, float b2, float b2w,
+                                float step_size, float bc2_sqrt, float eps) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+        float pi = p[i] * decay;
+        const float gi = g[i];
+        const float mi = m[i] + b1w * (gi - m[i]);
+        const float vi = v[i] * b2 + b2w * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        const float denom = sqrtf(vi) / bc2_sqrt + eps;
+        p[i] = pi - step_size * (mi / denom);
+    }
+}
+
+int grid_for(long long n, int bs) { return (int)std::min<long long>((n + bs - 1) / bs, 8192); }
+
+}  // namespace
+
+#define RS_NV_SWITCH(H, CALL)                \
+    switch (H) {                             \
+        case 256: { constexpr int NV = 1; CALL; } break;  \
+        case 512: { constexpr int NV = 2; CALL; } break;  \
+        case 768: { constexpr int NV = 3; CALL; } break;  \
+        case 1024: { constexpr int NV = 4; CALL; } break; \
+        default: return hipErrorInvalidValue; \
+    }
+
+hipError_t tr_embed_ln(const int* row_tok, const int* row_pos, int M, int vocab, const float* word,
+                       const float* pos, const float* type0, const float* g, const float* b, float eps, int H,
+                       float* x0, float2* st, float* h0, hipStream_t s) {
+    if (M <= 0) return hipSuccess;
+    RS_NV_SWITCH(H, hipLaunchKernelGGL(tr_embed_ln_kernel<NV>, dim3((M + 3) / 4), dim3(256), 0, s, row_tok, row_pos,
+                                       M, vocab, word, pos, type0, g, b, eps, x0, st, h0));
+    return hipGetLastError();
+}
+
+hipError_t tr_bias_res_ln(float* y, const float* bias, const float* res, int M, const float* g, const float* b,
+                          float eps, int H, float2* st, float* h, hipStream_t s) {
+    if (M <= 0) return hipSuccess;
+    RS_NV_SWITCH(H, hipLaunchKernelGGL(tr_bias_res_ln_kernel<NV>, dim3((M + 3) / 4), dim3(256), 0, s, y, bias, res,
+                                       M, g, b, eps, st, h));
+    return hipGetLastError();
+}
+
+hipError_t tr_bias_gelu(float* pre, const float* bias, float* act, int M, int N, hipStream_t s) {
+    const long long n4 = (long long)M * N / 4;
+    if (n4 <= 0) return hipSuccess;
+    hipLaunchKernelGGL(tr_bias_gelu_kernel, dim3(grid_for(n4, 256)), dim3(256), 0, s, pre, bias, act, n4, N);
+    return hipGetLastError();
+}
+
+hipError_t tr_gelu_bwd(float* d, const float* pre, long long n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(tr_gelu_bwd_kernel, dim3(grid_for(n / 4, 256)), dim3(256), 0, s, d, pre, n / 4);
+    return hipGetLastError();
+}
+
+hipError_t tr_bias(float* y, const float* bias, int M, int N, hipStream_t s) {
+    const long long n4 = (long long)M * N / 4;
+    if (n4 <= 0) return hipSuccess;
+    hipLaunchKernelGGL(tr_bias_kernel, dim3(grid_for(n4, 256)), dim3(256), 0, s, y, bias, n4, N);
+    return hipGetLastError();
+}
+
+static size_t attn_smem(int tmax, bool bwd) { return (size_t)(2 * tmax * 64 + (bwd ? tmax * tmax : 0)) * 4; }
+
+hipError_t tr_attn_fwd(const float* qkv, const int* seq_off, const long long* pofs, int S, int tmax, int H,
+                       int heads, float* P, float* ctx, hipStream_t s) {
+    if (S <= 0) return hipSuccess;
+    const size_t sm = attn_smem(tmax, false);
+    hipError_t e = hipFuncSetAttribute((const void*)tr_attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(tr_attn_fwd_kernel, dim3(S, heads), dim3(64), sm, s, qkv, seq_off, pofs, H, heads, P, ctx);
+    return hipGetLastError();
+}
+
+hipError_t tr_attn_bwd(const float* qkv, const float* P, const float* dctx, const int* seq_off, const long long* pofs,
+                       int S, int tmax, int H, int heads, float* dqkv, hipStream_t s) {
+    if (S <= 0) return hipSuccess;
+    const size_t sm = attn_smem(tmax, true);
+    hipError_t e = hipFuncSetAttribute((const void*)tr_attn_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(tr_attn_bwd_kernel, dim3(S, heads), dim3(64), sm, s, qkv, P, dctx, seq_off, pofs, H, heads, dqkv);
+    return hipGetLastError();
+}
+
+hipError_t tr_ln_bwd(const float* dy, const float* x, const float2* st, const float* g, float* dx, int M, int H,
+                     hipStream_t s) {
+    if (M <= 0) return hipSuccess;
+    RS_NV_SWITCH(H, hipLaunchKernelGGL(tr_ln_bwd_kernel<NV>, dim3((M + 3) / 4), dim3(256), 0, s, dy, x, st, g, dx, M));
+    return hipGetLastError();
+}
+
+size_t tr_colsum_scratch(int M, int N) { return (size_t)((M + kRB - 1) / kRB) * N * 4; }
+
+hipError_t tr_colsum(const float* dy, const float* x, const float2* st, int M, int N, int mode, float* part,
+                     float* out, int accumulate, hipStream_t s) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    const int nrb = (M + kRB - 1) / kRB;
+    hipLaunchKernelGGL(tr_colsum_partial_kernel, dim3((N + 255) / 256, nrb), dim3(256), 0, s, dy, x, st, M, N, mode, part);
+    hipLaunchKernelGGL(tr_colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, s, part, nrb, N, out, accumulate);
+    return hipGetLastError();
+}
+
+hipError_t tr_word_grad(const float* dx0, const int* utok, const int* toff, const int* rows, int n_uniq, int H,
+                        float* dword, hipStream_t s) {
+    if (n_uniq <= 0) return hipSuccess;
+    hipLaunchKernelGGL(tr_word_grad_kernel, dim3(n_uniq), dim3(256), 0, s, dx0, utok, toff, rows, H, dword);
+    return hipGetLastError();
+}
+
+hipError_t tr_pos_grad(const float* dx0, const int* seq_off, int S, int tmax, int H, float* dpos, hipStream_t s) {
+    if (S <= 0 || tmax <= 0) return hipSuccess;
+    hipLaunchKernelGGL(tr_pos_grad_kernel, dim3(tmax), dim3(256), 0, s, dx0, seq_off, S, H, dpos);
+    return hipGetLastError();
+}
+
+hipError_t tr_cls_fwd(const float* h, const int* seq_off, int S, int H, const float* w, const float* b, float* out,
+                      hipStream_t s) {
+    if (S <= 0) return hipSuccess;
+    hipLaunchKernelGGL(tr_cls_fwd_kernel, dim3((S + 3) / 4), dim3(256), 0, s, h, seq_off, S, H, w, b, out);
+    return hipGetLastError();
+}
+
+hipError_t tr_cls_bwd(const float* dsc, const float* h, const int* seq_off, int S, int H, const float* w, float* dh,
+                      float* dw, float* db, hipStream_t s) {
+    hipLaunchKernelGGL(tr_cls_bwd_kernel, dim3((H + 255) / 256), dim3(256), 0, s, dsc, h, seq_off, S, H, w, dh, dw, db);
+    return hipGetLastError();
+}
+
+hipError_t tr_loss(const float* sc, const float* tgt, const float* am, const float* err, const int* utt_off,
+                   int n_utt, int n_hyp, int kind, float lam, float* dsc, float* uloss, float* loss, hipStream_t s) {
+    hipLaunchKernelGGL(tr_loss_kernel, dim3(1), dim3(256), 0, s, sc, tgt, am, err, utt_off, n_utt, n_hyp, kind, lam,
+                       dsc, uloss, loss);
+    return hipGetLastError();
+}
+
+hipError_t tr_adamw(float* p, const float* g, float* m, float* v, long long n, float decay, float b1w, float b2,
+                    float b2w, float step_size, float bc2_sqrt, float eps, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(tr_adamw_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, p, g, m, v, n, decay, b1w, b2, b2w,
+                       step_size, bc2_sqrt, eps);
+    return hipGetLastError();
+}

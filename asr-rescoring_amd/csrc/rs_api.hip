@@ -774,3 +774,6 @@ void rs_model_destroy(rs_model* m) {
 }
 
 }  // extern "C"
+
+// shared error slot for the other C-ABI translation units (train_api.hip)
+int rs_fail(int code, const std::string& msg) { return fail(code, msg); }

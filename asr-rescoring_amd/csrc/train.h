@@ -1,0 +1,43 @@
+// Training kernels (k_train.hip) used by the trainer (train_api.hip).
+//
+// Distillation losses of RescoreBert training (RescoreBert/main.py:104-154: MD, MD_MWER,
+// MD_MWED), restated from the RescoreBERT paper (parity unpinned):
+//   s_i  = CLS score of hypothesis i, t_i = its MLM PLL target, c_i = am_i + s_i,
+//   eps_i = word errors of hypothesis i (utterance u holds hypotheses a..b-1)
+//   MD   = (1/N) sum_i (s_i - t_i)^2                                 (torch MSELoss)
+//   MWER = (1/U) sum_u sum_i softmax(c)_i (eps_i - mean_u eps)
+//   MWED = (1/U) sum_u -sum_i softmax(-eps)_i log softmax(c / tau)_i,
+//          tau = sum_i c_i / sum_i (-eps_i) (1 when that is not positive), held constant
+//   loss = MD + lambda * (MWER | MWED)
+#pragma once
+#include <hip/hip_runtime.h>
+#include "../../include/rescore.h"
+
+hipError_t tr_embed_ln(const int* row_tok, const int* row_pos, int M, int vocab, const float* word,
+                       const float* pos, const float* type0, const float* g, const float* b, float eps, int H,
+                       float* x0, float2* st, float* h0, hipStream_t s);
+hipError_t tr_bias_res_ln(float* y, const float* bias, const float* res, int M, const float* g, const float* b,
+                          float eps, int H, float2* st, float* h, hipStream_t s);
+hipError_t tr_bias_gelu(float* pre, const float* bias, float* act, int M, int N, hipStream_t s);
+hipError_t tr_gelu_bwd(float* d, const float* pre, long long n, hipStream_t s);
+hipError_t tr_bias(float* y, const float* bias, int M, int N, hipStream_t s);
+hipError_t tr_attn_fwd(const float* qkv, const int* seq_off, const long long* pofs, int S, int tmax, int H,
+                       int heads, float* P, float* ctx, hipStream_t s);
+hipError_t tr_attn_bwd(const float* qkv, const float* P, const float* dctx, const int* seq_off, const long long* pofs,
+                       int S, int tmax, int H, int heads, float* dqkv, hipStream_t s);
+hipError_t tr_ln_bwd(const float* dy, const float* x, const float2* st, const float* g, float* dx, int M, int H,
+                     hipStream_t s);
+size_t tr_colsum_scratch(int M, int N);
+hipError_t tr_colsum(const float* dy, const float* x, const float2* st, int M, int N, int mode, float* part,
+                     float* out, int accumulate, hipStream_t s);
+hipError_t tr_word_grad(const float* dx0, const int* utok, const int* toff, const int* rows, int n_uniq, int H,
+                        float* dword, hipStream_t s);
+hipError_t tr_pos_grad(const float* dx0, const int* seq_off, int S, int tmax, int H, float* dpos, hipStream_t s);
+hipError_t tr_cls_fwd(const float* h, const int* seq_off, int S, int H, const float* w, const float* b, float* out,
+                      hipStream_t s);
+hipError_t tr_cls_bwd(const float* dsc, const float* h, const int* seq_off, int S, int H, const float* w, float* dh,
+                      float* dw, float* db, hipStream_t s);
+hipError_t tr_loss(const float* sc, const float* tgt, const float* am, const float* err, const int* utt_off,
+                   int n_utt, int n_hyp, int kind, float lam, float* dsc, float* uloss, float* loss, hipStream_t s);
+hipError_t tr_adamw(float* p, const float* g, float* m, float* v, long long n, float decay, float b1w, float b2,
+                    float b2w, float step_size, float bc2_sqrt, float eps, hipStream_t s);

@@ -1,0 +1,426 @@
+// C-ABI trainer (include/rescore.h, rs_trainer_*): RescoreBert distillation training
+// (RescoreBert/main.py:104-229 — MD / MD_MWER / MD_MWED) on the GPU.
+//
+// One step = forward over the batch's hypotheses with every activation the backward needs
+// saved (ragged token rows, no padding), the loss and its gradient w.r.t. the CLS scores,
+// the backward through the head, the encoder layers and the embeddings, then one
+// torch.optim.AdamW update.  Parameters, gradients and Adam moments are single flat fp32
+// buffers (one AdamW launch); the fused Q|K|V weight is the contiguous [q; k; v] range of
+// the three HF tensors.  GEMMs: rocBLAS sgemm (fp32, atomics disabled: deterministic);
+// all other ops: k_train.hip.  Dropout is not applied (p = 0).
+#include <algorithm>
+#include <map>
+#include <string>
+#include <vector>
+#include <cstring>
+#include <cmath>
+
+#include <rocblas/rocblas.h>
+
+#include "common.h"
+#include "train.h"
+
+int rs_fail(int code, const std::string& msg);
+
+namespace {
+
+#define TRY_HIP(expr)                                                                       \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess) return rs_fail(RS_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+#define TRY_BLAS(expr)                                                                      \
+    do {                                                                                    \
+        rocblas_status s_ = (expr);                                                         \
+        if (s_ != rocblas_status_success)                                                   \
+            return rs_fail(RS_EHIP, std::string(#expr) + ": " + rocblas_status_to_string(s_)); \
+    } while (0)
+
+struct Buf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+    }
+    float* f() const { return (float*)p; }
+};
+
+struct TLayer {
+    size_t wqkv, bqkv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2;
+};
+
+}  // namespace
+
+struct rs_trainer {
+    rs_bert_cfg cfg{};
+    int device = 0;
+    bool finalized = false;
+    rocblas_handle blas = nullptr;
+    std::map<std::string, std::pair<size_t, size_t>> table;   // HF key -> (offset, numel) in floats
+    std::vector<float> host;                                  // staged parameters until finalize
+    std::vector<char> set;                                    // per table entry: provided?
+    size_t n_params = 0;
+    size_t o_word = 0, o_pos = 0, o_type = 0, o_eg = 0, o_eb = 0, o_wl = 0, o_bl = 0;
+    std::vector<TLayer> lay;
+    Buf P, G, M1, V1;       // parameters, gradients, Adam moments
+    Buf act, grad, meta, small;
+    long long step = 0;
+    std::vector<int> h_tok, h_meta;
+};
+
+namespace {
+
+size_t add_tensor(rs_trainer* t, const std::string& key, size_t n) {
+    size_t off = (t->n_params + 63) / 64 * 64;
+    t->table[key] = {off, n};
+    t->n_params = off + n;
+    return off;
+}
+
+// row-major Y[M, N] = X[M, K] . W[N, K]^T (+ beta Y)
+rocblas_status gemm_nt(rocblas_handle h, int M, int N, int K, const float* X, const float* W, float* Y, float beta) {
+    const float one = 1.0f;
+    return rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, N, M, K, &one, W, K, X, K, &beta, Y, N);
+}
+// row-major dX[M, K] = dY[M, N] . W[N, K] (+ beta dX)
+rocblas_status gemm_nn(rocblas_handle h, int M, int N, int K, const float* dY, const float* W, float* dX, float beta) {
+    const float one = 1.0f;
+    return rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, K, M, N, &one, W, K, dY, N, &beta, dX, K);
+}
+// row-major dW[N, K] = dY[M, N]^T . X[M, K]
+rocblas_status gemm_tn(rocblas_handle h, int M, int N, int K, const float* dY, const float* X, float* dW) {
+    const float one = 1.0f, zero = 0.0f;
+    return rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, K, N, M, &one, X, K, dY, N, &zero, dW, K);
+}
+
+}  // namespace
+
+extern "C" {
+
+int rs_trainer_create(const rs_bert_cfg* cfg, int device, rs_trainer** out) {
+    if (!cfg || !out) return rs_fail(RS_EARG, "null argument");
+    const rs_bert_cfg& c = *cfg;
+    if (c.hidden <= 0 || c.hidden % 256 || c.hidden > 1024) return rs_fail(RS_EUNSUP, "hidden must be 256/512/768/1024");
+    if (c.heads <= 0 || c.hidden / c.heads != 64 || c.hidden % c.heads) return rs_fail(RS_EUNSUP, "head_dim must be 64");
+    if (c.intermediate <= 0 || c.intermediate % 4) return rs_fail(RS_EUNSUP, "intermediate must be a multiple of 4");
+    if (c.layers < 1 || c.vocab < 1 || c.max_pos < 3 || c.type_vocab < 1) return rs_fail(RS_EARG, "bad config");
+    if (c.heads_mask != RS_HEAD_CLS) return rs_fail(RS_EUNSUP, "the trainer supports the RescoreBert head (RS_HEAD_CLS)");
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return rs_fail(RS_EHIP, "no such HIP device");
+    rs_trainer* t = new (std::nothrow) rs_trainer();
+    if (!t) return rs_fail(RS_ENOMEM, "alloc");
+    t->cfg = c;
+    t->device = device;
+    const size_t H = c.hidden, F = c.intermediate, V = c.vocab;
+    const std::string e = "bert.embeddings.";
+    t->o_word = add_tensor(t, e + "word_embeddings.weight", V * H);
+    t->o_pos = add_tensor(t, e + "position_embeddings.weight", (size_t)c.max_pos * H);
+    t->o_type = add_tensor(t, e + "token_type_embeddings.weight", (size_t)c.type_vocab * H);
+    t->o_eg = add_tensor(t, e + "LayerNorm.weight", H);
+    t->o_eb = add_tensor(t, e + "LayerNorm.bias", H);
+    t->lay.resize(c.layers);
+    for (int i = 0; i < c.layers; ++i) {
+        const std::string p = "bert.encoder.layer." + std::to_string(i) + ".";
+        TLayer& L = t->lay[i];
+        L.wqkv = add_tensor(t, p + "attention.self.query.weight", H * H);     // H*H % 64 == 0: contiguous
+        add_tensor(t, p + "attention.self.key.weight", H * H);
+        add_tensor(t, p + "attention.self.value.weight", H * H);
+        L.bqkv = add_tensor(t, p + "attention.self.query.bias", H);
+        add_tensor(t, p + "attention.self.key.bias", H);
+        add_tensor(t, p + "attention.self.value.bias", H);
+        L.wo = add_tensor(t, p + "attention.output.dense.weight", H * H);
+        L.bo = add_tensor(t, p + "attention.output.dense.bias", H);
+        L.g1 = add_tensor(t, p + "attention.output.LayerNorm.weight", H);
+        L.be1 = add_tensor(t, p + "attention.output.LayerNorm.bias", H);
+        L.w1 = add_tensor(t, p + "intermediate.dense.weight", F * H);
+        L.b1 = add_tensor(t, p + "intermediate.dense.bias", F);
+        L.w2 = add_tensor(t, p + "output.dense.weight", H * F);
+        L.b2 = add_tensor(t, p + "output.dense.bias", H);
+        L.g2 = add_tensor(t, p + "output.LayerNorm.weight", H);
+        L.be2 = add_tensor(t, p + "output.LayerNorm.bias", H);
+    }
+    t->o_wl = add_tensor(t, "linear.weight", H);
+    t->o_bl = add_tensor(t, "linear.bias", 1);
+    t->n_params = (t->n_params + 63) / 64 * 64;
+    t->host.assign(t->n_params, 0.0f);
+    t->set.assign(t->table.size(), 0);
+    *out = t;
+    return RS_OK;
+}
+
+int rs_trainer_set_tensor(rs_trainer* t, const char* key, const void* host_ptr, int dtype, const int64_t* shape,
+                          int ndim) {
+    if (!t || !key || !host_ptr || (ndim > 0 && !shape)) return rs_fail(RS_EARG, "null argument");
+    if (dtype != RS_DT_F32) return rs_fail(RS_EUNSUP, "only float32 tensors are accepted");
+    if (t->finalized) return rs_fail(RS_ESTATE, "trainer already finalized");
+    const std::string k(key);
+    if (k.rfind("bert.pooler.", 0) == 0) return RS_OK;   // RescoreBert never uses the pooler output: no gradient
+    auto it = t->table.find(k);
+    if (it == t->table.end()) return rs_fail(RS_EARG, "unknown tensor " + k);
+    int64_t n = 1;
+    for (int i = 0; i < ndim; ++i) n *= shape[i];
+    if ((size_t)n != it->second.second) return rs_fail(RS_EARG, "tensor " + k + " has the wrong size");
+    std::memcpy(t->host.data() + it->second.first, host_ptr, (size_t)n * 4);
+    t->set[std::distance(t->table.begin(), it)] = 1;
+    return RS_OK;
+}
+
+int rs_trainer_finalize(rs_trainer* t) {
+    if (!t) return rs_fail(RS_EARG, "null trainer");
+    if (t->finalized) return RS_OK;
+    size_t i = 0;
+    for (auto& kv : t->table) {
+        if (!t->set[i++]) return rs_fail(RS_ESTATE, "tensor " + kv.first + " (missing)");
+    }
+    TRY_HIP(hipSetDevice(t->device));
+    const size_t bytes = t->n_params * 4;
+    TRY_HIP(t->P.ensure(bytes));
+    TRY_HIP(t->G.ensure(bytes));
+    TRY_HIP(t->M1.ensure(bytes));
+    TRY_HIP(t->V1.ensure(bytes));
+    TRY_HIP(hipMemcpy(t->P.p, t->host.data(), bytes, hipMemcpyHostToDevice));
+    TRY_HIP(hipMemset(t->G.p, 0, bytes));
+    TRY_HIP(hipMemset(t->M1.p, 0, bytes));
+    TRY_HIP(hipMemset(t->V1.p, 0, bytes));
+    TRY_BLAS(rocblas_create_handle(&t->blas));
+    TRY_BLAS(rocblas_set_atomics_mode(t->blas, rocblas_atomics_not_allowed));
+    t->host.clear();
+    t->host.shrink_to_fit();
+    t->finalized = true;
+    return RS_OK;
+}
+
+static int copy_out(rs_trainer* t, const Buf& b, const char* key, void* host_out, int64_t numel) {
+    if (!t || !key || !host_out) return rs_fail(RS_EARG, "null argument");
+    if (!t->finalized) return rs_fail(RS_ESTATE, "rs_trainer_finalize not called");
+    auto it = t->table.find(key);
+    if (it == t->table.end()) return rs_fail(RS_EARG, std::string("unknown tensor ") + key);
+    if ((size_t)numel != it->second.second) return rs_fail(RS_EARG, std::string("tensor ") + key + " has a different size");
+    TRY_HIP(hipSetDevice(t->device));
+    TRY_HIP(hipDeviceSynchronize());
+    TRY_HIP(hipMemcpy(host_out, b.f() + it->second.first, (size_t)numel * 4, hipMemcpyDeviceToHost));
+    return RS_OK;
+}
+
+int rs_trainer_get_tensor(rs_trainer* t, const char* key, void* host_out, int64_t numel) {
+    return copy_out(t, t ? t->P : Buf{}, key, host_out, numel);
+}
+
+int rs_trainer_get_grad(rs_trainer* t, const char* key, void* host_out, int64_t numel) {
+    return copy_out(t, t ? t->G : Buf{}, key, host_out, numel);
+}
+
+int rs_train_step_cls(rs_trainer* t, const int32_t* d_tok, const int32_t* h_hyp_off, int32_t n_hyp,
+                      const int32_t* h_utt_off, int32_t n_utt, const float* d_target, const float* d_am,
+                      const float* d_err, const rs_train_opts* o, float* d_scores, float* d_loss, void* stream) {
+    if (!t || !h_hyp_off || !h_utt_off || !o || !d_loss || n_hyp <= 0 || n_utt <= 0 || !d_tok || !d_target)
+        return rs_fail(RS_EARG, "null argument / empty batch");
+    if (!t->finalized) return rs_fail(RS_ESTATE, "rs_trainer_finalize not called");
+    if (o->loss != RS_LOSS_MD && (!d_am || !d_err)) return rs_fail(RS_EARG, "MWER/MWED need am scores and errors");
+    if (o->loss < RS_LOSS_MD || o->loss > RS_LOSS_MWED) return rs_fail(RS_EARG, "unknown loss");
+    if (h_hyp_off[0] != 0 || h_utt_off[0] != 0 || h_utt_off[n_utt] != n_hyp)
+        return rs_fail(RS_EARG, "offsets must start at 0 and utt_off[n_utt] == n_hyp");
+    const rs_bert_cfg& c = t->cfg;
+    const int H = c.hidden, F = c.intermediate, nh = c.heads, NL = c.layers, S = n_hyp;
+    const int M = h_hyp_off[n_hyp];
+    int tmax = 0;
+    for (int s = 0; s < S; ++s) {
+        const int T = h_hyp_off[s + 1] - h_hyp_off[s];
+        if (T < 1) return rs_fail(RS_EARG, "empty hypothesis");
+        tmax = std::max(tmax, T);
+    }
+    for (int u = 0; u < n_utt; ++u)
+        if (h_utt_off[u + 1] < h_utt_off[u]) return rs_fail(RS_EARG, "utt_off not ascending");
+    if (tmax > c.max_pos) return rs_fail(RS_EUNSUP, "sequence longer than max_position_embeddings");
+    if (tmax > 128) return rs_fail(RS_EUNSUP, "training sequences are limited to 128 tokens");
+    hipStream_t st = (hipStream_t)stream;
+    TRY_HIP(hipSetDevice(t->device));
+    TRY_BLAS(rocblas_set_stream(t->blas, st));
+
+    // ---- host metadata (tokens come back once for the word-gradient CSR) ----------------
+    t->h_tok.resize(M);
+    TRY_HIP(hipMemcpyAsync(t->h_tok.data(), d_tok, (size_t)M * 4, hipMemcpyDeviceToHost, st));
+    TRY_HIP(hipStreamSynchronize(st));
+    std::vector<int> row_pos(M), order(M);
+    for (int s = 0; s < S; ++s)
+        for (int r = h_hyp_off[s]; r < h_hyp_off[s + 1]; ++r) row_pos[r] = r - h_hyp_off[s];
+    for (int r = 0; r < M; ++r) {
+        order[r] = r;
+        t->h_tok[r] = std::min(std::max(t->h_tok[r], 0), c.vocab - 1);
+    }
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return t->h_tok[a] < t->h_tok[b]; });
+    std::vector<int> utok, toff;
+    for (int k = 0; k < M; ++k)
+        if (k == 0 || t->h_tok[order[k]] != t->h_tok[order[k - 1]]) {
+            utok.push_back(t->h_tok[order[k]]);
+            toff.push_back(k);
+        }
+    toff.push_back(M);
+    const int n_uniq = (int)utok.size();
+    std::vector<long long> pofs(S + 1, 0);
+    for (int s = 0; s < S; ++s) {
+        const long long T = h_hyp_off[s + 1] - h_hyp_off[s];
+        pofs[s + 1] = pofs[s] + (long long)nh * T * T;
+    }
+    // int layout: pofs (int64) | row_tok | row_pos | seq_off | utt_off | utok | toff | order
+    std::vector<int>& hm = t->h_meta;
+    hm.assign(2 * (S + 1), 0);
+    std::memcpy(hm.data(), pofs.data(), (S + 1) * 8);
+    const size_t i_tok = hm.size();
+    hm.insert(hm.end(), t->h_tok.begin(), t->h_tok.end());
+    const size_t i_pos = hm.size();
+    hm.insert(hm.end(), row_pos.begin(), row_pos.end());
+    const size_t i_seq = hm.size();
+    hm.insert(hm.end(), h_hyp_off, h_hyp_off + S + 1);
+    const size_t i_utt = hm.size();
+    hm.insert(hm.end(), h_utt_off, h_utt_off + n_utt + 1);
+    const size_t i_utok = hm.size();
+    hm.insert(hm.end(), utok.begin(), utok.end());
+    const size_t i_toff = hm.size();
+    hm.insert(hm.end(), toff.begin(), toff.end());
+    const size_t i_ord = hm.size();
+    hm.insert(hm.end(), order.begin(), order.end());
+    TRY_HIP(t->meta.ensure(hm.size() * 4));
+    TRY_HIP(hipMemcpyAsync(t->meta.p, hm.data(), hm.size() * 4, hipMemcpyHostToDevice, st));
+    const int* dm = (const int*)t->meta.p;
+    const long long* d_pofs = (const long long*)dm;
+    const int* d_seq = dm + i_seq;
+
+    // ---- activation layout (floats) -------------------------------------------------------
+    const size_t MH = (size_t)M * H, MF = (size_t)M * F, M2 = (size_t)M * 2, PS = (size_t)pofs[S];
+    const size_t per_layer = MH /*h_in*/ + 3 * MH /*qkv*/ + PS + MH /*ctx*/ + MH /*x1*/ + M2 + MH /*h1*/ +
+                             2 * MF /*pre, act*/ + MH /*x2*/ + M2;
+    const size_t n_act = MH + M2 /*x0, st0*/ + NL * per_layer + MH /*h_final*/;
+    TRY_HIP(t->act.ensure(n_act * 4));
+    const size_t n_grad = 2 * MH + 3 * MH + MF + tr_colsum_scratch(M, std::max(3 * H, F)) / 4 + 2 * (size_t)S + n_utt + 64;
+    TRY_HIP(t->grad.ensure(n_grad * 4));
+    float* A = t->act.f();
+    float* x0 = A;
+    float2* st0 = (float2*)(x0 + MH);
+    float* lbase = (float*)(st0 + M);
+    struct LA { float *hin, *qkv, *P, *ctx, *x1, *h1, *pre, *act, *x2; float2 *st1, *st2; };
+    std::vector<LA> la(NL + 1);
+    for (int l = 0; l <= NL; ++l) {
+        float* b = lbase + (size_t)l * per_layer;
+        la[l].hin = b;
+        if (l == NL) break;
+        la[l].qkv = b + MH;
+        la[l].P = la[l].qkv + 3 * MH;
+        la[l].ctx = la[l].P + PS;
+        la[l].x1 = la[l].ctx + MH;
+        la[l].st1 = (float2*)(la[l].x1 + MH);
+        la[l].h1 = (float*)(la[l].st1 + M);
+        la[l].pre = la[l].h1 + MH;
+        la[l].act = la[l].pre + MF;
+        la[l].x2 = la[l].act + MF;
+        la[l].st2 = (float2*)(la[l].x2 + MH);
+    }
+    float* Gd = t->grad.f();
+    float* dA = Gd;
+    float* dB = dA + MH;
+    float* dQKV = dB + MH;
+    float* dF = dQKV + 3 * MH;
+    float* part = dF + MF;
+    float* sc = part + tr_colsum_scratch(M, std::max(3 * H, F)) / 4;
+    float* dsc = sc + S;
+    float* uloss = dsc + S;
+    float* Pm = t->P.f();
+    float* Gm = t->G.f();
+    rocblas_handle bh = t->blas;
+
+    // ---- forward --------------------------------------------------------------------------
+    TRY_HIP(tr_embed_ln(dm + i_tok, dm + i_pos, M, c.vocab, Pm + t->o_word, Pm + t->o_pos, Pm + t->o_type,
+                        Pm + t->o_eg, Pm + t->o_eb, c.ln_eps, H, x0, st0, la[0].hin, st));
+    for (int l = 0; l < NL; ++l) {
+        const TLayer& L = t->lay[l];
+        LA& a = la[l];
+        TRY_BLAS(gemm_nt(bh, M, 3 * H, H, a.hin, Pm + L.wqkv, a.qkv, 0.f));
+        TRY_HIP(tr_bias(a.qkv, Pm + L.bqkv, M, 3 * H, st));
+        TRY_HIP(tr_attn_fwd(a.qkv, d_seq, d_pofs, S, tmax, H, nh, a.P, a.ctx, st));
+        TRY_BLAS(gemm_nt(bh, M, H, H, a.ctx, Pm + L.wo, a.x1, 0.f));
+        TRY_HIP(tr_bias_res_ln(a.x1, Pm + L.bo, a.hin, M, Pm + L.g1, Pm + L.be1, c.ln_eps, H, a.st1, a.h1, st));
+        TRY_BLAS(gemm_nt(bh, M, F, H, a.h1, Pm + L.w1, a.pre, 0.f));
+        TRY_HIP(tr_bias_gelu(a.pre, Pm + L.b1, a.act, M, F, st));
+        TRY_BLAS(gemm_nt(bh, M, H, F, a.act, Pm + L.w2, a.x2, 0.f));
+        TRY_HIP(tr_bias_res_ln(a.x2, Pm + L.b2, a.h1, M, Pm + L.g2, Pm + L.be2, c.ln_eps, H, a.st2, la[l + 1].hin, st));
+    }
+    const float* hfin = la[NL].hin;
+    TRY_HIP(tr_cls_fwd(hfin, d_seq, S, H, Pm + t->o_wl, Pm + t->o_bl, sc, st));
+    if (d_scores) TRY_HIP(hipMemcpyAsync(d_scores, sc, (size_t)S * 4, hipMemcpyDeviceToDevice, st));
+    TRY_HIP(tr_loss(sc, d_target, d_am, d_err, dm + i_utt, n_utt, S, o->loss, o->lambda_, dsc, uloss, d_loss, st));
+
+    // ---- backward -------------------------------------------------------------------------
+    TRY_HIP(hipMemsetAsync(Gm, 0, t->n_params * 4, st));
+    TRY_HIP(hipMemsetAsync(dA, 0, MH * 4, st));
+    TRY_HIP(tr_cls_bwd(dsc, hfin, d_seq, S, H, Pm + t->o_wl, dA, Gm + t->o_wl, Gm + t->o_bl, st));
+    for (int l = NL - 1; l >= 0; --l) {
+        const TLayer& L = t->lay[l];
+        LA& a = la[l];
+        // dA = d(LN2 output)
+        TRY_HIP(tr_colsum(dA, a.x2, a.st2, M, H, 1, part, Gm + L.g2, 0, st));
+        TRY_HIP(tr_colsum(dA, nullptr, nullptr, M, H, 0, part, Gm + L.be2, 0, st));
+        TRY_HIP(tr_ln_bwd(dA, a.x2, a.st2, Pm + L.g2, dB, M, H, st));              // dB = dx2
+        TRY_HIP(tr_colsum(dB, nullptr, nullptr, M, H, 0, part, Gm + L.b2, 0, st));
+        TRY_BLAS(gemm_tn(bh, M, H, F, dB, a.act, Gm + L.w2));
+        TRY_BLAS(gemm_nn(bh, M, H, F, dB, Pm + L.w2, dF, 0.f));                    // d act
+        TRY_HIP(tr_gelu_bwd(dF, a.pre, (long long)MF, st));                         // d pre
+        TRY_HIP(tr_colsum(dF, nullptr, nullptr, M, F, 0, part, Gm + L.b1, 0, st));
+        TRY_BLAS(gemm_tn(bh, M, F, H, dF, a.h1, Gm + L.w1));
+        TRY_HIP(hipMemcpyAsync(dA, dB, MH * 4, hipMemcpyDeviceToDevice, st));      // residual
+        TRY_BLAS(gemm_nn(bh, M, F, H, dF, Pm + L.w1, dA, 1.f));                     // dA = d h1
+        TRY_HIP(tr_colsum(dA, a.x1, a.st1, M, H, 1, part, Gm + L.g1, 0, st));
+        TRY_HIP(tr_colsum(dA, nullptr, nullptr, M, H, 0, part, Gm + L.be1, 0, st));
+        TRY_HIP(tr_ln_bwd(dA, a.x1, a.st1, Pm + L.g1, dB, M, H, st));              // dB = dx1
+        TRY_HIP(tr_colsum(dB, nullptr, nullptr, M, H, 0, part, Gm + L.bo, 0, st));
+        TRY_BLAS(gemm_tn(bh, M, H, H, dB, a.ctx, Gm + L.wo));
+        TRY_BLAS(gemm_nn(bh, M, H, H, dB, Pm + L.wo, dA, 0.f));                     // dA = d ctx
+        TRY_HIP(tr_attn_bwd(a.qkv, a.P, dA, d_seq, d_pofs, S, tmax, H, nh, dQKV, st));
+        TRY_HIP(tr_colsum(dQKV, nullptr, nullptr, M, 3 * H, 0, part, Gm + L.bqkv, 0, st));
+        TRY_BLAS(gemm_tn(bh, M, 3 * H, H, dQKV, a.hin, Gm + L.wqkv));
+        TRY_HIP(hipMemcpyAsync(dA, dB, MH * 4, hipMemcpyDeviceToDevice, st));      // residual
+        TRY_BLAS(gemm_nn(bh, M, 3 * H, H, dQKV, Pm + L.wqkv, dA, 1.f));             // dA = d h_in
+    }
+    TRY_HIP(tr_colsum(dA, x0, st0, M, H, 1, part, Gm + t->o_eg, 0, st));
+    TRY_HIP(tr_colsum(dA, nullptr, nullptr, M, H, 0, part, Gm + t->o_eb, 0, st));
+    TRY_HIP(tr_ln_bwd(dA, x0, st0, Pm + t->o_eg, dB, M, H, st));                    // dB = dx0
+    TRY_HIP(tr_word_grad(dB, dm + i_utok, dm + i_toff, dm + i_ord, n_uniq, H, Gm + t->o_word, st));
+    TRY_HIP(tr_pos_grad(dB, d_seq, S, tmax, H, Gm + t->o_pos, st));
+    TRY_HIP(tr_colsum(dB, nullptr, nullptr, M, H, 0, part, Gm + t->o_type, 0, st));  // token_type row 0
+
+    // ---- torch.optim.AdamW ----------------------------------------------------------------
+    if (o->update) {
+        t->step += 1;
+        const double bc1 = 1.0 - std::pow((double)o->beta1, (double)t->step);
+        const double bc2 = 1.0 - std::pow((double)o->beta2, (double)t->step);
+        // python-float (double) scalars as torch computes them, cast to the fp32 tensor dtype
+        const float decay = (float)(1.0 - (double)o->lr * (double)o->weight_decay);
+        TRY_HIP(tr_adamw(Pm, Gm, t->M1.f(), t->V1.f(), (long long)t->n_params, decay,
+                         (float)(1.0 - (double)o->beta1), o->beta2, (float)(1.0 - (double)o->beta2),
+                         (float)((double)o->lr / bc1), (float)std::sqrt(bc2), o->eps, st));
+    }
+    // the metadata upload reads t->h_meta: finish before the host may reuse it
+    TRY_HIP(hipStreamSynchronize(st));
+    return RS_OK;
+}
+
+void rs_trainer_destroy(rs_trainer* t) {
+    if (!t) return;
+    (void)hipSetDevice(t->device);
+    (void)hipDeviceSynchronize();
+    if (t->blas) (void)rocblas_destroy_handle(t->blas);
+    for (Buf* b : {&t->P, &t->G, &t->M1, &t->V1, &t->act, &t->grad, &t->meta, &t->small}) b->release();
+    delete t;
+}
+
+}  // extern "C"

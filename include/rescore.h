@@ -39,6 +39,10 @@ extern "C" {
 #define RS_HEAD_CLS 2     /* RescoreBert head: linear.weight [1,H], linear.bias [1] */
 #define RS_HEAD_EMB 4     /* encoder only: token embeddings (BERTScore, bert_score.utils.bert_encode) */
 
+#define RS_LOSS_MD 0      /* RescoreBert training losses (RescoreBert/main.py:104-154) */
+#define RS_LOSS_MWER 1    /* MD + lambda * MWER */
+#define RS_LOSS_MWED 2    /* MD + lambda * MWED */
+
 #define RS_BS_P 0         /* BERTScore component used as the MBR utility */
 #define RS_BS_R 1
 #define RS_BS_F 2
@@ -163,6 +167,38 @@ int rs_bertscore_recall(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_
  * summation and argmax as rs_mbr_scores. */
 int rs_mbr_scores_bs(const float* d_rmat, const int64_t* d_mat_off, const int32_t* d_utt_off, int32_t n_utt,
                      int32_t k, int32_t which, float* d_scores, int32_t* d_argmax, void* stream);
+
+/* ---- RescoreBert training (RescoreBert/main.py:104-229) --------------------------------
+ * A trainer holds fp32 parameters (HF keys as for rs_model; bert.pooler.* is accepted and
+ * ignored — RescoreBert's loss never reaches it), their gradients and AdamW moments.
+ * rs_train_step_cls runs forward (activations kept), the distillation loss, the full
+ * backward and (opts->update) one torch.optim.AdamW step.  Losses (train.h):
+ *   MD = mean_i (s_i - t_i)^2;  MWER / MWED per utterance over c_i = am_i + s_i;
+ *   loss = MD + lambda * (MWER | MWED).  Dropout is not applied. */
+typedef struct rs_trainer rs_trainer;
+typedef struct rs_train_opts {
+    int32_t loss;          /* RS_LOSS_MD / RS_LOSS_MWER / RS_LOSS_MWED */
+    float lambda_;         /* weight of the MWER / MWED term */
+    float lr, beta1, beta2, eps, weight_decay;   /* torch.optim.AdamW arguments */
+    int32_t update;        /* 0: gradients only (no optimizer step) */
+} rs_train_opts;
+
+/* cfg->heads_mask must be RS_HEAD_CLS; shapes as rs_model_create (T <= 128 per sequence). */
+int rs_trainer_create(const rs_bert_cfg* cfg, int device, rs_trainer** out);
+int rs_trainer_set_tensor(rs_trainer* t, const char* hf_key, const void* host_ptr, int dtype,
+                          const int64_t* shape, int ndim);
+int rs_trainer_finalize(rs_trainer* t);
+/* d_tok/h_hyp_off as rs_cls_score; h_utt_off int32 [n_utt+1] groups hypotheses by utterance;
+ * d_target (PLL), d_am, d_err (word errors) float32 [n_hyp] (am/err only for MWER/MWED);
+ * d_scores (nullable) float32 [n_hyp] out; d_loss float32 [1] out.  Synchronises `stream`. */
+int rs_train_step_cls(rs_trainer* t, const int32_t* d_tok, const int32_t* h_hyp_off, int32_t n_hyp,
+                      const int32_t* h_utt_off, int32_t n_utt, const float* d_target, const float* d_am,
+                      const float* d_err, const rs_train_opts* opts, float* d_scores, float* d_loss,
+                      void* stream);
+/* Synchronous copies of one parameter / its last gradient (numel must match). */
+int rs_trainer_get_tensor(rs_trainer* t, const char* hf_key, void* host_out, int64_t numel);
+int rs_trainer_get_grad(rs_trainer* t, const char* hf_key, void* host_out, int64_t numel);
+void rs_trainer_destroy(rs_trainer* t);
 
 /* RMBR mbr_decode scores for top-k (RMBR/mbr.py:17-22):
  *   score[u][i] = float32 torch-CPU-order sum over j != i (j < k) of
