@@ -300,17 +300,21 @@ __global__ void tr_colsum_partial_kernel(const float* __restrict__ dy, const flo
                                          float* __restrict__ part) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x, rb = blockIdx.y;
     if (c >= N) return;
-    const int r1 = min(M, (rb + 1) * kRB);
-    float acc = 0.f;
-    for (int r = rb * kRB; r < r1; ++r) {
-        const float d = dy[(size_t)r * N + c];
-        if (mode == 0) acc += d;
-        else {
+    const int r0 = rb * kRB, r1 = min(M, r0 + kRB);
+    // four interleaved accumulators (rows r % 4), combined in a fixed order: independent
+    // loads in flight, still deterministic
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (mode == 0) {
+#pragma unroll 8
+        for (int r = r0; r < r1; ++r) acc[r & 3] += dy[(size_t)r * N + c];
+    } else {
+#pragma unroll 4
+        for (int r = r0; r < r1; ++r) {
             const float2 s = st[r];
-            acc += d * ((x[(size_t)r * N + c] - s.x) * s.y);
+            acc[r & 3] += dy[(size_t)r * N + c] * ((x[(size_t)r * N + c] - s.x) * s.y);
         }
     }
-    part[(size_t)rb * N + c] = acc;
+    part[(size_t)rb * N + c] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
 
 // stage 2: out[c] (+)= sum over row blocks in order
@@ -318,9 +322,11 @@ __global__ void tr_colsum_final_kernel(const float* __restrict__ part, int nrb, 
                                        int accumulate) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= N) return;
-    float acc = 0.f;
-    for (int rb = 0; rb < nrb; ++rb) acc += part[(size_t)rb * N + c];
-    out[c] = accumulate ? out[c] + acc : acc;
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll 8
+    for (int rb = 0; rb < nrb; ++rb) acc[rb & 3] += part[(size_t)rb * N + c];
+    const float a = (acc[0] + acc[1]) + (acc[2] + acc[3]);
+    out[c] = accumulate ? out[c] + a : a;
 }
 
 // word-embedding gradient: block per distinct token, its rows summed in row order
@@ -539,7 +545,7 @@ hipError_t tr_colsum(const float* dy, const float* x, const float2* st, int M, i
     if (M <= 0 || N <= 0) return hipSuccess;
     const int nrb = (M + kRB - 1) / kRB;
     hipLaunchKernelGGL(tr_colsum_partial_kernel, dim3((N + 255) / 256, nrb), dim3(256), 0, s, dy, x, st, M, N, mode, part);
-    hipLaunchKernelGGL(tr_colsum_final_kernel, dim3((N + 255) / 256), dim3(256), 0, s, part, nrb, N, out, accumulate);
+    hipLaunchKernelGGL(tr_colsum_final_kernel, dim3((N + 63) / 64), dim3(64), 0, s, part, nrb, N, out, accumulate);
     return hipGetLastError();
 }
 

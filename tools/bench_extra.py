@@ -131,19 +131,48 @@ def c5bs():
     dt_all = _timed(rec)
     rmat, moff = holder["r"]
     dt_mbr = _timed(lambda: [BS.mbr_scores(rmat, moff, nb.utt_off, k, "R") for k in range(2, 11)])
+    sc.profile(True)
+    sc.embed(d_tok, nb.hyp_off)
+    torch.cuda.synchronize()
+    kinds = {k: round(v[0], 1) for k, v in sc.profile_read().items()}
+    sc.profile(False)
     sc.close()
     dt_sim = max(dt_all - dt_emb, 1e-9)
     return [{"workload": "C5 RMBR BERTScore utility U=7176 N=100 real-length, bert-base 8 layers",
              "value": round(int(moff[-1]) / dt_all / 1e6, 2), "unit": "M ordered pairs/s (embeddings included)",
              "tokens": rows, "ms_total": round(dt_all * 1e3, 1), "ms_embed": round(dt_emb * 1e3, 1),
              "ms_recall_kernel": round(dt_sim * 1e3, 1), "embed_tflops": round(enc_fl / dt_emb / 1e12, 1),
-             "recall_tflops_algorithmic": round(sim_fl / dt_sim / 1e12, 1), "ms_mbr_k2_10": round(dt_mbr * 1e3, 2)}]
+             "recall_tflops_algorithmic": round(sim_fl / dt_sim / 1e12, 1), "ms_mbr_k2_10": round(dt_mbr * 1e3, 2),
+             "embed_ms_by_kind": kinds}]
+
+
+def c2train():
+    """RescoreBert distillation training (MD_MWER) on bert-base: batches of 3 utterances x
+    N=50 (RescoreBert/main.py:75 batch_size * n_best rows), hypotheses / s and fp32 TFLOP/s
+    (forward + backward ~ 3 x the forward's dense FLOPs)."""
+    from asr_rescoring_amd.train import RescoreBertTrainer
+    w = make_weights(BERT_BASE, seed=1234, with_cls_linear=True, with_pooler=True)
+    tr = RescoreBertTrainer(w, BERT_BASE, loss="MD_MWER", lam=1.0, lr=1e-5)
+    nb = D.synthetic_nbest(3, 50, seed=1)
+    rng = np.random.default_rng(0)
+    tgt = -np.abs(rng.normal(40, 8, nb.n_hyp)).astype(np.float32)
+    err = rng.integers(0, 6, nb.n_hyp).astype(np.float32)
+    am = nb.am.astype(np.float32)
+    step = lambda: tr.step(nb.tokens, nb.hyp_off, nb.utt_off, tgt, am, err)
+    dt = _timed(step, steps=5, warmup=2)
+    tr.close()
+    T = np.diff(nb.hyp_off).astype(np.float64)
+    H, F, L = BERT_BASE.hidden, BERT_BASE.intermediate, BERT_BASE.layers
+    fl = 3.0 * (float(T.sum()) * L * 2 * (4 * H * H + 2 * H * F) + L * 4 * float((T * T).sum()) * H)
+    return [{"workload": "RescoreBert training MD_MWER, bert-base, 3 utts x N=50 per step (fp32)",
+             "value": round(nb.n_hyp / dt, 1), "unit": "hypotheses/s", "rows_per_step": int(T.sum()),
+             "ms_per_step": round(dt * 1e3, 1), "tflops_fp32": round(fl / dt / 1e12, 1)}]
 
 
 def main():
     which = sys.argv[1].split(",") if len(sys.argv) > 1 else ["c2", "c4", "c5", "c5bs"]
     for name in which:
-        for rec in {"c2": c2, "c4": c4, "c5": c5, "c5bs": c5bs}[name]():
+        for rec in {"c2": c2, "c4": c4, "c5": c5, "c5bs": c5bs, "c2train": c2train}[name]():
             print(json.dumps(rec), flush=True)
 
 
