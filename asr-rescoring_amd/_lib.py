@@ -71,6 +71,7 @@ _SIGS = {
     "rs_train_step_cls": (ctypes.c_int, [P, P, P, I32, P, I32, P, P, P, ctypes.POINTER(RsTrainOpts), P, P, P]),
     "rs_trainer_get_tensor": (ctypes.c_int, [P, ctypes.c_char_p, P, I64]),
     "rs_trainer_get_grad": (ctypes.c_int, [P, ctypes.c_char_p, P, I64]),
+    "rs_trainer_reset_optimizer": (ctypes.c_int, [P]),
     "rs_trainer_destroy": (None, [P]),
     "rs_bertscore_recall": (ctypes.c_int, [P, P, P, P, I32, P, P]),
     "rs_fuse_rerank": (ctypes.c_int, [P, P, P, P, I32, I32, P, I32, I32, P, P]),

@@ -2,6 +2,7 @@
 
   python -m asr_rescoring_amd.cli mlm_pll     --config score.yaml    # MLM_PLL/main.py (task: scoring)
   python -m asr_rescoring_amd.cli rescorebert --config MD_score.yaml # RescoreBert/main.py (task: scoring)
+  python -m asr_rescoring_amd.cli rescorebert_train --config MD.yaml # RescoreBert/main.py (task: train)
   python -m asr_rescoring_amd.cli rescore     --config rescore.yaml  # rescore.py
   python -m asr_rescoring_amd.cli rmbr        --config CER.yaml      # RMBR/main.py (utility: cer / bertscore)
 
@@ -137,6 +138,54 @@ def rescorebert(cfg) -> Dict[str, str]:
     return out_files
 
 
+def rescorebert_train(cfg) -> Dict[str, object]:
+    """RescoreBert/main.py:166-229 (train) on the native trainer (``train.RescoreBertTrainer``).
+
+    ``train_feature`` / ``train_feature_path`` name ``hyps_text``, ``ref_text``, ``hyps_score``
+    (AM) and ``mlm_score`` (the MLM_PLL teacher JSON written by ``mlm_pll``).  Keys:
+    ``loss_type`` (MD / MD_MWER / MD_MWED), ``lambda``, ``epochs``, ``batch_size``
+    (utterances per step), ``lr``, ``weight_decay``, ``n_best``, ``reset_optimizer`` (a fresh
+    AdamW each epoch).  Writes ``checkpoint_{epoch}.pt`` (HF keys, torch.save of tensors:
+    loadable with ``torch.load(weights_only=True)`` as ``checkpoint_path``) and ``train.log``."""
+    import torch
+    from . import rerank
+    from .train import RescoreBertTrainer
+    os.makedirs(cfg.output_path, exist_ok=True)
+    log = _logger(os.path.join(cfg.output_path, "train.log"))
+    feats, paths = cfg.train_feature, cfg.train_feature_path
+    src = {f: _load(p) for f, p in zip(feats, paths)}
+    n_best, max_utt = get(cfg, "n_best", 1 << 30), get(cfg, "max_utt", 1 << 30)
+    hyps = src["hyps_text"]
+    nb_c = D.from_texts(hyps, src["ref_text"], src["hyps_score"], n_best=n_best, max_utt=max_utt)
+    tok = _tokenizer(cfg, [t for h in hyps.values() for t in h.values()])
+    nb, keys = _nbest_tokens(hyps, tok, max_utt, n_best)
+    target = np.asarray([src["mlm_score"][u][h] for u, h in keys], np.float32)
+    err = rerank.ref_edits(nb_c, device=_dev(cfg)).cpu().numpy().astype(np.float32)
+    am = nb_c.am.astype(np.float32)
+    tr = RescoreBertTrainer(_weights(cfg, "cls"), BERT_BASE, device=_dev(cfg), loss=get(cfg, "loss_type", "MD"),
+                            lam=float(get(cfg, "lambda", 1.0)), lr=float(get(cfg, "lr", 1e-5)),
+                            weight_decay=float(get(cfg, "weight_decay", 0.01)))
+    bs = int(get(cfg, "batch_size", 3))
+    losses, ckpts = [], []
+    for ep in range(int(get(cfg, "epochs", 1))):
+        if ep and get(cfg, "reset_optimizer", False):
+            tr.reset_optimizer()
+        tot = 0.0
+        for b0 in range(0, nb.n_utt, bs):
+            utts = list(range(b0, min(nb.n_utt, b0 + bs)))
+            sub = nb.subset(utts)
+            h0, h1 = nb.utt_off[utts[0]], nb.utt_off[utts[-1] + 1]
+            loss, _ = tr.step(sub.tokens, sub.hyp_off, sub.utt_off, target[h0:h1], am[h0:h1], err[h0:h1])
+            tot += loss
+        losses.append(tot / max(1, -(-nb.n_utt // bs)))
+        log.info(f"epoch {ep + 1} loss {losses[-1]}")
+        path = os.path.join(cfg.output_path, f"checkpoint_{ep + 1}.pt")
+        torch.save({k: torch.from_numpy(v) for k, v in tr.state_dict().items()}, path)
+        ckpts.append(path)
+    tr.close()
+    return {"losses": losses, "checkpoints": ckpts}
+
+
 def rescore(cfg) -> Dict[str, float]:
     """rescore.py:61-120: best weight on dev, CER on test, logged to output_path/rescore.log."""
     from . import rerank
@@ -257,7 +306,8 @@ def _logger(path):
     return log
 
 
-COMMANDS = {"mlm_pll": mlm_pll, "rescorebert": rescorebert, "rescore": rescore, "rmbr": rmbr}
+COMMANDS = {"mlm_pll": mlm_pll, "rescorebert": rescorebert, "rescorebert_train": rescorebert_train,
+            "rescore": rescore, "rmbr": rmbr}
 
 
 def main(argv=None):

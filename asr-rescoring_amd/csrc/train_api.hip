@@ -414,6 +414,17 @@ int rs_train_step_cls(rs_trainer* t, const int32_t* d_tok, const int32_t* h_hyp_
     return RS_OK;
 }
 
+int rs_trainer_reset_optimizer(rs_trainer* t) {
+    if (!t) return rs_fail(RS_EARG, "null trainer");
+    if (!t->finalized) return rs_fail(RS_ESTATE, "rs_trainer_finalize not called");
+    TRY_HIP(hipSetDevice(t->device));
+    TRY_HIP(hipDeviceSynchronize());
+    TRY_HIP(hipMemset(t->M1.p, 0, t->n_params * 4));
+    TRY_HIP(hipMemset(t->V1.p, 0, t->n_params * 4));
+    t->step = 0;
+    return RS_OK;
+}
+
 void rs_trainer_destroy(rs_trainer* t) {
     if (!t) return;
     (void)hipSetDevice(t->device);

@@ -108,6 +108,9 @@ class RescoreBertTrainer:
                                               _lib.stream_ptr(dev)))
         return float(loss.item()), sc.cpu().numpy()
 
+    def reset_optimizer(self):
+        _lib.check(self.lib.rs_trainer_reset_optimizer(self.handle))
+
     def _get(self, fn, key: str) -> np.ndarray:
         shp = self.shapes[key]
         out = np.empty(shp, np.float32)

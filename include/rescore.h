@@ -198,6 +198,9 @@ int rs_train_step_cls(rs_trainer* t, const int32_t* d_tok, const int32_t* h_hyp_
 /* Synchronous copies of one parameter / its last gradient (numel must match). */
 int rs_trainer_get_tensor(rs_trainer* t, const char* hf_key, void* host_out, int64_t numel);
 int rs_trainer_get_grad(rs_trainer* t, const char* hf_key, void* host_out, int64_t numel);
+/* A fresh AdamW state (moments and step count zeroed; MLM_PLL/main.py:76 builds its
+ * optimizer inside every epoch). */
+int rs_trainer_reset_optimizer(rs_trainer* t);
 void rs_trainer_destroy(rs_trainer* t);
 
 /* RMBR mbr_decode scores for top-k (RMBR/mbr.py:17-22):

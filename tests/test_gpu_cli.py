@@ -94,3 +94,31 @@ def test_cli_rmbr_bertscore(c1):
     mbr = json.load(open(d / "mbr_bs_out" / "dev_MBR.json", encoding="utf-8"))
     got = np.array([list(mbr[u].values())[:k] for u in g["utt_ids"]], np.float32)
     assert np.allclose(got, want, rtol=1e-3, atol=1e-5)
+
+
+def test_cli_rescorebert_train_then_score(c1):
+    """rescorebert_train on the C1 texts (MLM_PLL teacher = the golden lm JSON), then the
+    written checkpoint feeds rescorebert scoring."""
+    import torch
+    from asr_rescoring_amd import cli
+    g, d = c1
+    json.dump(g["lm"], open(d / "mlm_score.json", "w", encoding="utf-8"), ensure_ascii=False)
+    out = d / "train_out"
+    res = cli.rescorebert_train(cli.ArgParser().parse(["--config", _cfg(d, "MD_MWER.yaml", {
+        "device": "cuda:0", "random_init_seed": 1234, "loss_type": "MD_MWER", "lambda": 0.5, "epochs": 2,
+        "batch_size": 3, "lr": 1e-5, "n_best": 10, "reset_optimizer": True,
+        "model": {"bert": "bert-base-chinese", "vocab": str(d / "vocab.txt")},
+        "train_feature": ["hyps_text", "ref_text", "hyps_score", "mlm_score"],
+        "train_feature_path": [str(d / f) for f in ("hyps_text.json", "ref_text.json", "hyps_score.json",
+                                                    "mlm_score.json")],
+        "output_path": str(out)})]))
+    assert len(res["losses"]) == 2 and all(np.isfinite(res["losses"]))
+    sd = torch.load(res["checkpoints"][-1], map_location="cpu", weights_only=True)
+    assert "linear.weight" in sd and "bert.pooler.dense.weight" in sd
+    files = cli.rescorebert(cli.ArgParser().parse(["--config", _cfg(d, "MD_score.yaml", {
+        "device": "cuda:0", "checkpoint_path": res["checkpoints"][-1], "n_best": 10,
+        "model": {"bert": "bert-base-chinese", "vocab": str(d / "vocab.txt")},
+        "dev_feature": ["hyps_token_ids"], "dev_feature_path": [str(d / "hyps_text.json")],
+        "dev_output_format": str(d / "hyps_score.json"), "output_path": str(out)})]))
+    lm = json.load(open(files["dev"], encoding="utf-8"))
+    assert list(lm) == g["utt_ids"] and all(np.isfinite(v) for u in lm.values() for v in u.values())
