@@ -61,10 +61,10 @@ tr_embed_ln_kernel(const int* __restrict__ row_tok, const int* __restrict__ row_
     ln_fwd_row<NV>(x, g, b, eps, lane, st + row, h0 + (size_t)row * H);
 }
 
-// y <- (y + bias) + res (pre-LN, saved), h = LN(y)
+// y <- (y + bias) + res (pre-LN, saved), h = LN(y); bias == nullptr: plain LN of y
 template <int NV>
 __global__ void __launch_bounds__(256)
-tr_bias_res_ln_kernel(float* __restrict__ y, const float* __restrict__ bias, const float* __restrict__ res,
+tr_bias_res_ln_kernel(float* __restrict__ y, const float* bias, const float* res,
                       int M, const float* __restrict__ g, const float* __restrict__ b, float eps,
                       float2* __restrict__ st, float* __restrict__ h) {
     constexpr int H = NV * 256;
@@ -74,11 +74,13 @@ tr_bias_res_ln_kernel(float* __restrict__ y, const float* __restrict__ bias, con
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         const int c = v * 256 + lane * 4;
-        const float4 a = *(const float4*)(y + (size_t)row * H + c);
-        const float4 bb = *(const float4*)(bias + c);
-        const float4 r = *(const float4*)(res + (size_t)row * H + c);
-        x[v] = make_float4((a.x + bb.x) + r.x, (a.y + bb.y) + r.y, (a.z + bb.z) + r.z, (a.w + bb.w) + r.w);
-        *(float4*)(y + (size_t)row * H + c) = x[v];
+        x[v] = *(const float4*)(y + (size_t)row * H + c);
+        if (bias) {
+            const float4 bb = *(const float4*)(bias + c);
+            const float4 r = *(const float4*)(res + (size_t)row * H + c);
+            x[v] = make_float4((x[v].x + bb.x) + r.x, (x[v].y + bb.y) + r.y, (x[v].z + bb.z) + r.z, (x[v].w + bb.w) + r.w);
+            *(float4*)(y + (size_t)row * H + c) = x[v];
+        }
     }
     ln_fwd_row<NV>(x, g, b, eps, lane, st + row, h + (size_t)row * H);
 }
@@ -443,6 +445,50 @@ __global__ void tr_loss_kernel(const float* __restrict__ sc, const float* __rest
     }
 }
 
+// fixed-tree block reductions (256 threads)
+__device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
+    const int tid = threadIdx.x;
+    sh[tid] = v;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (tid < w) sh[tid] = is_max ? fmaxf(sh[tid], sh[tid + w]) : sh[tid] + sh[tid + w];
+        __syncthreads();
+    }
+    const float r = sh[0];
+    __syncthreads();
+    return r;
+}
+
+// BertForMaskedLM CE (modeling_bert.py:972-975, mean over rows): per row lse - logit[label];
+// logits are replaced by d loss / d logits = (softmax - onehot) / M
+__global__ void __launch_bounds__(256)
+tr_ce_kernel(float* __restrict__ logits, const int* __restrict__ labels, int M, int V, float* __restrict__ rl) {
+    __shared__ float sh[256];
+    const int row = blockIdx.x, tid = threadIdx.x;
+    float* x = logits + (size_t)row * V;
+    const int lab = min(max(labels[row], 0), V - 1);
+    float m = -INFINITY;
+    for (int j = tid; j < V; j += 256) m = fmaxf(m, x[j]);
+    m = block_reduce(m, sh, true);
+    float sum = 0.f;
+    for (int j = tid; j < V; j += 256) sum += __expf(x[j] - m);
+    sum = block_reduce(sum, sh, false);
+    const float lse = m + __logf(sum);
+    const float xl = x[lab];
+    __syncthreads();
+    if (tid == 0) rl[row] = lse - xl;
+    const float inv = 1.0f / (float)M;
+    for (int j = tid; j < V; j += 256) x[j] = (__expf(x[j] - lse) - (j == lab ? 1.0f : 0.0f)) * inv;
+}
+
+__global__ void __launch_bounds__(256) tr_mean_kernel(const float* __restrict__ v, int n, float* __restrict__ out) {
+    __shared__ float sh[256];
+    float acc = 0.f;
+    for (int i = threadIdx.x; i < n; i += 256) acc += v[i];
+    acc = block_reduce(acc, sh, false);
+    if (threadIdx.x == 0) out[0] = acc / (float)n;
+}
+
 // torch.optim.AdamW step (decoupled decay, bias-corrected, exp_avg via lerp)
 __global__ void tr_adamw_kernel(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
                                 float* __restrict__ v, long long n, float decay, float b1w, float b2, float b2w,
@@ -579,6 +625,13 @@ hipError_t tr_loss(const float* sc, const float* tgt, const float* am, const flo
                    int n_utt, int n_hyp, int kind, float lam, float* dsc, float* uloss, float* loss, hipStream_t s) {
     hipLaunchKernelGGL(tr_loss_kernel, dim3(1), dim3(256), 0, s, sc, tgt, am, err, utt_off, n_utt, n_hyp, kind, lam,
                        dsc, uloss, loss);
+    return hipGetLastError();
+}
+
+hipError_t tr_ce(float* logits, const int* labels, int M, int V, float* row_loss, float* loss, hipStream_t s) {
+    if (M <= 0) return hipSuccess;
+    hipLaunchKernelGGL(tr_ce_kernel, dim3(M), dim3(256), 0, s, logits, labels, M, V, row_loss);
+    hipLaunchKernelGGL(tr_mean_kernel, dim3(1), dim3(256), 0, s, row_loss, M, loss);
     return hipGetLastError();
 }
 

@@ -39,5 +39,6 @@ hipError_t tr_cls_bwd(const float* dsc, const float* h, const int* seq_off, int 
                       float* dw, float* db, hipStream_t s);
 hipError_t tr_loss(const float* sc, const float* tgt, const float* am, const float* err, const int* utt_off,
                    int n_utt, int n_hyp, int kind, float lam, float* dsc, float* uloss, float* loss, hipStream_t s);
+hipError_t tr_ce(float* logits, const int* labels, int M, int V, float* row_loss, float* loss, hipStream_t s);
 hipError_t tr_adamw(float* p, const float* g, float* m, float* v, long long n, float decay, float b1w, float b2,
                     float b2w, float step_size, float bc2_sqrt, float eps, hipStream_t s);

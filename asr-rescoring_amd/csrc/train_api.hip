@@ -72,6 +72,7 @@ struct rs_trainer {
     std::vector<char> set;                                    // per table entry: provided?
     size_t n_params = 0;
     size_t o_word = 0, o_pos = 0, o_type = 0, o_eg = 0, o_eb = 0, o_wl = 0, o_bl = 0;
+    size_t o_wt = 0, o_bt = 0, o_tg = 0, o_tb = 0, o_db = 0;   // MLM head (decoder tied to o_word)
     std::vector<TLayer> lay;
     Buf P, G, M1, V1;       // parameters, gradients, Adam moments
     Buf act, grad, meta, small;
@@ -99,9 +100,9 @@ rocblas_status gemm_nn(rocblas_handle h, int M, int N, int K, const float* dY, c
     return rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, K, M, N, &one, W, K, dY, N, &beta, dX, K);
 }
 // row-major dW[N, K] = dY[M, N]^T . X[M, K]
-rocblas_status gemm_tn(rocblas_handle h, int M, int N, int K, const float* dY, const float* X, float* dW) {
-    const float one = 1.0f, zero = 0.0f;
-    return rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, K, N, M, &one, X, K, dY, N, &zero, dW, K);
+rocblas_status gemm_tn(rocblas_handle h, int M, int N, int K, const float* dY, const float* X, float* dW, float beta) {
+    const float one = 1.0f;
+    return rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, K, N, M, &one, X, K, dY, N, &beta, dW, K);
 }
 
 }  // namespace
@@ -115,7 +116,9 @@ int rs_trainer_create(const rs_bert_cfg* cfg, int device, rs_trainer** out) {
     if (c.heads <= 0 || c.hidden / c.heads != 64 || c.hidden % c.heads) return rs_fail(RS_EUNSUP, "head_dim must be 64");
     if (c.intermediate <= 0 || c.intermediate % 4) return rs_fail(RS_EUNSUP, "intermediate must be a multiple of 4");
     if (c.layers < 1 || c.vocab < 1 || c.max_pos < 3 || c.type_vocab < 1) return rs_fail(RS_EARG, "bad config");
-    if (c.heads_mask != RS_HEAD_CLS) return rs_fail(RS_EUNSUP, "the trainer supports the RescoreBert head (RS_HEAD_CLS)");
+    if (c.heads_mask != RS_HEAD_CLS && c.heads_mask != RS_HEAD_MLM)
+        return rs_fail(RS_EUNSUP, "the trainer takes one head: RS_HEAD_CLS (RescoreBert) or RS_HEAD_MLM (MLM fine-tuning)");
+    if (c.heads_mask == RS_HEAD_MLM && c.vocab % 4) return rs_fail(RS_EUNSUP, "MLM training needs vocab % 4 == 0");
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || device < 0 || device >= n) return rs_fail(RS_EHIP, "no such HIP device");
     rs_trainer* t = new (std::nothrow) rs_trainer();
@@ -150,8 +153,17 @@ int rs_trainer_create(const rs_bert_cfg* cfg, int device, rs_trainer** out) {
         L.g2 = add_tensor(t, p + "output.LayerNorm.weight", H);
         L.be2 = add_tensor(t, p + "output.LayerNorm.bias", H);
     }
-    t->o_wl = add_tensor(t, "linear.weight", H);
-    t->o_bl = add_tensor(t, "linear.bias", 1);
+    if (c.heads_mask == RS_HEAD_CLS) {
+        t->o_wl = add_tensor(t, "linear.weight", H);
+        t->o_bl = add_tensor(t, "linear.bias", 1);
+    } else {
+        const std::string p = "cls.predictions.";
+        t->o_wt = add_tensor(t, p + "transform.dense.weight", H * H);
+        t->o_bt = add_tensor(t, p + "transform.dense.bias", H);
+        t->o_tg = add_tensor(t, p + "transform.LayerNorm.weight", H);
+        t->o_tb = add_tensor(t, p + "transform.LayerNorm.bias", H);
+        t->o_db = add_tensor(t, p + "bias", V);
+    }
     t->n_params = (t->n_params + 63) / 64 * 64;
     t->host.assign(t->n_params, 0.0f);
     t->set.assign(t->table.size(), 0);
@@ -166,6 +178,8 @@ int rs_trainer_set_tensor(rs_trainer* t, const char* key, const void* host_ptr, 
     if (t->finalized) return rs_fail(RS_ESTATE, "trainer already finalized");
     const std::string k(key);
     if (k.rfind("bert.pooler.", 0) == 0) return RS_OK;   // RescoreBert never uses the pooler output: no gradient
+    // tied to the word embeddings / to cls.predictions.bias (BertForMaskedLM._tied_weights_keys)
+    if (k == "cls.predictions.decoder.weight" || k == "cls.predictions.decoder.bias") return RS_OK;
     auto it = t->table.find(k);
     if (it == t->table.end()) return rs_fail(RS_EARG, "unknown tensor " + k);
     int64_t n = 1;
@@ -221,43 +235,57 @@ int rs_trainer_get_grad(rs_trainer* t, const char* key, void* host_out, int64_t 
     return copy_out(t, t ? t->G : Buf{}, key, host_out, numel);
 }
 
-int rs_train_step_cls(rs_trainer* t, const int32_t* d_tok, const int32_t* h_hyp_off, int32_t n_hyp,
-                      const int32_t* h_utt_off, int32_t n_utt, const float* d_target, const float* d_am,
-                      const float* d_err, const rs_train_opts* o, float* d_scores, float* d_loss, void* stream) {
-    if (!t || !h_hyp_off || !h_utt_off || !o || !d_loss || n_hyp <= 0 || n_utt <= 0 || !d_tok || !d_target)
-        return rs_fail(RS_EARG, "null argument / empty batch");
-    if (!t->finalized) return rs_fail(RS_ESTATE, "rs_trainer_finalize not called");
-    if (o->loss != RS_LOSS_MD && (!d_am || !d_err)) return rs_fail(RS_EARG, "MWER/MWED need am scores and errors");
-    if (o->loss < RS_LOSS_MD || o->loss > RS_LOSS_MWED) return rs_fail(RS_EARG, "unknown loss");
-    if (h_hyp_off[0] != 0 || h_utt_off[0] != 0 || h_utt_off[n_utt] != n_hyp)
-        return rs_fail(RS_EARG, "offsets must start at 0 and utt_off[n_utt] == n_hyp");
-    const rs_bert_cfg& c = t->cfg;
-    const int H = c.hidden, F = c.intermediate, nh = c.heads, NL = c.layers, S = n_hyp;
-    const int M = h_hyp_off[n_hyp];
-    int tmax = 0;
-    for (int s = 0; s < S; ++s) {
-        const int T = h_hyp_off[s + 1] - h_hyp_off[s];
-        if (T < 1) return rs_fail(RS_EARG, "empty hypothesis");
-        tmax = std::max(tmax, T);
+}  // extern "C"
+
+namespace {
+
+// One step's ragged batch: metadata on the device, saved activations, gradient scratch.
+struct StepCtx {
+    rs_trainer* t;
+    hipStream_t st;
+    int M = 0, S = 0, tmax = 0, n_uniq = 0;
+    const int* dm = nullptr;
+    const long long* pofs = nullptr;
+    const int* seq = nullptr;
+    size_t i_tok = 0, i_pos = 0, i_aux = 0, i_utok = 0, i_toff = 0, i_ord = 0;
+    float* x0 = nullptr;
+    float2* st0 = nullptr;
+    struct LA { float *hin, *qkv, *P, *ctx, *x1, *h1, *pre, *act, *x2; float2 *st1, *st2; };
+    std::vector<LA> la;
+    float *dA = nullptr, *dB = nullptr, *dQKV = nullptr, *dF = nullptr, *part = nullptr, *tail = nullptr;
+    // MLM head (RS_HEAD_MLM): transform pre-GELU / GELU out (pre-LN) / LN out, stats, logits
+    float *tpre = nullptr, *tx = nullptr, *th = nullptr, *logits = nullptr;
+    float2* tst = nullptr;
+};
+
+// host metadata + buffers.  aux: extra int32 array uploaded with the metadata (utt_off).
+int prepare(StepCtx& c, const int32_t* d_tok, const int32_t* h_off, int n_seq, const std::vector<int>& aux) {
+    rs_trainer* t = c.t;
+    const rs_bert_cfg& cf = t->cfg;
+    const int H = cf.hidden, F = cf.intermediate, nh = cf.heads, NL = cf.layers;
+    if (n_seq <= 0 || h_off[0] != 0) return rs_fail(RS_EARG, "empty batch or offsets not starting at 0");
+    c.S = n_seq;
+    c.M = h_off[n_seq];
+    for (int s = 0; s < n_seq; ++s) {
+        const int T = h_off[s + 1] - h_off[s];
+        if (T < 1) return rs_fail(RS_EARG, "empty sequence");
+        c.tmax = std::max(c.tmax, T);
     }
-    for (int u = 0; u < n_utt; ++u)
-        if (h_utt_off[u + 1] < h_utt_off[u]) return rs_fail(RS_EARG, "utt_off not ascending");
-    if (tmax > c.max_pos) return rs_fail(RS_EUNSUP, "sequence longer than max_position_embeddings");
-    if (tmax > 128) return rs_fail(RS_EUNSUP, "training sequences are limited to 128 tokens");
-    hipStream_t st = (hipStream_t)stream;
+    if (c.tmax > cf.max_pos) return rs_fail(RS_EUNSUP, "sequence longer than max_position_embeddings");
+    if (c.tmax > 128) return rs_fail(RS_EUNSUP, "training sequences are limited to 128 tokens");
+    const int M = c.M, S = c.S;
+    hipStream_t st = c.st;
     TRY_HIP(hipSetDevice(t->device));
     TRY_BLAS(rocblas_set_stream(t->blas, st));
-
-    // ---- host metadata (tokens come back once for the word-gradient CSR) ----------------
     t->h_tok.resize(M);
     TRY_HIP(hipMemcpyAsync(t->h_tok.data(), d_tok, (size_t)M * 4, hipMemcpyDeviceToHost, st));
     TRY_HIP(hipStreamSynchronize(st));
     std::vector<int> row_pos(M), order(M);
     for (int s = 0; s < S; ++s)
-        for (int r = h_hyp_off[s]; r < h_hyp_off[s + 1]; ++r) row_pos[r] = r - h_hyp_off[s];
+        for (int r = h_off[s]; r < h_off[s + 1]; ++r) row_pos[r] = r - h_off[s];
     for (int r = 0; r < M; ++r) {
         order[r] = r;
-        t->h_tok[r] = std::min(std::max(t->h_tok[r], 0), c.vocab - 1);
+        t->h_tok[r] = std::min(std::max(t->h_tok[r], 0), cf.vocab - 1);
     }
     std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return t->h_tok[a] < t->h_tok[b]; });
     std::vector<int> utok, toff;
@@ -267,149 +295,251 @@ int rs_train_step_cls(rs_trainer* t, const int32_t* d_tok, const int32_t* h_hyp_
             toff.push_back(k);
         }
     toff.push_back(M);
-    const int n_uniq = (int)utok.size();
+    c.n_uniq = (int)utok.size();
     std::vector<long long> pofs(S + 1, 0);
     for (int s = 0; s < S; ++s) {
-        const long long T = h_hyp_off[s + 1] - h_hyp_off[s];
+        const long long T = h_off[s + 1] - h_off[s];
         pofs[s + 1] = pofs[s] + (long long)nh * T * T;
     }
-    // int layout: pofs (int64) | row_tok | row_pos | seq_off | utt_off | utok | toff | order
+    // int layout: pofs (int64) | row_tok | row_pos | seq_off | aux | utok | toff | order
     std::vector<int>& hm = t->h_meta;
     hm.assign(2 * (S + 1), 0);
     std::memcpy(hm.data(), pofs.data(), (S + 1) * 8);
-    const size_t i_tok = hm.size();
+    c.i_tok = hm.size();
     hm.insert(hm.end(), t->h_tok.begin(), t->h_tok.end());
-    const size_t i_pos = hm.size();
+    c.i_pos = hm.size();
     hm.insert(hm.end(), row_pos.begin(), row_pos.end());
     const size_t i_seq = hm.size();
-    hm.insert(hm.end(), h_hyp_off, h_hyp_off + S + 1);
-    const size_t i_utt = hm.size();
-    hm.insert(hm.end(), h_utt_off, h_utt_off + n_utt + 1);
-    const size_t i_utok = hm.size();
+    hm.insert(hm.end(), h_off, h_off + S + 1);
+    c.i_aux = hm.size();
+    hm.insert(hm.end(), aux.begin(), aux.end());
+    c.i_utok = hm.size();
     hm.insert(hm.end(), utok.begin(), utok.end());
-    const size_t i_toff = hm.size();
+    c.i_toff = hm.size();
     hm.insert(hm.end(), toff.begin(), toff.end());
-    const size_t i_ord = hm.size();
+    c.i_ord = hm.size();
     hm.insert(hm.end(), order.begin(), order.end());
     TRY_HIP(t->meta.ensure(hm.size() * 4));
     TRY_HIP(hipMemcpyAsync(t->meta.p, hm.data(), hm.size() * 4, hipMemcpyHostToDevice, st));
-    const int* dm = (const int*)t->meta.p;
-    const long long* d_pofs = (const long long*)dm;
-    const int* d_seq = dm + i_seq;
+    c.dm = (const int*)t->meta.p;
+    c.pofs = (const long long*)c.dm;
+    c.seq = c.dm + i_seq;
 
-    // ---- activation layout (floats) -------------------------------------------------------
+    const bool mlm = cf.heads_mask == RS_HEAD_MLM;
     const size_t MH = (size_t)M * H, MF = (size_t)M * F, M2 = (size_t)M * 2, PS = (size_t)pofs[S];
-    const size_t per_layer = MH /*h_in*/ + 3 * MH /*qkv*/ + PS + MH /*ctx*/ + MH /*x1*/ + M2 + MH /*h1*/ +
-                             2 * MF /*pre, act*/ + MH /*x2*/ + M2;
-    const size_t n_act = MH + M2 /*x0, st0*/ + NL * per_layer + MH /*h_final*/;
+    const size_t MV = mlm ? (size_t)M * cf.vocab : 0;
+    const size_t per_layer = MH + 3 * MH + PS + MH + MH + M2 + MH + 2 * MF + MH + M2;
+    const size_t n_head = mlm ? 3 * MH + M2 + MV : 0;
+    const size_t n_act = MH + M2 + NL * per_layer + MH + n_head;
     TRY_HIP(t->act.ensure(n_act * 4));
-    const size_t n_grad = 2 * MH + 3 * MH + MF + tr_colsum_scratch(M, std::max(3 * H, F)) / 4 + 2 * (size_t)S + n_utt + 64;
+    const int widest = std::max(std::max(3 * H, F), mlm ? cf.vocab : 0);
+    const size_t n_part = tr_colsum_scratch(M, widest) / 4;
+    const size_t n_grad = 2 * MH + 3 * MH + MF + n_part + 2 * (size_t)S + aux.size() + M + 64;
     TRY_HIP(t->grad.ensure(n_grad * 4));
     float* A = t->act.f();
-    float* x0 = A;
-    float2* st0 = (float2*)(x0 + MH);
-    float* lbase = (float*)(st0 + M);
-    struct LA { float *hin, *qkv, *P, *ctx, *x1, *h1, *pre, *act, *x2; float2 *st1, *st2; };
-    std::vector<LA> la(NL + 1);
+    c.x0 = A;
+    c.st0 = (float2*)(c.x0 + MH);
+    float* lbase = (float*)(c.st0 + M);
+    c.la.assign(NL + 1, StepCtx::LA{});
     for (int l = 0; l <= NL; ++l) {
         float* b = lbase + (size_t)l * per_layer;
-        la[l].hin = b;
+        StepCtx::LA& a = c.la[l];
+        a.hin = b;
         if (l == NL) break;
-        la[l].qkv = b + MH;
-        la[l].P = la[l].qkv + 3 * MH;
-        la[l].ctx = la[l].P + PS;
-        la[l].x1 = la[l].ctx + MH;
-        la[l].st1 = (float2*)(la[l].x1 + MH);
-        la[l].h1 = (float*)(la[l].st1 + M);
-        la[l].pre = la[l].h1 + MH;
-        la[l].act = la[l].pre + MF;
-        la[l].x2 = la[l].act + MF;
-        la[l].st2 = (float2*)(la[l].x2 + MH);
+        a.qkv = b + MH;
+        a.P = a.qkv + 3 * MH;
+        a.ctx = a.P + PS;
+        a.x1 = a.ctx + MH;
+        a.st1 = (float2*)(a.x1 + MH);
+        a.h1 = (float*)(a.st1 + M);
+        a.pre = a.h1 + MH;
+        a.act = a.pre + MF;
+        a.x2 = a.act + MF;
+        a.st2 = (float2*)(a.x2 + MH);
     }
-    float* Gd = t->grad.f();
-    float* dA = Gd;
-    float* dB = dA + MH;
-    float* dQKV = dB + MH;
-    float* dF = dQKV + 3 * MH;
-    float* part = dF + MF;
-    float* sc = part + tr_colsum_scratch(M, std::max(3 * H, F)) / 4;
-    float* dsc = sc + S;
-    float* uloss = dsc + S;
-    float* Pm = t->P.f();
-    float* Gm = t->G.f();
-    rocblas_handle bh = t->blas;
+    if (mlm) {
+        c.tpre = c.la[NL].hin + MH;
+        c.tx = c.tpre + MH;
+        c.th = c.tx + MH;
+        c.tst = (float2*)(c.th + MH);
+        c.logits = (float*)(c.tst + M);
+    }
+    float* G = t->grad.f();
+    c.dA = G;
+    c.dB = c.dA + MH;
+    c.dQKV = c.dB + MH;
+    c.dF = c.dQKV + 3 * MH;
+    c.part = c.dF + MF;
+    c.tail = c.part + n_part;        // per-sequence / per-row small arrays
+    return RS_OK;
+}
 
-    // ---- forward --------------------------------------------------------------------------
-    TRY_HIP(tr_embed_ln(dm + i_tok, dm + i_pos, M, c.vocab, Pm + t->o_word, Pm + t->o_pos, Pm + t->o_type,
-                        Pm + t->o_eg, Pm + t->o_eb, c.ln_eps, H, x0, st0, la[0].hin, st));
-    for (int l = 0; l < NL; ++l) {
+int encoder_forward(StepCtx& c) {
+    rs_trainer* t = c.t;
+    const rs_bert_cfg& cf = t->cfg;
+    const int H = cf.hidden, F = cf.intermediate, nh = cf.heads, M = c.M;
+    float* Pm = t->P.f();
+    rocblas_handle bh = t->blas;
+    hipStream_t st = c.st;
+    TRY_HIP(tr_embed_ln(c.dm + c.i_tok, c.dm + c.i_pos, M, cf.vocab, Pm + t->o_word, Pm + t->o_pos, Pm + t->o_type,
+                        Pm + t->o_eg, Pm + t->o_eb, cf.ln_eps, H, c.x0, c.st0, c.la[0].hin, st));
+    for (int l = 0; l < cf.layers; ++l) {
         const TLayer& L = t->lay[l];
-        LA& a = la[l];
+        StepCtx::LA& a = c.la[l];
         TRY_BLAS(gemm_nt(bh, M, 3 * H, H, a.hin, Pm + L.wqkv, a.qkv, 0.f));
         TRY_HIP(tr_bias(a.qkv, Pm + L.bqkv, M, 3 * H, st));
-        TRY_HIP(tr_attn_fwd(a.qkv, d_seq, d_pofs, S, tmax, H, nh, a.P, a.ctx, st));
+        TRY_HIP(tr_attn_fwd(a.qkv, c.seq, c.pofs, c.S, c.tmax, H, nh, a.P, a.ctx, st));
         TRY_BLAS(gemm_nt(bh, M, H, H, a.ctx, Pm + L.wo, a.x1, 0.f));
-        TRY_HIP(tr_bias_res_ln(a.x1, Pm + L.bo, a.hin, M, Pm + L.g1, Pm + L.be1, c.ln_eps, H, a.st1, a.h1, st));
+        TRY_HIP(tr_bias_res_ln(a.x1, Pm + L.bo, a.hin, M, Pm + L.g1, Pm + L.be1, cf.ln_eps, H, a.st1, a.h1, st));
         TRY_BLAS(gemm_nt(bh, M, F, H, a.h1, Pm + L.w1, a.pre, 0.f));
         TRY_HIP(tr_bias_gelu(a.pre, Pm + L.b1, a.act, M, F, st));
         TRY_BLAS(gemm_nt(bh, M, H, F, a.act, Pm + L.w2, a.x2, 0.f));
-        TRY_HIP(tr_bias_res_ln(a.x2, Pm + L.b2, a.h1, M, Pm + L.g2, Pm + L.be2, c.ln_eps, H, a.st2, la[l + 1].hin, st));
+        TRY_HIP(tr_bias_res_ln(a.x2, Pm + L.b2, a.h1, M, Pm + L.g2, Pm + L.be2, cf.ln_eps, H, a.st2,
+                               c.la[l + 1].hin, st));
     }
-    const float* hfin = la[NL].hin;
-    TRY_HIP(tr_cls_fwd(hfin, d_seq, S, H, Pm + t->o_wl, Pm + t->o_bl, sc, st));
-    if (d_scores) TRY_HIP(hipMemcpyAsync(d_scores, sc, (size_t)S * 4, hipMemcpyDeviceToDevice, st));
-    TRY_HIP(tr_loss(sc, d_target, d_am, d_err, dm + i_utt, n_utt, S, o->loss, o->lambda_, dsc, uloss, d_loss, st));
+    return RS_OK;
+}
 
-    // ---- backward -------------------------------------------------------------------------
-    TRY_HIP(hipMemsetAsync(Gm, 0, t->n_params * 4, st));
-    TRY_HIP(hipMemsetAsync(dA, 0, MH * 4, st));
-    TRY_HIP(tr_cls_bwd(dsc, hfin, d_seq, S, H, Pm + t->o_wl, dA, Gm + t->o_wl, Gm + t->o_bl, st));
-    for (int l = NL - 1; l >= 0; --l) {
+// from dA = d(final hidden) down to the embeddings; gradients written into t->G (zeroed by
+// the caller before the head's backward)
+int encoder_backward(StepCtx& c) {
+    rs_trainer* t = c.t;
+    const rs_bert_cfg& cf = t->cfg;
+    const int H = cf.hidden, F = cf.intermediate, nh = cf.heads, M = c.M;
+    const size_t MH = (size_t)M * H, MF = (size_t)M * F;
+    float *Pm = t->P.f(), *Gm = t->G.f();
+    float *dA = c.dA, *dB = c.dB, *dF = c.dF, *dQKV = c.dQKV, *part = c.part;
+    rocblas_handle bh = t->blas;
+    hipStream_t st = c.st;
+    for (int l = cf.layers - 1; l >= 0; --l) {
         const TLayer& L = t->lay[l];
-        LA& a = la[l];
-        // dA = d(LN2 output)
+        StepCtx::LA& a = c.la[l];
         TRY_HIP(tr_colsum(dA, a.x2, a.st2, M, H, 1, part, Gm + L.g2, 0, st));
         TRY_HIP(tr_colsum(dA, nullptr, nullptr, M, H, 0, part, Gm + L.be2, 0, st));
         TRY_HIP(tr_ln_bwd(dA, a.x2, a.st2, Pm + L.g2, dB, M, H, st));              // dB = dx2
         TRY_HIP(tr_colsum(dB, nullptr, nullptr, M, H, 0, part, Gm + L.b2, 0, st));
-        TRY_BLAS(gemm_tn(bh, M, H, F, dB, a.act, Gm + L.w2));
+        TRY_BLAS(gemm_tn(bh, M, H, F, dB, a.act, Gm + L.w2, 0.f));
         TRY_BLAS(gemm_nn(bh, M, H, F, dB, Pm + L.w2, dF, 0.f));                    // d act
         TRY_HIP(tr_gelu_bwd(dF, a.pre, (long long)MF, st));                         // d pre
         TRY_HIP(tr_colsum(dF, nullptr, nullptr, M, F, 0, part, Gm + L.b1, 0, st));
-        TRY_BLAS(gemm_tn(bh, M, F, H, dF, a.h1, Gm + L.w1));
+        TRY_BLAS(gemm_tn(bh, M, F, H, dF, a.h1, Gm + L.w1, 0.f));
         TRY_HIP(hipMemcpyAsync(dA, dB, MH * 4, hipMemcpyDeviceToDevice, st));      // residual
         TRY_BLAS(gemm_nn(bh, M, F, H, dF, Pm + L.w1, dA, 1.f));                     // dA = d h1
         TRY_HIP(tr_colsum(dA, a.x1, a.st1, M, H, 1, part, Gm + L.g1, 0, st));
         TRY_HIP(tr_colsum(dA, nullptr, nullptr, M, H, 0, part, Gm + L.be1, 0, st));
         TRY_HIP(tr_ln_bwd(dA, a.x1, a.st1, Pm + L.g1, dB, M, H, st));              // dB = dx1
         TRY_HIP(tr_colsum(dB, nullptr, nullptr, M, H, 0, part, Gm + L.bo, 0, st));
-        TRY_BLAS(gemm_tn(bh, M, H, H, dB, a.ctx, Gm + L.wo));
+        TRY_BLAS(gemm_tn(bh, M, H, H, dB, a.ctx, Gm + L.wo, 0.f));
         TRY_BLAS(gemm_nn(bh, M, H, H, dB, Pm + L.wo, dA, 0.f));                     // dA = d ctx
-        TRY_HIP(tr_attn_bwd(a.qkv, a.P, dA, d_seq, d_pofs, S, tmax, H, nh, dQKV, st));
+        TRY_HIP(tr_attn_bwd(a.qkv, a.P, dA, c.seq, c.pofs, c.S, c.tmax, H, nh, dQKV, st));
         TRY_HIP(tr_colsum(dQKV, nullptr, nullptr, M, 3 * H, 0, part, Gm + L.bqkv, 0, st));
-        TRY_BLAS(gemm_tn(bh, M, 3 * H, H, dQKV, a.hin, Gm + L.wqkv));
+        TRY_BLAS(gemm_tn(bh, M, 3 * H, H, dQKV, a.hin, Gm + L.wqkv, 0.f));
         TRY_HIP(hipMemcpyAsync(dA, dB, MH * 4, hipMemcpyDeviceToDevice, st));      // residual
         TRY_BLAS(gemm_nn(bh, M, 3 * H, H, dQKV, Pm + L.wqkv, dA, 1.f));             // dA = d h_in
     }
-    TRY_HIP(tr_colsum(dA, x0, st0, M, H, 1, part, Gm + t->o_eg, 0, st));
+    TRY_HIP(tr_colsum(dA, c.x0, c.st0, M, H, 1, part, Gm + t->o_eg, 0, st));
     TRY_HIP(tr_colsum(dA, nullptr, nullptr, M, H, 0, part, Gm + t->o_eb, 0, st));
-    TRY_HIP(tr_ln_bwd(dA, x0, st0, Pm + t->o_eg, dB, M, H, st));                    // dB = dx0
-    TRY_HIP(tr_word_grad(dB, dm + i_utok, dm + i_toff, dm + i_ord, n_uniq, H, Gm + t->o_word, st));
-    TRY_HIP(tr_pos_grad(dB, d_seq, S, tmax, H, Gm + t->o_pos, st));
+    TRY_HIP(tr_ln_bwd(dA, c.x0, c.st0, Pm + t->o_eg, dB, M, H, st));                // dB = dx0
+    // word embeddings: += (the tied MLM decoder already wrote its part)
+    TRY_HIP(tr_word_grad(dB, c.dm + c.i_utok, c.dm + c.i_toff, c.dm + c.i_ord, c.n_uniq, H, Gm + t->o_word, st));
+    TRY_HIP(tr_pos_grad(dB, c.seq, c.S, c.tmax, H, Gm + t->o_pos, st));
     TRY_HIP(tr_colsum(dB, nullptr, nullptr, M, H, 0, part, Gm + t->o_type, 0, st));  // token_type row 0
+    return RS_OK;
+}
 
-    // ---- torch.optim.AdamW ----------------------------------------------------------------
-    if (o->update) {
-        t->step += 1;
-        const double bc1 = 1.0 - std::pow((double)o->beta1, (double)t->step);
-        const double bc2 = 1.0 - std::pow((double)o->beta2, (double)t->step);
-        // python-float (double) scalars as torch computes them, cast to the fp32 tensor dtype
-        const float decay = (float)(1.0 - (double)o->lr * (double)o->weight_decay);
-        TRY_HIP(tr_adamw(Pm, Gm, t->M1.f(), t->V1.f(), (long long)t->n_params, decay,
-                         (float)(1.0 - (double)o->beta1), o->beta2, (float)(1.0 - (double)o->beta2),
-                         (float)((double)o->lr / bc1), (float)std::sqrt(bc2), o->eps, st));
-    }
-    // the metadata upload reads t->h_meta: finish before the host may reuse it
+int adamw(rs_trainer* t, const rs_train_opts* o, hipStream_t st) {
+    if (!o->update) return RS_OK;
+    t->step += 1;
+    const double bc1 = 1.0 - std::pow((double)o->beta1, (double)t->step);
+    const double bc2 = 1.0 - std::pow((double)o->beta2, (double)t->step);
+    // python-float (double) scalars as torch computes them, cast to the fp32 tensor dtype
+    const float decay = (float)(1.0 - (double)o->lr * (double)o->weight_decay);
+    TRY_HIP(tr_adamw(t->P.f(), t->G.f(), t->M1.f(), t->V1.f(), (long long)t->n_params, decay,
+                     (float)(1.0 - (double)o->beta1), o->beta2, (float)(1.0 - (double)o->beta2),
+                     (float)((double)o->lr / bc1), (float)std::sqrt(bc2), o->eps, st));
+    return RS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int rs_train_step_cls(rs_trainer* t, const int32_t* d_tok, const int32_t* h_hyp_off, int32_t n_hyp,
+                      const int32_t* h_utt_off, int32_t n_utt, const float* d_target, const float* d_am,
+                      const float* d_err, const rs_train_opts* o, float* d_scores, float* d_loss, void* stream) {
+    if (!t || !h_hyp_off || !h_utt_off || !o || !d_loss || n_hyp <= 0 || n_utt <= 0 || !d_tok || !d_target)
+        return rs_fail(RS_EARG, "null argument / empty batch");
+    if (!t->finalized) return rs_fail(RS_ESTATE, "rs_trainer_finalize not called");
+    if (t->cfg.heads_mask != RS_HEAD_CLS) return rs_fail(RS_ESTATE, "trainer has no RescoreBert head");
+    if (o->loss < RS_LOSS_MD || o->loss > RS_LOSS_MWED) return rs_fail(RS_EARG, "unknown loss");
+    if (o->loss != RS_LOSS_MD && (!d_am || !d_err)) return rs_fail(RS_EARG, "MWER/MWED need am scores and errors");
+    if (h_utt_off[0] != 0 || h_utt_off[n_utt] != n_hyp) return rs_fail(RS_EARG, "utt_off must span 0..n_hyp");
+    for (int u = 0; u < n_utt; ++u)
+        if (h_utt_off[u + 1] < h_utt_off[u]) return rs_fail(RS_EARG, "utt_off not ascending");
+    StepCtx c;
+    c.t = t;
+    c.st = (hipStream_t)stream;
+    if (int r = prepare(c, d_tok, h_hyp_off, n_hyp, std::vector<int>(h_utt_off, h_utt_off + n_utt + 1))) return r;
+    if (int r = encoder_forward(c)) return r;
+    const int H = t->cfg.hidden, S = c.S;
+    float *Pm = t->P.f(), *Gm = t->G.f();
+    float* sc = c.tail;
+    float* dsc = sc + S;
+    float* uloss = dsc + S;
+    const float* hfin = c.la[t->cfg.layers].hin;
+    hipStream_t st = c.st;
+    TRY_HIP(tr_cls_fwd(hfin, c.seq, S, H, Pm + t->o_wl, Pm + t->o_bl, sc, st));
+    if (d_scores) TRY_HIP(hipMemcpyAsync(d_scores, sc, (size_t)S * 4, hipMemcpyDeviceToDevice, st));
+    TRY_HIP(tr_loss(sc, d_target, d_am, d_err, c.dm + c.i_aux, n_utt, S, o->loss, o->lambda_, dsc, uloss, d_loss, st));
+    TRY_HIP(hipMemsetAsync(Gm, 0, t->n_params * 4, st));
+    TRY_HIP(hipMemsetAsync(c.dA, 0, (size_t)c.M * H * 4, st));
+    TRY_HIP(tr_cls_bwd(dsc, hfin, c.seq, S, H, Pm + t->o_wl, c.dA, Gm + t->o_wl, Gm + t->o_bl, st));
+    if (int r = encoder_backward(c)) return r;
+    if (int r = adamw(t, o, st)) return r;
+    TRY_HIP(hipStreamSynchronize(st));        // the metadata upload read t->h_meta
+    return RS_OK;
+}
+
+int rs_train_step_mlm(rs_trainer* t, const int32_t* d_ids, const int32_t* h_seq_off, int32_t n_seq,
+                      const int32_t* d_labels, const rs_train_opts* o, float* d_loss, void* stream) {
+    if (!t || !h_seq_off || !o || !d_loss || n_seq <= 0 || !d_ids || !d_labels)
+        return rs_fail(RS_EARG, "null argument / empty batch");
+    if (!t->finalized) return rs_fail(RS_ESTATE, "rs_trainer_finalize not called");
+    if (t->cfg.heads_mask != RS_HEAD_MLM) return rs_fail(RS_ESTATE, "trainer has no MLM head");
+    StepCtx c;
+    c.t = t;
+    c.st = (hipStream_t)stream;
+    if (int r = prepare(c, d_ids, h_seq_off, n_seq, {})) return r;
+    if (int r = encoder_forward(c)) return r;
+    const rs_bert_cfg& cf = t->cfg;
+    const int H = cf.hidden, V = cf.vocab, M = c.M;
+    float *Pm = t->P.f(), *Gm = t->G.f();
+    rocblas_handle bh = t->blas;
+    hipStream_t st = c.st;
+    const float* hfin = c.la[cf.layers].hin;
+    // BertOnlyMLMHead: transform (dense + GELU + LN), tied decoder + bias (modeling_bert.py:466-506)
+    TRY_BLAS(gemm_nt(bh, M, H, H, hfin, Pm + t->o_wt, c.tpre, 0.f));
+    TRY_HIP(tr_bias_gelu(c.tpre, Pm + t->o_bt, c.tx, M, H, st));
+    TRY_HIP(tr_bias_res_ln(c.tx, nullptr, nullptr, M, Pm + t->o_tg, Pm + t->o_tb, cf.ln_eps, H, c.tst, c.th, st));
+    TRY_BLAS(gemm_nt(bh, M, V, H, c.th, Pm + t->o_word, c.logits, 0.f));
+    TRY_HIP(tr_bias(c.logits, Pm + t->o_db, M, V, st));
+    float* rl = c.tail;
+    TRY_HIP(tr_ce(c.logits, d_labels, M, V, rl, d_loss, st));       // logits <- dlogits
+    TRY_HIP(hipMemsetAsync(Gm, 0, t->n_params * 4, st));
+    float* dT = c.dB;
+    float* dT2 = c.dF;
+    TRY_HIP(tr_colsum(c.logits, nullptr, nullptr, M, V, 0, c.part, Gm + t->o_db, 0, st));
+    TRY_BLAS(gemm_tn(bh, M, V, H, c.logits, c.th, Gm + t->o_word, 0.f));          // tied decoder part
+    TRY_BLAS(gemm_nn(bh, M, V, H, c.logits, Pm + t->o_word, dT, 0.f));
+    TRY_HIP(tr_colsum(dT, c.tx, c.tst, M, H, 1, c.part, Gm + t->o_tg, 0, st));
+    TRY_HIP(tr_colsum(dT, nullptr, nullptr, M, H, 0, c.part, Gm + t->o_tb, 0, st));
+    TRY_HIP(tr_ln_bwd(dT, c.tx, c.tst, Pm + t->o_tg, dT2, M, H, st));
+    TRY_HIP(tr_gelu_bwd(dT2, c.tpre, (long long)M * H, st));
+    TRY_HIP(tr_colsum(dT2, nullptr, nullptr, M, H, 0, c.part, Gm + t->o_bt, 0, st));
+    TRY_BLAS(gemm_tn(bh, M, H, H, dT2, hfin, Gm + t->o_wt, 0.f));
+    TRY_BLAS(gemm_nn(bh, M, H, H, dT2, Pm + t->o_wt, c.dA, 0.f));                  // dA = d hidden
+    if (int r = encoder_backward(c)) return r;
+    if (int r = adamw(t, o, st)) return r;
     TRY_HIP(hipStreamSynchronize(st));
     return RS_OK;
 }

@@ -183,7 +183,8 @@ typedef struct rs_train_opts {
     int32_t update;        /* 0: gradients only (no optimizer step) */
 } rs_train_opts;
 
-/* cfg->heads_mask must be RS_HEAD_CLS; shapes as rs_model_create (T <= 128 per sequence). */
+/* cfg->heads_mask: RS_HEAD_CLS (RescoreBert) or RS_HEAD_MLM (MLM fine-tuning); shapes as
+ * rs_model_create (T <= 128 per sequence). */
 int rs_trainer_create(const rs_bert_cfg* cfg, int device, rs_trainer** out);
 int rs_trainer_set_tensor(rs_trainer* t, const char* hf_key, const void* host_ptr, int dtype,
                           const int64_t* shape, int ndim);
@@ -195,6 +196,13 @@ int rs_train_step_cls(rs_trainer* t, const int32_t* d_tok, const int32_t* h_hyp_
                       const int32_t* h_utt_off, int32_t n_utt, const float* d_target, const float* d_am,
                       const float* d_err, const rs_train_opts* opts, float* d_scores, float* d_loss,
                       void* stream);
+/* MLM fine-tuning step (MLM_PLL/main.py:117-161 mlm_finetune_bert; trainer created with
+ * heads_mask RS_HEAD_MLM — cls.predictions.* with the decoder tied to the word embeddings):
+ * d_ids / d_labels ragged int32 rows (h_seq_off host int32 [n_seq+1]), e.g. do_job rows of
+ * the reference texts (one [MASK] per row, labels = the unmasked tokens); loss = mean over
+ * all real positions of the CE of BertForMaskedLM's logits.  Synchronises `stream`. */
+int rs_train_step_mlm(rs_trainer* t, const int32_t* d_ids, const int32_t* h_seq_off, int32_t n_seq,
+                      const int32_t* d_labels, const rs_train_opts* opts, float* d_loss, void* stream);
 /* Synchronous copies of one parameter / its last gradient (numel must match). */
 int rs_trainer_get_tensor(rs_trainer* t, const char* hf_key, void* host_out, int64_t numel);
 int rs_trainer_get_grad(rs_trainer* t, const char* hf_key, void* host_out, int64_t numel);

@@ -19,10 +19,12 @@ from .bert_ref import TorchBert
 
 class TorchTrainer:
     def __init__(self, weights: Dict[str, np.ndarray], shape, lr=1e-5, betas=(0.9, 0.999), eps=1e-8,
-                 weight_decay=0.01):
+                 weight_decay=0.01, head: str = "cls"):
         # own copies: TorchBert wraps numpy memory and AdamW updates in place
-        self.model = TorchBert({k: np.array(v, np.float32, copy=True) for k, v in weights.items()
-                                if not k.startswith("bert.pooler.") and not k.startswith("cls.")}, shape)
+        keep = (lambda k: not k.startswith("cls.") and not k.startswith("bert.pooler.")) if head == "cls" else \
+            (lambda k: not k.startswith("linear.") and not k.startswith("bert.pooler.")
+             and not k.startswith("cls.predictions.decoder."))
+        self.model = TorchBert({k: np.array(v, np.float32, copy=True) for k, v in weights.items() if keep(k)}, shape)
         for t in self.model.w.values():
             t.requires_grad_(True)
         self.opt = torch.optim.AdamW(list(self.model.w.values()), lr=lr, betas=betas, eps=eps,
@@ -71,3 +73,23 @@ class TorchTrainer:
 
     def tensor(self, key: str) -> np.ndarray:
         return self.model.w[key].detach().numpy()
+
+
+    def step_mlm(self, ids: np.ndarray, seq_off: np.ndarray, labels: np.ndarray, update=True) -> float:
+        """BertForMaskedLM CE over every real position (pads ignored), mean; AdamW."""
+        seqs = [ids[seq_off[i]:seq_off[i + 1]] for i in range(len(seq_off) - 1)]
+        T = max(len(x) for x in seqs)
+        x = torch.zeros(len(seqs), T, dtype=torch.long)
+        am = torch.zeros(len(seqs), T, dtype=torch.long)
+        lab = torch.full((len(seqs), T), -100, dtype=torch.long)
+        for i, sq in enumerate(seqs):
+            x[i, :len(sq)] = torch.as_tensor(sq.astype(np.int64))
+            am[i, :len(sq)] = 1
+            lab[i, :len(sq)] = torch.as_tensor(labels[seq_off[i]:seq_off[i + 1]].astype(np.int64))
+        self.opt.zero_grad(set_to_none=False)
+        logits = self.model.mlm_logits(self.model.encoder(x, am))
+        loss = torch.nn.functional.cross_entropy(logits.view(-1, logits.shape[-1]), lab.view(-1), ignore_index=-100)
+        loss.backward()
+        if update:
+            self.opt.step()
+        return float(loss.detach())

@@ -101,3 +101,47 @@ def test_trained_checkpoint_feeds_the_scorer_and_is_deterministic():
     finally:
         scorer.close()
     assert np.abs(got - sc).max() <= 1e-4 * max(1.0, np.abs(sc).max())
+
+
+def test_mlm_finetune_matches_autograd_and_feeds_the_pll_scorer():
+    """MLM fine-tuning (MLM_PLL/main.py:117-161) on do_job rows: loss and every gradient vs
+    torch autograd, AdamW updates vs torch.optim.AdamW, checkpoint -> PLLScorer."""
+    from asr_rescoring_amd.scorer import PLLScorer
+    from asr_rescoring_amd.train import MLMTrainer, do_job_rows
+    from oracle.train_ref import TorchTrainer
+    w = make_weights(BERT_TINY, seed=6)
+    tr = MLMTrainer(w, BERT_TINY, lr=1e-3)
+    ref = TorchTrainer(w, BERT_TINY, lr=1e-3, head="mlm")
+    try:
+        for step in range(2):
+            nb, seqs, *_ = _batch(30 + step, n_utt=2, n_best=3, len_hi=12)
+            ids, off, lab = do_job_rows(seqs)
+            l = tr.step(ids, off, lab)
+            rl = ref.step_mlm(ids, off, lab)
+            assert abs(l - rl) <= 1e-4 * abs(rl), (step, l, rl)
+            if step == 0:
+                gn = np.sqrt(sum(float(np.sum(ref.model.w[k].grad.numpy().astype(np.float64) ** 2))
+                                 for k in tr.shapes))
+                for k in tr.shapes:
+                    g, rg = tr.grad(k), ref.model.w[k].grad.numpy()
+                    rel = np.linalg.norm(g - rg) / max(np.linalg.norm(rg), 1e-4 * gn)
+                    assert rel < 2e-4, (k, rel)
+        worst = {}
+        for k in tr.shapes:
+            if k.endswith("attention.self.key.bias"):
+                continue
+            d, dr = tr.tensor(k) - w[k], ref.tensor(k) - w[k]
+            worst[k] = float(np.linalg.norm(d - dr) / max(np.linalg.norm(dr), 1e-12))
+        assert max(worst.values()) < 2e-2, sorted(worst.items(), key=lambda kv: -kv[1])[:4]
+        sd = tr.state_dict()
+    finally:
+        tr.close()
+    nb, seqs, *_ = _batch(40, n_utt=2, n_best=3, len_hi=12)
+    sc = PLLScorer(sd, BERT_TINY, device=0, precision="fp16x3")
+    try:
+        got = sc.score(nb)
+    finally:
+        sc.close()
+    from oracle.bert_ref import TorchBert, pll_reference_pattern
+    _, want = pll_reference_pattern(TorchBert(sd, BERT_TINY), nb.tokens, nb.hyp_off, full_head=False)
+    assert (np.abs(got - want) / np.abs(want)).max() < 1e-3
