@@ -1,6 +1,7 @@
 """Command-line drivers with the reference's entry points, YAML keys and output files.
 
   python -m asr_rescoring_amd.cli mlm_pll     --config score.yaml    # MLM_PLL/main.py (task: scoring)
+  python -m asr_rescoring_amd.cli mlm_finetune --config train.yaml   # MLM_PLL/main.py (task: train)
   python -m asr_rescoring_amd.cli rescorebert --config MD_score.yaml # RescoreBert/main.py (task: scoring)
   python -m asr_rescoring_amd.cli rescorebert_train --config MD.yaml # RescoreBert/main.py (task: train)
   python -m asr_rescoring_amd.cli rescore     --config rescore.yaml  # rescore.py
@@ -109,6 +110,57 @@ def mlm_pll(cfg) -> Dict[str, str]:
         out_files[split] = path
     scorer.close()
     return out_files
+
+
+def mlm_finetune(cfg) -> Dict[str, object]:
+    """MLM_PLL/main.py:117-161 (mlm_finetune_bert) on the native trainer (``train.MLMTrainer``).
+
+    Data: ``train_data_path`` (preprocessed ``do_job`` rows: input_ids / labels) or
+    ``train_ref_text_path`` ({utt: text}; tokenised and expanded by ``do_job_rows``).  Keys:
+    ``epochs``, ``batch_size`` (rows per step, 32), ``lr``, ``weight_decay``, ``shuffle`` +
+    ``seed``; AdamW is re-created every epoch as the reference does (``:76``,
+    ``reset_optimizer`` false keeps it).  Writes ``checkpoint_{epoch}.pt`` per epoch (``:157``)."""
+    import torch
+    from .train import MLMTrainer, do_job_rows
+    os.makedirs(cfg.output_path, exist_ok=True)
+    log = _logger(os.path.join(cfg.output_path, "train.log"))
+    rows_path, ref_path = get(cfg, "train_data_path"), get(cfg, "train_ref_text_path")
+    if rows_path and os.path.exists(rows_path):
+        rows = _load(rows_path)
+        seqs = [r["input_ids"] for r in rows]
+        labs = [r["labels"] for r in rows]
+    else:
+        refs = _load(ref_path)
+        tok = _tokenizer(cfg, list(refs.values()))
+        hyps = [[101] + list(tok.encode_words(t)) + [102] for t in refs.values()]
+        ids, off, lab = do_job_rows(hyps)
+        seqs = [ids[off[i]:off[i + 1]].tolist() for i in range(len(off) - 1)]
+        labs = [lab[off[i]:off[i + 1]].tolist() for i in range(len(off) - 1)]
+    tr = MLMTrainer(_weights(cfg, "mlm"), BERT_BASE, device=_dev(cfg), lr=float(get(cfg, "lr", 1e-5)),
+                    weight_decay=float(get(cfg, "weight_decay", 0.01)))
+    bs = int(get(cfg, "batch_size", 32))
+    rng = np.random.default_rng(int(get(cfg, "seed", 0)))
+    losses, ckpts = [], []
+    for ep in range(int(get(cfg, "epochs", 1))):
+        if ep and get(cfg, "reset_optimizer", True):
+            tr.reset_optimizer()
+        order = rng.permutation(len(seqs)) if get(cfg, "shuffle", True) else np.arange(len(seqs))
+        tot, nb_ = 0.0, 0
+        for b0 in range(0, len(order), bs):
+            idx = order[b0:b0 + bs]
+            off = np.zeros(len(idx) + 1, np.int32)
+            off[1:] = np.cumsum([len(seqs[i]) for i in idx])
+            ids = np.concatenate([np.asarray(seqs[i], np.int32) for i in idx])
+            lab = np.concatenate([np.asarray(labs[i], np.int32) for i in idx])
+            tot += tr.step(ids, off, lab)
+            nb_ += 1
+        losses.append(tot / max(nb_, 1))
+        log.info(f"epoch {ep + 1} loss {losses[-1]}")
+        path = os.path.join(cfg.output_path, f"checkpoint_{ep + 1}.pt")
+        torch.save({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in tr.state_dict().items()}, path)
+        ckpts.append(path)
+    tr.close()
+    return {"losses": losses, "checkpoints": ckpts}
 
 
 def rescorebert(cfg) -> Dict[str, str]:
@@ -306,7 +358,8 @@ def _logger(path):
     return log
 
 
-COMMANDS = {"mlm_pll": mlm_pll, "rescorebert": rescorebert, "rescorebert_train": rescorebert_train,
+COMMANDS = {"mlm_pll": mlm_pll, "mlm_finetune": mlm_finetune, "rescorebert": rescorebert,
+            "rescorebert_train": rescorebert_train,
             "rescore": rescore, "rmbr": rmbr}
 
 
