@@ -169,10 +169,32 @@ def c2train():
              "ms_per_step": round(dt * 1e3, 1), "tflops_fp32": round(fl / dt / 1e12, 1)}]
 
 
+def mlmtrain():
+    """MLM fine-tuning on bert-base: do_job rows of 32 reference sentences (L ~ U{24..40}),
+    rows / s (one row = one masked copy) and fp32 TFLOP/s (3 x forward incl. the full-vocab head)."""
+    from asr_rescoring_amd.train import MLMTrainer, do_job_rows
+    w = make_weights(BERT_BASE, seed=1234)
+    tr = MLMTrainer(w, BERT_BASE, lr=1e-5)
+    nb = D.synthetic_nbest(32, 1, seed=1)
+    seqs = [nb.tokens[nb.hyp_off[h]:nb.hyp_off[h + 1]].tolist() for h in range(nb.n_hyp)]
+    ids, off, lab = do_job_rows(seqs)
+    o = off[:161]
+    step = lambda: tr.step(ids[:o[-1]], o, lab[:o[-1]])
+    dt = _timed(step, steps=5, warmup=2)
+    tr.close()
+    T = np.diff(o).astype(np.float64)
+    H, F, L, V = BERT_BASE.hidden, BERT_BASE.intermediate, BERT_BASE.layers, BERT_BASE.vocab
+    fl = 3.0 * (float(T.sum()) * (L * 2 * (4 * H * H + 2 * H * F) + 2 * (H * H + H * V)) + L * 4 * float((T * T).sum()) * H)
+    return [{"workload": "MLM fine-tuning, bert-base, 160 do_job rows per step (fp32)", "value": round(160 / dt, 1),
+             "unit": "rows/s", "tokens_per_step": int(T.sum()), "ms_per_step": round(dt * 1e3, 1),
+             "tflops_fp32": round(fl / dt / 1e12, 1)}]
+
+
 def main():
     which = sys.argv[1].split(",") if len(sys.argv) > 1 else ["c2", "c4", "c5", "c5bs"]
     for name in which:
-        for rec in {"c2": c2, "c4": c4, "c5": c5, "c5bs": c5bs, "c2train": c2train}[name]():
+        for rec in {"c2": c2, "c4": c4, "c5": c5, "c5bs": c5bs, "c2train": c2train,
+                    "mlmtrain": mlmtrain}[name]():
             print(json.dumps(rec), flush=True)
 
 
