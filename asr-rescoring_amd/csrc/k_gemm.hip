@@ -61,6 +61,22 @@ __device__ __forceinline__ void st16(uint4* p, uint4 v) {
     else *p = v;
 }
 
+// MFMA shape abstraction: MS = 32 -> v_mfma_f32_32x32x16_f16 (16 accumulators per lane,
+// 4 column quads), MS = 16 -> v_mfma_f32_16x16x32_f16 (4 accumulators, 1 quad).  Operands
+// swapped (D = W_tile . A_tile^T): lane l owns output row (l % MS) of the block and, per quad
+// g, the 4 consecutive columns qcol(g, l); fragment reads: lane l takes the 16 bytes of tile
+// row (l % MS) at k-chunk (l / MS) of the substep (KPS = 512 / MS k per MFMA).
+template <int MS> struct AccT;
+template <> struct AccT<32> { typedef f32x16 type; };
+template <> struct AccT<16> { typedef f32x4 type; };
+template <int MS>
+__device__ __forceinline__ typename AccT<MS>::type mfma_f16(half8 a, half8 b, typename AccT<MS>::type c) {
+    if constexpr (MS == 32) return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+    else return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
+template <int MS>
+__device__ __forceinline__ int qcol(int g, int lane) { return MS == 32 ? 8 * g + 4 * (lane >> 5) : 4 * (lane >> 4); }
+
 // VAR = variant bits.  Production: 128 (K loop software-pipelined by sched_group_barrier)
 // and 64 (non-temporal epilogue stores).  Alternatives kept for timing: 256 (front-loaded
 // read schedule), 32 (direct permlane epilogue, no LDS pass).  Timing experiments only
@@ -76,7 +92,12 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     constexpr int A_BYTES = BM * BK * 2;
     constexpr int STAGE = (BM + BN) * BK * 2;
     constexpr int WTM = BM / WM, WTN = BN / WN;
-    constexpr int TM = WTM / 32, TN = WTN / 32;
+    constexpr int MS = (VAR & 8192) ? 16 : 32;         // MFMA shape (VAR bit 8192: 16x16x32)
+    constexpr int KPS = 512 / MS, CPS = KPS / 8, NQ = MS * MS / 256;
+    typedef typename AccT<MS>::type accT;
+    constexpr int TM = WTM / MS, TN = WTN / MS;
+    static_assert(MS == 32 || (!(VAR & (4 | 32 | 256 | 1024 | 2048)) && EPI != EPI_LSE && BK / KPS >= 2),
+                  "16x16x32 MFMA: default K loop and the LDS epilogue only");
     constexpr int RB = BK * 2;            // LDS row bytes
     constexpr int CPR = BK / 8;           // 16-byte chunks per row
     constexpr int RPP = 1024 / RB;        // rows per 1 KiB LDS-DMA piece
@@ -136,21 +157,21 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
 
     // Accumulators start at bias (+ residual): these loads' latency hides behind the whole
     // K loop and the epilogue only converts / activates / stores.
-    //   acc[i][j][4g + e] <-> C[m0 + wm*WTM + 32i + (lane&31)][n0 + wn*WTN + 32j + 8g + 4(lane>>5) + e]
-    f32x16 acc[TM][TN];
+    //   acc[i][j][4g + e] <-> C[m0 + wm*WTM + MS*i + (lane%MS)][n0 + wn*WTN + MS*j + qcol(g) + e]
+    accT acc[TM][TN];
     {
-        const int arow = m0 + wm * WTM + (lane & 31);
-        const int acol = n0 + wn * WTN + 4 * (lane >> 5);
+        const int arow = m0 + wm * WTM + (lane % MS);
+        const int acol = n0 + wn * WTN;
         float2 rst[TM];                       // EPI_RESLN_F32: LN statistics of the residual rows
         if constexpr (EPI == EPI_RESLN_F32) {
 #pragma unroll
-            for (int i = 0; i < TM; ++i) rst[i] = ep.res_stats[arow + 32 * i];
+            for (int i = 0; i < TM; ++i) rst[i] = ep.res_stats[arow + MS * i];
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const int col = acol + 32 * j + 8 * g;
+            for (int g = 0; g < NQ; ++g) {
+                const int col = acol + MS * j + qcol<MS>(g, lane);
                 const float4 b4 = (VAR & 2) ? make_float4(0.f, 0.f, 0.f, 0.f) : *(const float4*)(ep.bias + col);
                 float4 lg4, lb4;
                 if constexpr (EPI == EPI_RESLN_F32) {
@@ -161,7 +182,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 for (int i = 0; i < TM; ++i) {
                     float4 v = b4;
                     if constexpr ((EPI == EPI_RES_F32 || EPI == EPI_RESLN_F32) && !(VAR & 2)) {
-                        float4 r4 = *(const float4*)(ep.res + (size_t)(arow + 32 * i) * ep.ldc + col);
+                        float4 r4 = *(const float4*)(ep.res + (size_t)(arow + MS * i) * ep.ldc + col);
                         if constexpr (EPI == EPI_RESLN_F32) {
                             r4.x = ln_apply(r4.x, rst[i], lg4.x, lb4.x);
                             r4.y = ln_apply(r4.y, rst[i], lg4.y, lb4.y);
@@ -183,7 +204,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     for (int s = 0; s < NSTAGE - 1; ++s)
         if (s < nk) stage(s, s * BK);
 
-    const int frow = lane & 31, fh = lane >> 5;
+    const int frow = lane % MS, fh = lane / MS;
     if constexpr (NSTAGE == 2 && WM == 2 && BK == 64 && (VAR & 2048)) {
         // Ping-pong: the two wave rows (grp = wm; every SIMD holds one wave of each) run one
         // barrier apart, so while one issues its MFMA cluster the other reads its next
@@ -331,7 +352,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         }
         if constexpr (VAR & 384) __builtin_amdgcn_sched_barrier(0);
         // VAR&4: the next stage's LDS-DMA pieces are spread over the MFMA clusters
-        constexpr int NSUB = BK / 16;          // k-substeps per stage
+        constexpr int NSUB = BK / KPS;         // k-substeps per stage
         auto stage_part = [&](int q) {
             if constexpr (VAR & 4) {
                 __builtin_amdgcn_sched_barrier(0);
@@ -350,15 +371,15 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         // fragments of k-substep s+1 are read while the MFMAs of substep s issue
         half8 af0[TM], bf0[TN], af1[TM], bf1[TN];
         auto load_frags = [&](int s, half8 (&af)[TM], half8 (&bf)[TN]) {
-            const int lc = 2 * s + fh;
+            const int lc = CPS * s + fh;
 #pragma unroll
             for (int j = 0; j < TN; ++j) {
-                const int row = wn * WTN + j * 32 + frow;
+                const int row = wn * WTN + j * MS + frow;
                 bf[j] = *(const half8*)(sB + row * RB + (swz<BK>(row, lc) << 4));
             }
 #pragma unroll
             for (int i = 0; i < TM; ++i) {
-                const int row = wm * WTM + i * 32 + frow;
+                const int row = wm * WTM + i * MS + frow;
                 af[i] = *(const half8*)(sA + row * RB + (swz<BK>(row, lc) << 4));
             }
         };
@@ -367,13 +388,14 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             for (int i = 0; i < TM; ++i)
 #pragma unroll
                 for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+                    acc[i][j] = mfma_f16<MS>(bf[j], af[i], acc[i][j]);
         };
+        static_assert(NSUB == 2 || NSUB == 4, "substeps per stage");
         load_frags(0, af0, bf0);
         load_frags(1, af1, bf1);
         mfmas(af0, bf0);
         stage_part(0);
-        if constexpr (BK == 64) {
+        if constexpr (NSUB == 4) {
             load_frags(2, af0, bf0);
             mfmas(af1, bf1);
             stage_part(1);
@@ -551,17 +573,21 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         const int rr0 = lane / LPR, cc = (lane % LPR) * 8;
         const int col = n0 + wn * WTN + cc;
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
+        for (int i32 = 0; i32 < WTM / 32; ++i32) {     // 32-row slices of the wave tile
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
+            for (int sub = 0; sub < 32 / MS; ++sub) {
+                const int i = i32 * (32 / MS) + sub;
 #pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    *(float4*)(lw + frow * LDW + j * 32 + 8 * g + 4 * fh) =
-                        make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int g = 0; g < NQ; ++g)
+                        *(float4*)(lw + (sub * MS + frow) * LDW + j * MS + qcol<MS>(g, lane)) =
+                            make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]);
+            }
 #pragma unroll
             for (int it = 0; it < NIT; ++it) {
                 const int rr = it * RPI + rr0;
-                const int row = m0 + wm * WTM + i * 32 + rr;
+                const int row = m0 + wm * WTM + i32 * 32 + rr;
                 const float4 u0 = *(const float4*)(lw + rr * LDW + cc);
                 const float4 u1 = *(const float4*)(lw + rr * LDW + cc + 4);
                 float x[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
@@ -627,12 +653,16 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
                     int n_tiles, EpiArgs ep) {
     constexpr int BM = 256, BN = 256, WN = 4, BK = 64, NW = 8;
     constexpr int A_BYTES = BM * BK * 2, STAGE = (BM + BN) * BK * 2;
-    constexpr int WTM = 128, WTN = 64, TM = 4, TN = 2;
+    constexpr int WTM = 128, WTN = 64;
+    constexpr int MS = (VAR & 8192) ? 16 : 32;    // MFMA shape (VAR bit 8192: 16x16x32)
+    constexpr int KPS = 512 / MS, CPS = KPS / 8, NQ = MS * MS / 256;
+    typedef typename AccT<MS>::type accT;
+    constexpr int TM = WTM / MS, TN = WTN / MS, NBQ = TN * NQ;   // NBQ: bias quads per lane
     constexpr int RB = BK * 2, CPR = BK / 8, RPP = 1024 / RB;
     constexpr int A_PIECES = BM / RPP, PIECES = (BM + BN) / RPP, PPW = PIECES / NW;
     constexpr int LDH = WTN + 8;                  // epilogue slab row, halfs (16-B aligned rows)
-    constexpr int NSTORE = TM * 4;                // 16-B stores per wave per tile
-    constexpr int NSUB = BK / 16, NR = TM + TN, NM = TM * TN;
+    constexpr int NSTORE = (WTM / 32) * 4;        // 16-B stores per wave per tile
+    constexpr int NSUB = BK / KPS, NR = TM + TN, NM = TM * TN;
     static_assert(EPI == EPI_BIAS_F16 || EPI == EPI_GELU_F16, "fp16-output epilogues only");
     static_assert(NW * 32 * LDH * 2 <= STAGE, "epilogue slab fits in one buffer");
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -640,7 +670,7 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
-    const int frow = lane & 31, fh = lane >> 5;
+    const int frow = lane % MS, fh = lane / MS;
     const int nk = K / BK;
 
     int t = blockIdx.x;
@@ -679,22 +709,29 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
         }
     };
     typedef float f32x4 __attribute__((ext_vector_type(4)));
-    f32x4 bz[TN][4];                              // bias of the tile about to start
+    f32x4 bz[NBQ];                                // bias of the tile about to start (quad j*NQ+g)
     auto load_bias = [&](int n0) {
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-            for (int g = 0; g < 4; ++g) {
-                const float* bp = ep.bias + n0 + wn * WTN + 4 * fh + 32 * j + 8 * g;
-                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bz[j][g]) : "v"(bp) : "memory");
+            for (int g = 0; g < NQ; ++g) {
+                const float* bp = ep.bias + n0 + wn * WTN + MS * j + qcol<MS>(g, lane);
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bz[j * NQ + g]) : "v"(bp) : "memory");
             }
     };
+    static_assert(NBQ == 8 || NBQ == 4, "RS_PERSIST_WAIT operand list");
 #define RS_PERSIST_WAIT(N)                                                                         \
-    asm volatile("s_waitcnt vmcnt(" #N ")"                                                         \
-                 : "+v"(bz[0][0]), "+v"(bz[0][1]), "+v"(bz[0][2]), "+v"(bz[0][3]), "+v"(bz[1][0]),  \
-                   "+v"(bz[1][1]), "+v"(bz[1][2]), "+v"(bz[1][3])                                   \
-                 :                                                                                  \
-                 : "memory")
+    if constexpr (NBQ == 8)                                                                        \
+        asm volatile("s_waitcnt vmcnt(" #N ")"                                                     \
+                     : "+v"(bz[0]), "+v"(bz[1]), "+v"(bz[2]), "+v"(bz[3]), "+v"(bz[4]), "+v"(bz[5]), \
+                       "+v"(bz[6]), "+v"(bz[7])                                                     \
+                     :                                                                              \
+                     : "memory");                                                                   \
+    else                                                                                            \
+        asm volatile("s_waitcnt vmcnt(" #N ")"                                                     \
+                     : "+v"(bz[0]), "+v"(bz[1]), "+v"(bz[2]), "+v"(bz[3])                           \
+                     :                                                                              \
+                     : "memory")
 
     int m0, n0;
     tile_of(t, m0, n0);
@@ -705,17 +742,17 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
     const int offA = (wm * WTM + frow) * RB + (swz<BK>(wm * WTM + frow, fh) << 4);
     const int offB = A_BYTES + (wn * WTN + frow) * RB + (swz<BK>(wn * WTN + frow, fh) << 4);
     for (;;) {
-        f32x16 acc[TM][TN];
+        accT acc[TM][TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
             for (int j = 0; j < TN; ++j)
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    acc[i][j][4 * g] = bz[j][g].x;
-                    acc[i][j][4 * g + 1] = bz[j][g].y;
-                    acc[i][j][4 * g + 2] = bz[j][g].z;
-                    acc[i][j][4 * g + 3] = bz[j][g].w;
+                for (int g = 0; g < NQ; ++g) {
+                    acc[i][j][4 * g] = bz[j * NQ + g].x;
+                    acc[i][j][4 * g + 1] = bz[j * NQ + g].y;
+                    acc[i][j][4 * g + 2] = bz[j * NQ + g].z;
+                    acc[i][j][4 * g + 3] = bz[j * NQ + g].w;
                 }
         // ---- K loop: stage kt landed (this tile's stage 0 was waited with the bias)
         for (int kt = 0; kt < nk; ++kt) {
@@ -725,27 +762,65 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
             __builtin_amdgcn_sched_barrier(0);
             const char* sb = smem + (kt & 1) * STAGE;
             half8 af0[TM], bf0[TN], af1[TM], bf1[TN];
+            // substep s covers chunks CPS*s .. CPS*s + CPS-1: one XOR of the per-lane base
             auto load_frags = [&](int s, half8 (&af)[TM], half8 (&bf)[TN]) {
-                const int xa = offA ^ (s << 5), xb = offB ^ (s << 5);
+                const int xa = offA ^ ((CPS * s) << 4), xb = offB ^ ((CPS * s) << 4);
 #pragma unroll
-                for (int j = 0; j < TN; ++j) bf[j] = *(const half8*)(sb + xb + j * 32 * RB);
+                for (int j = 0; j < TN; ++j) bf[j] = *(const half8*)(sb + xb + j * MS * RB);
 #pragma unroll
-                for (int i = 0; i < TM; ++i) af[i] = *(const half8*)(sb + xa + i * 32 * RB);
+                for (int i = 0; i < TM; ++i) af[i] = *(const half8*)(sb + xa + i * MS * RB);
             };
             auto mfmas = [&](const half8 (&af)[TM], const half8 (&bf)[TN]) {
 #pragma unroll
                 for (int i = 0; i < TM; ++i)
 #pragma unroll
                     for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
+                        acc[i][j] = mfma_f16<MS>(bf[j], af[i], acc[i][j]);
             };
+            static_assert(NSUB == 2 || NSUB == 4, "substeps per K-step");
+            if constexpr (MS == 16 && (VAR & 16384)) {
+                // Rolling fragments (16x16x32, NSUB = 2): the B fragments are double-buffered,
+                // the A fragment i of substep 1 is read into af0[i] right after the MFMAs
+                // reading it retire from issue: 128 accumulator + 64 fragment registers.
+                static_assert(NSUB == 2, "rolling schedule: two substeps per K-step");
+                const int xa1 = offA ^ (CPS << 4), xb1 = offB ^ (CPS << 4);
+                load_frags(0, af0, bf0);
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+#pragma unroll
+                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f16<MS>(bf0[j], af0[i], acc[i][j]);
+                    if (i == 0) {
+#pragma unroll
+                        for (int j = 0; j < TN; ++j) bf1[j] = *(const half8*)(sb + xb1 + j * MS * RB);
+                    }
+                    af0[i] = *(const half8*)(sb + xa1 + i * MS * RB);
+                }
+                mfmas(af0, bf1);
+                __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                }
+#pragma unroll
+                for (int i = 1; i < TM; ++i) {
+                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                    __builtin_amdgcn_sched_group_barrier(0x008, TN - 1, 0);
+                }
+                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+                continue;
+            }
             load_frags(0, af0, bf0);
             load_frags(1, af1, bf1);
             mfmas(af0, bf0);
-            load_frags(2, af0, bf0);
-            mfmas(af1, bf1);
-            load_frags(3, af1, bf1);
-            mfmas(af0, bf0);
+            if constexpr (NSUB == 4) {
+                load_frags(2, af0, bf0);
+                mfmas(af1, bf1);
+                load_frags(3, af1, bf1);
+                mfmas(af0, bf0);
+            }
             mfmas(af1, bf1);
             __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
 #pragma unroll
@@ -765,23 +840,27 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
         // whole-row registers; no LDS access follows the next tile's DMA issue below
         f16* slab = (f16*)(smem + STAGE) + wave * 32 * LDH;
         const int rr0 = lane >> 3, cc = (lane & 7) * 8;
-        uint4 ov[TM][4];
+        uint4 ov[WTM / 32][4];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
+        for (int i32 = 0; i32 < WTM / 32; ++i32) {     // 32-row slices of the wave tile
 #pragma unroll
-            for (int j = 0; j < TN; ++j)
+            for (int sub = 0; sub < 32 / MS; ++sub) {
+                const int i = i32 * (32 / MS) + sub;
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    float x[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-                    if constexpr (EPI == EPI_GELU_F16) {
-                        const f32x2 a = gelu2((f32x2){x[0], x[1]}), b = gelu2((f32x2){x[2], x[3]});
-                        x[0] = a.x; x[1] = a.y; x[2] = b.x; x[3] = b.y;
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int g = 0; g < NQ; ++g) {
+                        float x[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+                        if constexpr (EPI == EPI_GELU_F16) {
+                            const f32x2 a = gelu2((f32x2){x[0], x[1]}), b = gelu2((f32x2){x[2], x[3]});
+                            x[0] = a.x; x[1] = a.y; x[2] = b.x; x[3] = b.y;
+                        }
+                        const half4 h = {(f16)x[0], (f16)x[1], (f16)x[2], (f16)x[3]};
+                        *(half4*)(slab + (sub * MS + frow) * LDH + MS * j + qcol<MS>(g, lane)) = h;
                     }
-                    const half4 h = {(f16)x[0], (f16)x[1], (f16)x[2], (f16)x[3]};
-                    *(half4*)(slab + frow * LDH + 32 * j + 8 * g + 4 * fh) = h;
-                }
+            }
 #pragma unroll
-            for (int it = 0; it < 4; ++it) ov[i][it] = *(const uint4*)(slab + (it * 8 + rr0) * LDH + cc);
+            for (int it = 0; it < 4; ++it) ov[i32][it] = *(const uint4*)(slab + (it * 8 + rr0) * LDH + cc);
         }
         // part 2: the next tile's stage 0 (buffer 0) and bias
         const int cm0 = m0, cn0 = n0;
@@ -796,7 +875,7 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
         // part 3: this tile's stores (whole 128-B row segments, non-temporal)
         f16* obase = (f16*)ep.out + (size_t)(cm0 + wm * WTM + rr0) * ep.ldc + cn0 + wn * WTN + cc;
 #pragma unroll
-        for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < WTM / 32; ++i)
 #pragma unroll
             for (int it = 0; it < 4; ++it)
                 st16<64>((uint4*)(obase + (size_t)(i * 32 + it * 8) * ep.ldc), ov[i][it]);
@@ -896,13 +975,26 @@ hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
         return f16;
     }();
     const int cfg = pick_cfg(N_pad);
+    // MFMA shape: 16x16x32 by default (RS_GEMM_MS=32 selects 32x32x16).  Same cycles per
+    // FLOP, but the chip holds a higher clock under the 16x16 loop on random data
+    // (MI355X_MICROARCH.md 'DVFS give-back' item 7): +5-8 % on the pipelined kernel
+    // (tools/gemm_bench.py, profiles/r1_gemm_ms16.txt) and -5..-7 % O-proj / FFN2 time end to
+    // end.  The persistent kernel keeps 32x32x16 (RS_GEMM_MS_PERSIST=16 to switch): with 16x16
+    // its QKV launches took +7 % end to end.  The decoder's logsumexp epilogue keeps 32x32x16.
+    static const int ms = getenv("RS_GEMM_MS") ? atoi(getenv("RS_GEMM_MS")) : 16;
+    static const int ms_p = getenv("RS_GEMM_MS_PERSIST") ? atoi(getenv("RS_GEMM_MS_PERSIST")) : 32;
     // RS_GEMM_PERSIST=0 disables the persistent kernel (fp16-output epilogues, kx = 1)
     static const int persist = getenv("RS_GEMM_PERSIST") ? atoi(getenv("RS_GEMM_PERSIST")) : 1;
     if constexpr (EPI == EPI_BIAS_F16 || EPI == EPI_GELU_F16) {
         if (persist && cfg == 0 && (EPI == EPI_BIAS_F16 || ep.kx == 1))
-            return launch_persist<EPI>(A, W, M_pad, N_pad, K, ep, st);
+            return ms_p == 16 ? launch_persist<EPI, 8192>(A, W, M_pad, N_pad, K, ep, st)
+                            : launch_persist<EPI>(A, W, M_pad, N_pad, K, ep, st);
     }
     if ((nt_mask >> EPI) & 1u) {
+        if constexpr (EPI != EPI_LSE) {
+            if (ms == 16 && cfg == 0) return launch_t<256, 256, 2, 4, 2, 64, EPI, 192 | 8192>(A, W, M_pad, N_pad, K, ep, st);
+            if (ms == 16 && cfg == 1) return launch_t<256, 128, 4, 2, 3, 64, EPI, 192 | 8192>(A, W, M_pad, N_pad, K, ep, st);
+        }
         if (cfg == 0) return launch_t<256, 256, 2, 4, 2, 64, EPI, 192>(A, W, M_pad, N_pad, K, ep, st);
         if (cfg == 1) return launch_t<256, 128, 4, 2, 3, 64, EPI, 192>(A, W, M_pad, N_pad, K, ep, st);
     }
@@ -913,6 +1005,10 @@ hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
     }();
     if (EPI == EPI_RESLN_F32 && res_direct && cfg == 0)
         return launch_t<256, 256, 2, 4, 2, 64, EPI, 160>(A, W, M_pad, N_pad, K, ep, st);
+    if constexpr (EPI != EPI_LSE) {
+        if (ms == 16 && cfg == 0) return launch_t<256, 256, 2, 4, 2, 64, EPI, 128 | 8192>(A, W, M_pad, N_pad, K, ep, st);
+        if (ms == 16 && cfg == 1) return launch_t<256, 128, 4, 2, 3, 64, EPI, 128 | 8192>(A, W, M_pad, N_pad, K, ep, st);
+    }
     switch (cfg) {
         case 0: return launch_t<256, 256, 2, 4, 2, 64, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
         case 1: return launch_t<256, 128, 4, 2, 3, 64, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
@@ -966,10 +1062,20 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 8: e = launch_t<256, 256, 2, 2, 2, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
         default: e = launch_t<128, 128, 2, 2, 2, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;   \
     }
+#define RS_DBG16(D)                                                                                   \
+    switch (cfg) {                                                                                    \
+        case 0: e = launch_t<256, 256, 2, 4, 2, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
+        case 1: e = launch_t<256, 128, 4, 2, 3, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
+        default: return -1;                                                                           \
+    }
     if (M % 256 || N % 256 || K % 64) return -1;
-    if (cfg == 9 || cfg == 11) {   // persistent fp16-output kernel (11: GELU epilogue)
+    if (cfg >= 9 && cfg <= 12) {   // persistent fp16-output kernel (11/12: GELU; 10/12: 16x16x32)
         e = cfg == 9 ? launch_persist<EPI_BIAS_F16>(a, w, M, N, K, ep, st)
-                     : launch_persist<EPI_GELU_F16>(a, w, M, N, K, ep, st);
+          : cfg == 10 ? (dbg ? launch_persist<EPI_BIAS_F16, 8192 | 16384>(a, w, M, N, K, ep, st)
+                             : launch_persist<EPI_BIAS_F16, 8192>(a, w, M, N, K, ep, st))
+          : cfg == 11 ? launch_persist<EPI_GELU_F16>(a, w, M, N, K, ep, st)
+                      : (dbg ? launch_persist<EPI_GELU_F16, 8192 | 16384>(a, w, M, N, K, ep, st)
+                             : launch_persist<EPI_GELU_F16, 8192>(a, w, M, N, K, ep, st));
         return e == hipSuccess ? 0 : -2;
     }
     switch (dbg) {
@@ -1003,8 +1109,14 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 259: RS_DBG(259); break;
         case 1: RS_DBG(1); break;
         case 2: RS_DBG(2); break;
+        // 16x16x32 MFMA (BK = 64 configurations only): pipelined / + nt stores / neither
+        case 8320: RS_DBG16(8320); break;
+        case 8384: RS_DBG16(8384); break;
+        case 8323: RS_DBG16(8323); break;
+        case 8322: RS_DBG16(8322); break;
         default: RS_DBG(3); break;
     }
 #undef RS_DBG
+#undef RS_DBG16
     return e == hipSuccess ? 0 : -2;
 }
