@@ -113,6 +113,10 @@ hipError_t launch_embed_ln(const int* tok, SeqMeta sm, int s0, int s1, int row0,
                            float2* stats, f16* h16, int kx, hipStream_t st);
 hipError_t launch_ln_rows(const float* x, int rows, const float* g, const float* b, float eps,
                           int H, float* y32, float2* stats, f16* y16, int kx, hipStream_t st);
+// x32 <- LN(x32; stats, pg, pb) + o16, then stats / fp16 image of LN(x32; g, b) (kx == 1)
+hipError_t launch_ln_res_rows(float* x32, float2* stats, const float* pg, const float* pb, const f16* o16,
+                             int rows, const float* g, const float* b, float eps, int H, f16* y16,
+                             hipStream_t st);
 // Unique layer-0 rows (dedup): for every hypothesis of the chunk its T rows, and every
 // sequence's [MASK] row, as the fp16 operand image of LN(embedding) (rows of SeqMeta.urow_*)
 hipError_t launch_embed_unique(const int* tok, SeqMeta sm, int s0, int s1, int mask_id, int vocab,

@@ -139,6 +139,37 @@ ln_rows_kernel(const float* __restrict__ xin, int rows, const float* __restrict_
                  y16 + (size_t)row * kx * H, kx);
 }
 
+// BertSelfOutput (modeling_bert.py:282-293) with the O projection done by the persistent
+// fp16-output GEMM (o16 = ctx . Wo^T + bo): the residual add and the LayerNorm happen here,
+// so the GEMM neither reads nor writes the fp32 stream.  x32 <- LN_prev(x32) + o16 (LN_prev
+// rebuilt from the row statistics in `stats` and (pg, pb)), then its statistics and the fp16
+// operand image of LN(x32) with (g, b).  fp16 precision mode (kx == 1) only.
+template <int NV>
+__global__ void __launch_bounds__(256)
+ln_res_rows_kernel(float* __restrict__ x32, float2* __restrict__ stats, const float* __restrict__ pg,
+                   const float* __restrict__ pb, const f16* __restrict__ o16, int rows,
+                   const float* __restrict__ g, const float* __restrict__ b, float eps,
+                   f16* __restrict__ y16) {
+    constexpr int H = NV * 256;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    const float2 st0 = stats[row];
+    float4 x[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int c = v * 256 + lane * 4;
+        const float4 r = *(const float4*)(x32 + (size_t)row * H + c);
+        const float4 gg = *(const float4*)(pg + c);
+        const float4 bb = *(const float4*)(pb + c);
+        const half4 o = *(const half4*)(o16 + (size_t)row * H + c);
+        x[v] = make_float4(ln_apply(r.x, st0, gg.x, bb.x) + (float)o[0], ln_apply(r.y, st0, gg.y, bb.y) + (float)o[1],
+                           ln_apply(r.z, st0, gg.z, bb.z) + (float)o[2], ln_apply(r.w, st0, gg.w, bb.w) + (float)o[3]);
+        *(float4*)(x32 + (size_t)row * H + c) = x[v];
+    }
+    ln_store<NV>(x, g, b, eps, lane, nullptr, stats + row, y16 + (size_t)row * H, 1);
+}
+
 __device__ __forceinline__ void load8(const f16* p, float (&o)[8]) {
     const half8 v = *(const half8*)p;
 #pragma unroll
@@ -374,11 +405,14 @@ attn_mfma_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int 
 template <bool DEDUP>
 __global__ void __launch_bounds__(64, 3)
 attn_tr_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
-               f16* __restrict__ ctx, int kx) {
+               f16* __restrict__ ctx, int kx, int heads_fast) {
     typedef __fp16 fp16x4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
     constexpr int VR = 96;
     __shared__ __attribute__((aligned(16))) f16 sV[64 * VR];
-    const int s = s0 + blockIdx.x, hd = blockIdx.y;
+    // heads_fast = number of heads: 1-D grid, the heads of one sequence are consecutive
+    // workgroups (their 128-B slices of the same rows are fetched together); 0: grid (seq, head)
+    const int s = s0 + (heads_fast ? (int)blockIdx.x / heads_fast : (int)blockIdx.x);
+    const int hd = heads_fast ? (int)blockIdx.x % heads_fast : (int)blockIdx.y;
     const int T = sm.len[s], rs = sm.row[s] - row0;
     const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5;
     const int ld = 3 * H;
@@ -710,13 +744,34 @@ hipError_t launch_ln_rows(const float* x, int rows, const float* g, const float*
     return hipGetLastError();
 }
 
+hipError_t launch_ln_res_rows(float* x32, float2* stats, const float* pg, const float* pb, const f16* o16,
+                             int rows, const float* g, const float* b, float eps, int H, f16* y16,
+                             hipStream_t st) {
+    if (rows <= 0) return hipSuccess;
+    const dim3 grid((rows + 3) / 4), block(256);
+    if (H == 768) hipLaunchKernelGGL(ln_res_rows_kernel<3>, grid, block, 0, st, x32, stats, pg, pb, o16, rows, g, b, eps, y16);
+    else if (H == 256) hipLaunchKernelGGL(ln_res_rows_kernel<1>, grid, block, 0, st, x32, stats, pg, pb, o16, rows, g, b, eps, y16);
+    else if (H == 512) hipLaunchKernelGGL(ln_res_rows_kernel<2>, grid, block, 0, st, x32, stats, pg, pb, o16, rows, g, b, eps, y16);
+    else if (H == 1024) hipLaunchKernelGGL(ln_res_rows_kernel<4>, grid, block, 0, st, x32, stats, pg, pb, o16, rows, g, b, eps, y16);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
 hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0, int s1, int row0,
                                  int H, int heads, f16* ctx, int kx, hipStream_t st, bool dedup) {
     if (s1 <= s0) return hipSuccess;
     const dim3 grid(s1 - s0, heads);
+    // RS_ATTN_ORDER: "seq" (default: grid (sequence, head)) or "head" (1-D grid, heads of a
+    // sequence adjacent: 7 % slower, tools/attn_bench.py kind 5)
+    static const int head_order = [] {
+        const char* v = getenv("RS_ATTN_ORDER");
+        return v && !strcmp(v, "head") ? 1 : 0;
+    }();
+    const dim3 grid_tr = head_order ? dim3((s1 - s0) * heads) : grid;
+    const int hf = head_order ? heads : 0;
     if (dedup) {                                  // fp16 QKV, kx == 1 only (host gates it)
         if (qkv32 || kx != 1 || H % 64) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(attn_tr_kernel<true>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
+        hipLaunchKernelGGL(attn_tr_kernel<true>, grid_tr, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx, hf);
         return hipGetLastError();
     }
     // RS_ATTN: "tr" (default, transposed-read MFMA), "mfma" (LDS-transposed V), "valu"
@@ -733,7 +788,7 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
     else if (kind == 1)
         hipLaunchKernelGGL(attn_mfma_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
     else
-        hipLaunchKernelGGL(attn_tr_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
+        hipLaunchKernelGGL(attn_tr_kernel<false>, grid_tr, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx, hf);
     return hipGetLastError();
 }
 
@@ -808,8 +863,10 @@ extern "C" int rs_debug_attention(int kind, const void* qkv, const int* len, con
     sm.row = row;
     const dim3 grid(n_seq, heads);
     hipStream_t st = (hipStream_t)stream;
-    if (kind == 0)
-        hipLaunchKernelGGL(attn_tr_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
+    if (kind == 0)      // (sequence, head) grid
+        hipLaunchKernelGGL(attn_tr_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1, 0);
+    else if (kind == 5) // head-fastest 1-D grid (production order)
+        hipLaunchKernelGGL(attn_tr_kernel<false>, dim3(n_seq * heads), dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1, heads);
     else if (kind == 1)
         hipLaunchKernelGGL(attn_mfma_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
     else if (kind == 2)

@@ -979,15 +979,16 @@ hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
     // FLOP, but the chip holds a higher clock under the 16x16 loop on random data
     // (MI355X_MICROARCH.md 'DVFS give-back' item 7): +5-8 % on the pipelined kernel
     // (tools/gemm_bench.py, profiles/r1_gemm_ms16.txt) and -5..-7 % O-proj / FFN2 time end to
-    // end.  The persistent kernel keeps 32x32x16 (RS_GEMM_MS_PERSIST=16 to switch): with 16x16
-    // its QKV launches took +7 % end to end.  The decoder's logsumexp epilogue keeps 32x32x16.
+    // end.  The persistent kernel keeps 32x32x16 (RS_GEMM_MS_PERSIST=16 to switch, 0: 16x16
+    // for K >= 2048 only): with 16x16 its QKV launches took +7 % end to end.  The decoder's
+    // logsumexp epilogue keeps 32x32x16.
     static const int ms = getenv("RS_GEMM_MS") ? atoi(getenv("RS_GEMM_MS")) : 16;
     static const int ms_p = getenv("RS_GEMM_MS_PERSIST") ? atoi(getenv("RS_GEMM_MS_PERSIST")) : 32;
     // RS_GEMM_PERSIST=0 disables the persistent kernel (fp16-output epilogues, kx = 1)
     static const int persist = getenv("RS_GEMM_PERSIST") ? atoi(getenv("RS_GEMM_PERSIST")) : 1;
     if constexpr (EPI == EPI_BIAS_F16 || EPI == EPI_GELU_F16) {
         if (persist && cfg == 0 && (EPI == EPI_BIAS_F16 || ep.kx == 1))
-            return ms_p == 16 ? launch_persist<EPI, 8192>(A, W, M_pad, N_pad, K, ep, st)
+            return (ms_p == 16 || (ms_p == 0 && K >= 2048)) ? launch_persist<EPI, 8192>(A, W, M_pad, N_pad, K, ep, st)
                             : launch_persist<EPI>(A, W, M_pad, N_pad, K, ep, st);
     }
     if ((nt_mask >> EPI) & 1u) {

@@ -236,6 +236,24 @@ int gemm(rs_model* m, hipStream_t st, int kind, int epi, const f16* A, const f16
 
 enum Mode { MODE_MLM = 0, MODE_CLS = 1, MODE_EMB = 2 };
 
+// RS_OPROJ: "f16" (default in the fp16 precision mode: fp16-output O projection + fused
+// residual/LayerNorm rows kernel) or "resln" (residual rebuilt in the GEMM's accumulators)
+bool oproj_f16() {
+    static const bool v = [] {
+        const char* e = getenv("RS_OPROJ");
+        return !(e && !strcmp(e, "resln"));
+    }();
+    return v;
+}
+// RS_FFN2: "resln" (default) or "f16" (the O-projection split applied to BertOutput)
+bool ffn2_f16() {
+    static const bool v = [] {
+        const char* e = getenv("RS_FFN2");
+        return e && !strcmp(e, "f16");
+    }();
+    return v;
+}
+
 // Runs the encoder + head over sequences [c.s0, c.s1) (one chunk).
 int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, const Chunk& c,
               int mode, float* d_out_rows /* indexed by sequence */) {
@@ -290,14 +308,33 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
                 ProfScope ps(m, st, RS_K_ATTN, 0);
                 HIPTRY(launch_attention_full(qkv, q32, sm, c.s0, c.s1, 0, H, nh, ctx, kx, st, uq));
             }
-            ep = resln_ep(L.bo, pg, pb);
-            if (int r = gemm(m, st, RS_K_OPROJ, EPI_RESLN_F32, ctx, L.wo, rows, H, kx * H, ep, H)) return r;
-            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(t32, rows, L.g1, L.be1, cf.ln_eps, H, nullptr, xst, h16, kx, st)); }
+            if (kx == 1 && oproj_f16()) {
+                // O projection as a persistent fp16-output GEMM into the (free) FFN1 buffer; the
+                // residual add + LayerNorm move into ln_res_rows, off the GEMM's critical path
+                ep = EpiArgs{}; ep.bias = L.bo; ep.out = inter; ep.ldc = H;
+                if (int r = gemm(m, st, RS_K_OPROJ, EPI_BIAS_F16, ctx, L.wo, rows, H, H, ep, H)) return r;
+                ProfScope ps(m, st, RS_K_OTHER, 0);
+                HIPTRY(launch_ln_res_rows(t32, xst, pg, pb, inter, rows, L.g1, L.be1, cf.ln_eps, H, h16, st));
+            } else {
+                ep = resln_ep(L.bo, pg, pb);
+                if (int r = gemm(m, st, RS_K_OPROJ, EPI_RESLN_F32, ctx, L.wo, rows, H, kx * H, ep, H)) return r;
+                ProfScope ps(m, st, RS_K_OTHER, 0);
+                HIPTRY(launch_ln_rows(t32, rows, L.g1, L.be1, cf.ln_eps, H, nullptr, xst, h16, kx, st));
+            }
             ep = gelu_ep(L.b1, inter);
             if (int r = gemm(m, st, RS_K_FFN1, EPI_GELU_F16, h16, L.w1, rows, F, kx * H, ep, F)) return r;
-            ep = resln_ep(L.b2, L.g1, L.be1);
-            if (int r = gemm(m, st, RS_K_FFN2, EPI_RESLN_F32, inter, L.w2, rows, H, kx * F, ep, H)) return r;
-            { ProfScope ps(m, st, RS_K_OTHER, 0); HIPTRY(launch_ln_rows(t32, rows, L.g2, L.be2, cf.ln_eps, H, nullptr, xst, h16, kx, st)); }
+            if (kx == 1 && ffn2_f16()) {
+                // same split for BertOutput: fp16-output GEMM into the (free) ctx buffer
+                ep = EpiArgs{}; ep.bias = L.b2; ep.out = ctx; ep.ldc = H;
+                if (int r = gemm(m, st, RS_K_FFN2, EPI_BIAS_F16, inter, L.w2, rows, H, F, ep, H)) return r;
+                ProfScope ps(m, st, RS_K_OTHER, 0);
+                HIPTRY(launch_ln_res_rows(t32, xst, L.g1, L.be1, ctx, rows, L.g2, L.be2, cf.ln_eps, H, h16, st));
+            } else {
+                ep = resln_ep(L.b2, L.g1, L.be1);
+                if (int r = gemm(m, st, RS_K_FFN2, EPI_RESLN_F32, inter, L.w2, rows, H, kx * F, ep, H)) return r;
+                ProfScope ps(m, st, RS_K_OTHER, 0);
+                HIPTRY(launch_ln_rows(t32, rows, L.g2, L.be2, cf.ln_eps, H, nullptr, xst, h16, kx, st));
+            }
         } else {
             // last layer: only the scored row of every sequence (one row per sequence)
             f16* ctxq = m->ctxq.as<f16>();

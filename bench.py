@@ -151,6 +151,22 @@ def main():
                 "launches": n, "avg_launch_ms": round(ms / max(n, 1), 4),
                 "flops_per_launch": fl / max(n, 1)}
 
+    # ---- reranked 1-best CER (second half of BASELINE.json's metric), rank-0 shard -------
+    # HIP fusion over the 101-weight grid + corpus CER on this step's LM scores, checked
+    # against the oracle's numpy restatement of rescore.py:25-58 on the same scores.
+    rr = None
+    if rank == 0:
+        from oracle import rescore_ref as RR
+        lm_np = lm.double().cpu().numpy()
+        bw, bcer, arg, cers = rerank.find_best_weight(nb, lm_np, n_best=args.nbest, device=local)
+        U, Nb = nb.n_utt, args.nbest
+        hyps = [[nb.hyp_words(nb.utt_off[u] + i) for i in range(Nb)] for u in range(U)]
+        obw, obcer, oarg = RR.find_best_weight(nb.am.reshape(U, Nb), lm_np.reshape(U, Nb), hyps,
+                                               nb.refs, n_best=Nb)
+        rr = {"best_weight": round(bw, 2), "cer": bcer, "am_only_cer": float(cers[0]),
+              "utterances": U, "cer_equal_oracle": bool(bcer == obcer and bw == obw),
+              "argmax_equal_oracle": bool(np.array_equal(np.asarray(arg), oarg))}
+
     # ---- CPU baseline: oracle restatement of the reference work pattern ------------------
     cpu = None
     if rank == 0 and args.cpu_seconds > 0:
@@ -184,7 +200,7 @@ def main():
                           "utts_per_rank": args.utts, "n_best": args.nbest, "forwards_per_rank_step": n_fwd,
                           "mean_T": round(mean_T, 2), "parallelism": f"dp{world} (utterance shards + RCCL all_gather)"},
                "achieved_tflops_canonical": round(flops_step * world * args.steps / dt / 1e12, 2),
-               "roofline": roof, "cpu_baseline": cpu,
+               "roofline": roof, "cpu_baseline": cpu, "rerank": rr,
                "kinds_ms": {k: round(v[0], 3) for k, v in kinds.items()}}
         print(json.dumps(rec))
     scorer.close()
