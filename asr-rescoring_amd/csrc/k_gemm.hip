@@ -963,7 +963,7 @@ int pick_cfg(int N_pad) {
 
 template <int EPI>
 hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep,
-                      hipStream_t st) {
+                      hipStream_t st, int tag) {
     // Production variant: software-pipelined K loop (VAR 128) + non-temporal stores (VAR 64)
     // for the epilogues selected by RS_GEMM_NT: "f16" (default: fp16 outputs stream past L2,
     // keeping the A panels resident), "all", "none".
@@ -989,7 +989,8 @@ hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
     if constexpr (EPI == EPI_BIAS_F16 || EPI == EPI_GELU_F16) {
         if (persist && cfg == 0 && (EPI == EPI_BIAS_F16 || ep.kx == 1))
             return (ms_p == 16 || (ms_p == 0 && K >= 2048)) ? launch_persist<EPI, 8192>(A, W, M_pad, N_pad, K, ep, st)
-                            : launch_persist<EPI>(A, W, M_pad, N_pad, K, ep, st);
+                 : tag ? launch_persist<EPI, 65536>(A, W, M_pad, N_pad, K, ep, st)   // VAR 65536: name tag only
+                       : launch_persist<EPI>(A, W, M_pad, N_pad, K, ep, st);
     }
     if ((nt_mask >> EPI) & 1u) {
         if constexpr (EPI != EPI_LSE) {
@@ -1027,16 +1028,16 @@ hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
 int gemm_row_align() { return 256; }
 
 hipError_t launch_gemm(int epi, const f16* A, const f16* W, int M_pad, int N_pad, int K,
-                       const EpiArgs& ep, hipStream_t st) {
+                       const EpiArgs& ep, hipStream_t st, int tag) {
     if (M_pad % 256 || N_pad % 128 || K % 64 || M_pad <= 0) return hipErrorInvalidValue;
     switch (epi) {
-        case EPI_BIAS_F16: return launch_epi<EPI_BIAS_F16>(A, W, M_pad, N_pad, K, ep, st);
-        case EPI_GELU_F16: return launch_epi<EPI_GELU_F16>(A, W, M_pad, N_pad, K, ep, st);
-        case EPI_GELU_F32: return launch_epi<EPI_GELU_F32>(A, W, M_pad, N_pad, K, ep, st);
-        case EPI_RES_F32: return launch_epi<EPI_RES_F32>(A, W, M_pad, N_pad, K, ep, st);
-        case EPI_LSE: return launch_epi<EPI_LSE>(A, W, M_pad, N_pad, K, ep, st);
-        case EPI_BIAS_F32: return launch_epi<EPI_BIAS_F32>(A, W, M_pad, N_pad, K, ep, st);
-        case EPI_RESLN_F32: return launch_epi<EPI_RESLN_F32>(A, W, M_pad, N_pad, K, ep, st);
+        case EPI_BIAS_F16: return launch_epi<EPI_BIAS_F16>(A, W, M_pad, N_pad, K, ep, st, tag);
+        case EPI_GELU_F16: return launch_epi<EPI_GELU_F16>(A, W, M_pad, N_pad, K, ep, st, tag);
+        case EPI_GELU_F32: return launch_epi<EPI_GELU_F32>(A, W, M_pad, N_pad, K, ep, st, tag);
+        case EPI_RES_F32: return launch_epi<EPI_RES_F32>(A, W, M_pad, N_pad, K, ep, st, tag);
+        case EPI_LSE: return launch_epi<EPI_LSE>(A, W, M_pad, N_pad, K, ep, st, tag);
+        case EPI_BIAS_F32: return launch_epi<EPI_BIAS_F32>(A, W, M_pad, N_pad, K, ep, st, tag);
+        case EPI_RESLN_F32: return launch_epi<EPI_RESLN_F32>(A, W, M_pad, N_pad, K, ep, st, tag);
     }
     return hipErrorInvalidValue;
 }

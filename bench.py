@@ -131,8 +131,8 @@ def main():
         # HBM(+MALL) bytes per launch from the committed rocprofv3 PMC summary (FETCH_SIZE x2
         # gfx950 correction + WRITE_SIZE, per row), scaled to this run's rows per launch
         traffic, tsrc = None, None
-        nk = {"qkv": (2304, 768, "qkv"), "oproj": (768, 768, "oproj/ffn2"), "ffn1": (3072, 768, "ffn1"),
-              "ffn2": (768, 3072, "oproj/ffn2")}.get(dom)
+        nk = {"qkv": (2304, 768, "qkv"), "oproj": (768, 768, "oproj"), "ffn1": (3072, 768, "ffn1"),
+              "ffn2": (768, 3072, "ffn2")}.get(dom)
         pmc_files = sorted(f for f in os.listdir(os.path.join(REPO, "profiles")) if f.endswith("_pmc_gemm_traffic.json"))
         if nk and pmc_files:
             pm = json.load(open(os.path.join(REPO, "profiles", pmc_files[-1])))

@@ -14,17 +14,19 @@ import os
 import re
 import sys
 
-EPI = {0: "qkv", 1: "ffn1", 2: "head_transform", 3: "oproj/ffn2(res)", 4: "decoder", 5: "qkv32", 6: "oproj/ffn2"}
+EPI = {0: "qkv", 1: "ffn1", 2: "head_transform", 3: "res_f32(last layer)", 4: "decoder", 5: "qkv32", 6: "ffn2"}
 
 
 def kname(n):
-    m = re.search(r"gemm_persist_kernelILi(\d+)E", n)
+    m = re.search(r"gemm_persist_kernelILi(\d+)ELi(\d+)E", n)
+    if m and int(m.group(2)) & 65536:
+        return "gemm_persist:oproj"
     if m:
         return "gemm_persist:" + EPI.get(int(m.group(1)), m.group(1))
     m = re.search(r"gemm_f16_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi\d+ELi\d+ELi(\d+)E", n)
     if m:
         return "gemm:" + EPI.get(int(m.group(1)), m.group(1))
-    m = re.search(r"(attn_\w+?|ln_rows|embed_ln)_kernel", n)
+    m = re.search(r"(attn_\w+?|ln_res_rows|ln_rows|embed_ln)_kernel", n)
     return m.group(1) if m else n[:40]
 
 

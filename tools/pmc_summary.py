@@ -18,10 +18,11 @@ import os
 import re
 import sys
 
-EPI_N = {0: ("qkv", 2304), 1: ("ffn1", 3072), 3: ("oproj/ffn2", 768), 6: ("oproj/ffn2", 768),
+EPI_N = {0: ("qkv", 2304), 1: ("ffn1", 3072), 3: ("res_f32", 768), 6: ("ffn2", 768),
          2: ("head_transform", 768), 4: ("decoder", 21248)}
+OPROJ_TAG = 65536          # VAR bit of the O-projection instance of the persistent kernel
 RE_GEMM = re.compile(r"gemm_f16_kernelILi(\d+)ELi(\d+)ELi\d+ELi\d+ELi\d+ELi\d+ELi(\d+)E")
-RE_PERSIST = re.compile(r"gemm_persist_kernelILi(\d+)E")
+RE_PERSIST = re.compile(r"gemm_persist_kernelILi(\d+)ELi(\d+)E")
 
 
 def load(d):
@@ -45,14 +46,15 @@ def main():
                 blocks = int(r["Grid_Size"]) // int(r["Workgroup_Size"])
                 rows = blocks // (n // bn) * bm if n else None
             elif mp:
-                name, n = EPI_N.get(int(mp.group(1)), (f"epi{mp.group(1)}", None))
+                name, n = ("oproj", 768) if int(mp.group(2)) & OPROJ_TAG else \
+                    EPI_N.get(int(mp.group(1)), (f"epi{mp.group(1)}", None))
                 rows = None                      # filled from the WRITE pass below
             else:
                 continue
             res["persist:" + name if mp else name][cname].append((byt, rows))
     for name, d in res.items():
         if name.startswith("persist:") and "WRITE_SIZE" in d:
-            n = dict(EPI_N.values())[name.split(":", 1)[1]]
+            n = dict(list(EPI_N.values()) + [("oproj", 768)])[name.split(":", 1)[1]]
             rows = [b / (2 * n) for b, _ in d["WRITE_SIZE"]]
             for cname in d:
                 d[cname] = [(b, rows[i] if i < len(rows) else None) for i, (b, _) in enumerate(d[cname])]
