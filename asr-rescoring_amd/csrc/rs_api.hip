@@ -238,20 +238,15 @@ enum Mode { MODE_MLM = 0, MODE_CLS = 1, MODE_EMB = 2 };
 
 // RS_OPROJ: "f16" (default in the fp16 precision mode: fp16-output O projection + fused
 // residual/LayerNorm rows kernel) or "resln" (residual rebuilt in the GEMM's accumulators)
+// (read per call, like RS_DEDUP, so a test can flip it in-process)
 bool oproj_f16() {
-    static const bool v = [] {
-        const char* e = getenv("RS_OPROJ");
-        return !(e && !strcmp(e, "resln"));
-    }();
-    return v;
+    const char* e = getenv("RS_OPROJ");
+    return !(e && !strcmp(e, "resln"));
 }
 // RS_FFN2: "resln" (default) or "f16" (the O-projection split applied to BertOutput)
 bool ffn2_f16() {
-    static const bool v = [] {
-        const char* e = getenv("RS_FFN2");
-        return e && !strcmp(e, "f16");
-    }();
-    return v;
+    const char* e = getenv("RS_FFN2");
+    return e && !strcmp(e, "f16");
 }
 
 // Runs the encoder + head over sequences [c.s0, c.s1) (one chunk).

@@ -209,3 +209,20 @@ def test_layer0_dedup_is_exact(w_tiny, w_base, max_rows, monkeypatch):
         finally:
             s.close()
         assert np.array_equal(a, b), np.abs(a - b).max()
+
+
+@pytest.mark.parametrize("env", [{"RS_OPROJ": "resln"}, {"RS_FFN2": "f16"}])
+def test_residual_paths_golden(pll_base, golden_dir, env, monkeypatch):
+    """The residual-block variants against the F1 fixture: O projection with the residual +
+    LayerNorm rebuilt in the GEMM accumulators (RS_OPROJ=resln; default: fp16-output GEMM +
+    ln_res_rows), and FFN2 split the same way as the O projection (RS_FFN2=f16)."""
+    g = _load(golden_dir, "pll_base.npz")
+    base = pll_base.score_nbest(g["tokens"], g["hyp_off"]).cpu().numpy()
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    pll, rows = pll_base.score_nbest(g["tokens"], g["hyp_off"], return_rows=True)
+    pll = pll.cpu().numpy()
+    assert rel_err(pll, g["pll"]).max() < REL
+    e = rel_err(rows.cpu().numpy(), g["row_lp"])
+    assert e.max() < ROW_REL_FP16 and np.percentile(e, 99) < REL
+    assert not np.array_equal(pll, base)          # the variant really ran a different path
