@@ -138,7 +138,10 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
 hipError_t launch_attention_query(const void* qkv, bool qkv32, const float* x32, const float2* stats,
                                   const float* g, const float* b, SeqMeta sm, int s0, int s1,
                                   int row0, int H, int heads, f16* ctxq, float* resq, int kx,
-                                  hipStream_t st);
+                                  hipStream_t st, const void* qd = nullptr);
+// dst[s - s0] = src[row of sequence s's query position], ld halfs per row
+hipError_t launch_gather_query_rows(const f16* src, int ld, SeqMeta sm, int s0, int s1, int row0, f16* dst,
+                                   hipStream_t st);
 hipError_t launch_gather_labels(const int* tok, SeqMeta sm, int s0, int s1, int* lab,
                                 hipStream_t st);
 hipError_t launch_lse_finalize(const float2* part, int n_parts, const float* label_logit,

@@ -539,7 +539,7 @@ attn_tr_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
 // for QK^T, lanes over the 64 head dims for P.V.
 template <class QT>
 __global__ void __launch_bounds__(64)
-attn_query_kernel(const QT* __restrict__ qkv, const float* __restrict__ x32,
+attn_query_kernel(const QT* __restrict__ qkv, const QT* __restrict__ qd, const float* __restrict__ x32,
                   const float2* __restrict__ stats, const float* __restrict__ lg,
                   const float* __restrict__ lb, SeqMeta sm, int s0, int row0, int H,
                   f16* __restrict__ ctxq, float* __restrict__ resq, int kx) {
@@ -550,7 +550,8 @@ attn_query_kernel(const QT* __restrict__ qkv, const float* __restrict__ x32,
     const int lane = threadIdx.x;
     const int ld = 3 * H;
     const QT* base = qkv + (size_t)rs * ld + h * 64;
-    sq[lane] = (float)base[(size_t)qi * ld + lane] * 0.125f;
+    // qd: dense [sequence, H] query rows (the last layer projects Q for the scored rows only)
+    sq[lane] = (float)(qd ? qd[(size_t)(s - s0) * H + h * 64 + lane] : base[(size_t)qi * ld + lane]) * 0.125f;
     __syncthreads();
     float m = -INFINITY, l = 0.f, acc = 0.f;
     for (int k0 = 0; k0 < T; k0 += 64) {
@@ -588,6 +589,17 @@ attn_query_kernel(const QT* __restrict__ qkv, const float* __restrict__ x32,
         const size_t r = (size_t)(rs + qi);
         resq[(size_t)s_loc * H + c] = ln_apply(x32[r * H + c], stats[r], lg[c], lb[c]);
     }
+}
+
+// Row gather: dst[s - s0] = src[row of sequence s's scored position] (ld halfs per row).
+__global__ void __launch_bounds__(64)
+gather_query_rows_kernel(const f16* __restrict__ src, int ld, SeqMeta sm, int s0, int row0,
+                         f16* __restrict__ dst) {
+    const int s = s0 + blockIdx.x;
+    const size_t r = (size_t)(sm.row[s] - row0 + sm.query[s]);
+    const uint4* a = (const uint4*)(src + r * ld);
+    uint4* o = (uint4*)(dst + (size_t)blockIdx.x * ld);
+    for (int i = threadIdx.x; i < ld / 8; i += 64) o[i] = a[i];
 }
 
 __global__ void gather_labels_kernel(const int* __restrict__ tok, SeqMeta sm, int s0, int n,
@@ -795,13 +807,21 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
 hipError_t launch_attention_query(const void* qkv, bool qkv32, const float* x32, const float2* stats,
                                   const float* g, const float* b, SeqMeta sm, int s0, int s1,
                                   int row0, int H, int heads, f16* ctxq, float* resq, int kx,
-                                  hipStream_t st) {
+                                  hipStream_t st, const void* qd) {
     if (s1 <= s0) return hipSuccess;
     const dim3 grid(s1 - s0, heads);
     if (qkv32)
-        hipLaunchKernelGGL(attn_query_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, x32, stats, g, b, sm, s0, row0, H, ctxq, resq, kx);
+        hipLaunchKernelGGL(attn_query_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, (const float*)qd, x32, stats, g, b, sm, s0, row0, H, ctxq, resq, kx);
     else
-        hipLaunchKernelGGL(attn_query_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, x32, stats, g, b, sm, s0, row0, H, ctxq, resq, kx);
+        hipLaunchKernelGGL(attn_query_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, (const f16*)qd, x32, stats, g, b, sm, s0, row0, H, ctxq, resq, kx);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_query_rows(const f16* src, int ld, SeqMeta sm, int s0, int s1, int row0, f16* dst,
+                                   hipStream_t st) {
+    if (s1 <= s0) return hipSuccess;
+    if (ld % 8) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(gather_query_rows_kernel, dim3(s1 - s0), dim3(64), 0, st, src, ld, sm, s0, row0, dst);
     return hipGetLastError();
 }
 

@@ -296,8 +296,28 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
         ep = EpiArgs{};
         ep.bias = L.bqkv; ep.out = qkv; ep.ldc = 3 * H;
         const bool uq = dedup && li == 0;
-        if (int r = gemm(m, st, RS_K_QKV, qkv_epi, h16, L.wqkv, uq ? c.urows : rows, 3 * H, kx * H, ep,
-                         last ? 2 * H : 3 * H)) return r;
+        const void* qdense = nullptr;
+        const char* lq_env = getenv("RS_LASTQ");      // "0": full Q/K/V GEMM at the last layer
+        if (last && !uq && !(lq_env && !strcmp(lq_env, "0"))) {
+            // Query-row-only layer: K and V for every row (rows H..3H of the fused weight,
+            // written into columns H..3H of qkv), Q only for the scored row of each sequence
+            // (gathered operand rows -> dense [sequence, H] in the idle tq32 buffer)
+            const size_t esz = q32 ? 4 : 2;
+            ep.bias = L.bqkv + H;
+            ep.out = (char*)qkv + H * esz;
+            if (int r = gemm(m, st, RS_K_QKV, qkv_epi, h16, L.wqkv + (size_t)H * kx * H, rows, 2 * H, kx * H, ep,
+                             2 * H)) return r;
+            f16* hq16g = m->hq16.as<f16>();
+            {
+                ProfScope ps(m, st, RS_K_OTHER, 0);
+                HIPTRY(launch_gather_query_rows(h16, kx * H, sm, c.s0, c.s1, 0, hq16g, st));
+            }
+            EpiArgs eq{};
+            eq.bias = L.bqkv; eq.out = m->tq32.p; eq.ldc = H;
+            if (int r = gemm(m, st, RS_K_QKV, qkv_epi, hq16g, L.wqkv, ns, H, kx * H, eq, H)) return r;
+            qdense = m->tq32.p;
+        } else if (int r = gemm(m, st, RS_K_QKV, qkv_epi, h16, L.wqkv, uq ? c.urows : rows, 3 * H, kx * H, ep,
+                                last ? 2 * H : 3 * H)) return r;
         if (!last) {
             {
                 ProfScope ps(m, st, RS_K_ATTN, 0);
@@ -340,7 +360,8 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
             f16* interq = m->interq.as<f16>();
             {
                 ProfScope ps(m, st, RS_K_ATTN, 0);
-                HIPTRY(launch_attention_query(qkv, q32, t32, xst, pg, pb, sm, c.s0, c.s1, 0, H, nh, ctxq, resq, kx, st));
+                HIPTRY(launch_attention_query(qkv, q32, t32, xst, pg, pb, sm, c.s0, c.s1, 0, H, nh, ctxq, resq, kx, st,
+                                              qdense));
             }
             ep = EpiArgs{}; ep.bias = L.bo; ep.res = resq; ep.out = tq; ep.ldc = H;
             if (int r = gemm(m, st, RS_K_OPROJ, EPI_RES_F32, ctxq, L.wo, ns, H, kx * H, ep, H)) return r;
