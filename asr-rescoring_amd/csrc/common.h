@@ -131,9 +131,12 @@ hipError_t launch_bertscore_recall(const f16* emb, int H, const int* hyp_off, co
 // Last hidden state, L2-normalised per token, fp16 at out[(tok_off + t) * H] (BERTScore)
 hipError_t launch_embed_out(const float* x32, const float2* stats, const float* g, const float* b,
                             SeqMeta sm, int s0, int s1, int row0, int H, f16* out, hipStream_t st);
+// max_len: longest sequence of the launch (0 = unknown): the 16x16x32 kernel serves chunks whose
+// sequences all fit one 64-key block, the 32x32x16 kernel the others (fewer K/V reloads).
 // dedup: qkv holds unique rows; sequence s, position t reads row (t == mask_pos ? urow_m : urow_h + t)
 hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0, int s1, int row0,
-                                 int H, int heads, f16* ctx, int kx, hipStream_t st, bool dedup = false);
+                                 int H, int heads, f16* ctx, int kx, hipStream_t st, bool dedup = false,
+                                 int max_len = 0);
 // resq = LN(x32[query row]) (x32 pre-LN, with its row statistics and LN weight / bias)
 hipError_t launch_attention_query(const void* qkv, bool qkv32, const float* x32, const float2* stats,
                                   const float* g, const float* b, SeqMeta sm, int s0, int s1,

@@ -535,6 +535,143 @@ attn_tr_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
     }
 }
 
+// One wave per (sequence, head) on v_mfma_f32_16x16x32_f16: query tiles of 16 and key tiles
+// of 16 (a T = 35 sequence computes 48 x 48 scores instead of 64 x 64 with 32-wide tiles, and
+// 12 instead of 16 softmax values per lane and query tile).
+//  * Xt = K.Qt per (16-key tile, 16-query tile): lane l holds query l&15, keys 4(l>>4)+e.
+//  * softmax over keys: in-lane over the key tiles, then across the 4 lanes of a query
+//    (xor 16, 32).
+//  * Ot = Vt.Pt per (16-dim tile, 32-key step m): the P fragment is the two key tiles 2m, 2m+1
+//    straight from the score registers, so its k index 8(l>>4)+j is key 32m + 4(l>>4) + j
+//    (j < 4) or 32m + 16 + 4(l>>4) + j - 4; the Vt fragment follows the same key order with two
+//    ds_read_b64_tr_b16 (rows 32m + 4g .. +3 and 32m + 16 + 4g .. +3 of the row-major V image,
+//    16 columns).  V row stride 80 halfs: the 8 rows x 16 columns a 32-lane half reads land on
+//    disjoint 8-bank ranges.  Vt fragments are read once per key block into registers.
+// Online softmax over key blocks of 64 for T > 64.  DEDUP as attn_tr_kernel.
+template <bool DEDUP>
+__global__ void __launch_bounds__(64, 3)
+attn16_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
+              f16* __restrict__ ctx, int kx) {
+    typedef __fp16 fp16x4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
+    constexpr int VR = 80;
+    __shared__ __attribute__((aligned(16))) f16 sV[64 * VR];
+    const int s = s0 + blockIdx.x, hd = blockIdx.y;
+    const int T = sm.len[s], rs = sm.row[s] - row0;
+    const int lane = threadIdx.x, r16 = lane & 15, g = lane >> 4;
+    const int ld = 3 * H;
+    const int ub = DEDUP ? sm.urow_h[s] : rs;
+    const int mp = DEDUP ? sm.mask_pos[s] : -1, um = DEDUP ? sm.urow_m[s] : 0;
+    const f16* base = qkv + (size_t)ub * ld + hd * 64;
+    const f16* mbase = qkv + (size_t)um * ld + hd * 64;
+    auto rowp = [&](int t) -> const f16* {
+        if constexpr (DEDUP) return t == mp ? mbase : base + (size_t)t * ld;
+        else return base + (size_t)t * ld;
+    };
+    const float scale = 0.125f;                   // head_dim ** -0.5
+    const int nkb = (T + 63) >> 6;
+    // transposed-read role: lane 4q+p of group g supplies row 4g + q, columns 4p
+    const int tr_off = (4 * g + ((lane & 15) >> 2)) * VR + 4 * (lane & 3);
+    auto tr_read = [&](const f16* p) {
+        const fp16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) fp16x4*)p);
+        return __builtin_bit_cast(half4, v);
+    };
+    half8 kf[4][2];                               // [key tile][32-dim step]
+    half8 vf[4][2];                               // Vt fragments [16-dim tile][32-key step]
+    auto load_kv = [&](int k0) {
+        half8 v[8];
+#pragma unroll
+        for (int it = 0; it < 8; ++it) {
+            const int kr = k0 + it * 8 + (lane >> 3);
+            v[it] = kr < T ? *(const half8*)(rowp(kr) + 2 * H + (lane & 7) * 8) : (half8){};
+        }
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+            for (int ks = 0; ks < 2; ++ks) {
+                const int key = k0 + kt * 16 + r16;
+                kf[kt][ks] = key < T ? *(const half8*)(rowp(key) + H + ks * 32 + g * 8) : (half8){};
+            }
+        __syncthreads();                          // previous block's V reads are done
+#pragma unroll
+        for (int it = 0; it < 8; ++it)
+            *(half8*)(sV + (it * 8 + (lane >> 3)) * VR + (lane & 7) * 8) = v[it];
+        __syncthreads();
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+            for (int m2 = 0; m2 < 2; ++m2) {
+                const f16* p = sV + (32 * m2) * VR + 16 * dt + tr_off;
+                const half4 lo = tr_read(p), hi = tr_read(p + 16 * VR);
+                vf[dt][m2] = (half8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            }
+    };
+    for (int q0 = 0; q0 < T; q0 += 16) {
+        const int t = q0 + r16;
+        half8 qf[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) qf[ks] = t < T ? *(const half8*)(rowp(t) + ks * 32 + g * 8) : (half8){};
+        f32x4 o[4] = {(f32x4){}, (f32x4){}, (f32x4){}, (f32x4){}};   // Ot[16-dim tile], lane = query
+        float m = -INFINITY, l = 0.f;
+        for (int kb = 0; kb < nkb; ++kb) {
+            const int k0 = kb * 64;
+            if (nkb > 1 || q0 == 0) load_kv(k0);
+            const int nkt = min(4, (T - k0 + 15) >> 4);
+            f32x4 x[4];
+            float bm = -INFINITY;
+#pragma unroll
+            for (int kt = 0; kt < 4; ++kt) {
+                x[kt] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+                if (kt < nkt) {
+                    f32x4 a = {};
+#pragma unroll
+                    for (int ks = 0; ks < 2; ++ks) a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kf[kt][ks], qf[ks], a, 0, 0, 0);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) {
+                        const int key = k0 + kt * 16 + 4 * g + e;
+                        const float v = key < T ? a[e] * scale : -INFINITY;
+                        x[kt][e] = v;
+                        bm = fmaxf(bm, v);
+                    }
+                }
+            }
+            bm = fmaxf(bm, __shfl_xor(bm, 16));
+            bm = fmaxf(bm, __shfl_xor(bm, 32));
+            const float mn = fmaxf(m, bm);
+            const float alpha = __expf(m - mn);
+            half8 pf[2];
+            float ls = 0.f;
+#pragma unroll
+            for (int m2 = 0; m2 < 2; ++m2)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const f16 ph = (f16)__expf(x[2 * m2 + (j >> 2)][j & 3] - mn);
+                    pf[m2][j] = ph;
+                    ls += (float)ph;
+                }
+            ls += __shfl_xor(ls, 16);
+            ls += __shfl_xor(ls, 32);
+            l = l * alpha + ls;
+            m = mn;
+            const int nm = (nkt + 1) >> 1;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                o[dt] *= alpha;
+#pragma unroll
+                for (int m2 = 0; m2 < 2; ++m2)
+                    if (m2 < nm) o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(vf[dt][m2], pf[m2], o[dt], 0, 0, 0);
+            }
+        }
+        if (t < T) {
+            const float il = 1.0f / l;
+            f16* orow = ctx + (size_t)(rs + t) * kx * H;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+                put_split4(orow, hd * 64 + dt * 16 + 4 * g, H, kx,
+                           make_float4(o[dt][0] * il, o[dt][1] * il, o[dt][2] * il, o[dt][3] * il));
+        }
+    }
+}
+
 // Last layer: one wave per (sequence, head), only the scored query row.  Lanes over keys
 // for QK^T, lanes over the 64 head dims for P.V.
 template <class QT>
@@ -770,7 +907,7 @@ hipError_t launch_ln_res_rows(float* x32, float2* stats, const float* pg, const 
 }
 
 hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0, int s1, int row0,
-                                 int H, int heads, f16* ctx, int kx, hipStream_t st, bool dedup) {
+                                 int H, int heads, f16* ctx, int kx, hipStream_t st, bool dedup, int max_len) {
     if (s1 <= s0) return hipSuccess;
     const dim3 grid(s1 - s0, heads);
     // RS_ATTN_ORDER: "seq" (default: grid (sequence, head)) or "head" (1-D grid, heads of a
@@ -781,8 +918,16 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
     }();
     const dim3 grid_tr = head_order ? dim3((s1 - s0) * heads) : grid;
     const int hf = head_order ? heads : 0;
+    // RS_ATTN16: 1 = 16x16x32 attention (attn16_kernel), 0 = 32x32x16 (attn_tr_kernel)
+    const char* a16 = getenv("RS_ATTN16");
+    // (T > 64 re-stages K/V per 16-query tile: slower than the 32-query tiles there)
+    const bool use16 = !(a16 && !strcmp(a16, "0")) && !head_order && max_len > 0 && max_len <= 64;
     if (dedup) {                                  // fp16 QKV, kx == 1 only (host gates it)
         if (qkv32 || kx != 1 || H % 64) return hipErrorInvalidValue;
+        if (use16) {
+            hipLaunchKernelGGL(attn16_kernel<true>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
+            return hipGetLastError();
+        }
         hipLaunchKernelGGL(attn_tr_kernel<true>, grid_tr, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx, hf);
         return hipGetLastError();
     }
@@ -795,6 +940,8 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
     }();
     if (qkv32)
         hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
+    else if (kind == 0 && use16)
+        hipLaunchKernelGGL(attn16_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
     else if (kind == 2)
         hipLaunchKernelGGL(attn_full_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
     else if (kind == 1)
@@ -885,7 +1032,9 @@ extern "C" int rs_debug_attention(int kind, const void* qkv, const int* len, con
     hipStream_t st = (hipStream_t)stream;
     if (kind == 0)      // (sequence, head) grid
         hipLaunchKernelGGL(attn_tr_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1, 0);
-    else if (kind == 5) // head-fastest 1-D grid (production order)
+    else if (kind == 6) // 16x16x32 attention
+        hipLaunchKernelGGL(attn16_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
+    else if (kind == 5) // head-fastest 1-D grid
         hipLaunchKernelGGL(attn_tr_kernel<false>, dim3(n_seq * heads), dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1, heads);
     else if (kind == 1)
         hipLaunchKernelGGL(attn_mfma_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);

@@ -58,6 +58,7 @@ struct Layer {
 struct Chunk {
     int s0, s1, rows;
     int urows = 0;     // layer-0 unique rows (dedup mode), 0 = dedup off for this chunk
+    int max_len = 0;   // longest sequence of the chunk (attention kernel choice)
 };
 
 }  // namespace
@@ -321,7 +322,7 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
         if (!last) {
             {
                 ProfScope ps(m, st, RS_K_ATTN, 0);
-                HIPTRY(launch_attention_full(qkv, q32, sm, c.s0, c.s1, 0, H, nh, ctx, kx, st, uq));
+                HIPTRY(launch_attention_full(qkv, q32, sm, c.s0, c.s1, 0, H, nh, ctx, kx, st, uq, c.max_len));
             }
             if (kx == 1 && oproj_f16()) {
                 // O projection as a persistent fp16-output GEMM into the (free) FFN1 buffer; the
@@ -442,21 +443,23 @@ int run_all(rs_model* m, hipStream_t st, const int* d_tok, SeqList& sl, int mode
     HIPTRY(hipSetDevice(m->device));
     const size_t S = sl.size();
     std::vector<Chunk> chunks;
-    int rows = 0, s0 = 0;
+    int rows = 0, s0 = 0, max_len = 0;
     for (size_t s = 0; s < S; ++s) {
         const int T = sl.len[s];
         if (T > m->cfg.max_pos) return fail(RS_EUNSUP, "sequence longer than max_position_embeddings");
         if (T < 1) return fail(RS_EARG, "empty sequence");
         if (T > m->max_rows) return fail(RS_EARG, "sequence longer than the reserved rows");
         if (rows + T > m->max_rows || (int)s - s0 >= m->s_cap) {
-            chunks.push_back({s0, (int)s, rows});
+            chunks.push_back({s0, (int)s, rows, 0, max_len});
             s0 = (int)s;
             rows = 0;
+            max_len = 0;
         }
         sl.row[s] = rows;
         rows += T;
+        max_len = std::max(max_len, T);
     }
-    if (S) chunks.push_back({s0, (int)S, rows});
+    if (S) chunks.push_back({s0, (int)S, rows, 0, max_len});
     // layer-0 dedup: MLM mode, fp16 operands, >= 2 layers (layer 0 is not the query-only layer)
     const char* dedup_s = getenv("RS_DEDUP");      // read per call (tests flip it)
     const int dedup_env = dedup_s ? atoi(dedup_s) : 1;

@@ -18,7 +18,7 @@ import __graft_entry__  # noqa: E402
 __graft_entry__._import_pkg()
 from asr_rescoring_amd import _lib  # noqa: E402
 
-NAMES = {0: "tr", 1: "mfma", 2: "valu", 3: "mem1", 4: "mem4", 5: "tr-headmajor"}
+NAMES = {0: "tr", 1: "mfma", 2: "valu", 3: "mem1", 4: "mem4", 5: "tr-headmajor", 6: "attn16"}
 
 
 def main():
@@ -55,7 +55,7 @@ def main():
         ctx.zero_()
         assert call() == 0
         torch.cuda.synchronize()
-        err = max((ctx[r0:r0 + t].float() - ref).abs().max().item() for r0, t, ref in refs) if kind in (0, 1, 2, 5) else float('nan')
+        err = max((ctx[r0:r0 + t].float() - ref).abs().max().item() for r0, t, ref in refs) if kind in (0, 1, 2, 5, 6) else float('nan')
         for _ in range(3):
             call()
         res = []
