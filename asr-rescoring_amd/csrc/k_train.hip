@@ -392,10 +392,13 @@ __global__ void tr_cls_bwd_kernel(const float* __restrict__ dsc, const float* __
 
 // Distillation losses (single block; utterances strided over threads, totals summed by
 // thread 0 in order).  See train.h for the definitions.
+// dsc and uloss are written by one thread and read by another across __syncthreads(): no
+// __restrict__ on them, so the compiler cannot move those accesses over the barriers (see
+// tr_ce_kernel).
 __global__ void tr_loss_kernel(const float* __restrict__ sc, const float* __restrict__ tgt,
                                const float* __restrict__ am, const float* __restrict__ err,
                                const int* __restrict__ utt_off, int n_utt, int n_hyp, int kind, float lam,
-                               float* __restrict__ dsc, float* __restrict__ uloss, float* __restrict__ loss) {
+                               float* dsc, float* uloss, float* __restrict__ loss) {
     const float inv_n = 1.0f / (float)n_hyp;
     for (int h = threadIdx.x; h < n_hyp; h += blockDim.x) dsc[h] = 2.0f * (sc[h] - tgt[h]) * inv_n;
     __syncthreads();
@@ -461,12 +464,19 @@ __device__ __forceinline__ float block_reduce(float v, float* sh, bool is_max) {
 
 // BertForMaskedLM CE (modeling_bert.py:972-975, mean over rows): per row lse - logit[label];
 // logits are replaced by d loss / d logits = (softmax - onehot) / M
+// The label logit goes through LDS before the first barrier: read from global after the
+// reductions (as before), the compiler was free to sink that load past the __syncthreads() that
+// precedes the in-place gradient writes (logits was __restrict__), so the row's CE sometimes
+// used the thread-(label) gradient instead of the logit — one row's CE off by ~1 in roughly
+// one step in four (tools/diag/mlm_first_step.py: 32 of 32 correct after the fix).
 __global__ void __launch_bounds__(256)
-tr_ce_kernel(float* __restrict__ logits, const int* __restrict__ labels, int M, int V, float* __restrict__ rl) {
+tr_ce_kernel(float* logits, const int* __restrict__ labels, int M, int V, float* __restrict__ rl) {
     __shared__ float sh[256];
+    __shared__ float s_xl;
     const int row = blockIdx.x, tid = threadIdx.x;
     float* x = logits + (size_t)row * V;
     const int lab = min(max(labels[row], 0), V - 1);
+    if (tid == 0) s_xl = x[lab];
     float m = -INFINITY;
     for (int j = tid; j < V; j += 256) m = fmaxf(m, x[j]);
     m = block_reduce(m, sh, true);
@@ -474,9 +484,8 @@ tr_ce_kernel(float* __restrict__ logits, const int* __restrict__ labels, int M, 
     for (int j = tid; j < V; j += 256) sum += __expf(x[j] - m);
     sum = block_reduce(sum, sh, false);
     const float lse = m + __logf(sum);
-    const float xl = x[lab];
+    if (tid == 0) rl[row] = lse - s_xl;       // s_xl written before block_reduce's barriers
     __syncthreads();
-    if (tid == 0) rl[row] = lse - xl;
     const float inv = 1.0f / (float)M;
     for (int j = tid; j < V; j += 256) x[j] = (__expf(x[j] - lse) - (j == lab ? 1.0f : 0.0f)) * inv;
 }

@@ -326,20 +326,24 @@ int prepare(StepCtx& c, const int32_t* d_tok, const int32_t* h_off, int n_seq, c
     c.seq = c.dm + i_seq;
 
     const bool mlm = cf.heads_mask == RS_HEAD_MLM;
-    const size_t MH = (size_t)M * H, MF = (size_t)M * F, M2 = (size_t)M * 2, PS = (size_t)pofs[S];
-    const size_t MV = mlm ? (size_t)M * cf.vocab : 0;
-    const size_t per_layer = MH + 3 * MH + PS + MH + MH + M2 + MH + 2 * MF + MH + M2;
+    // every region starts on a 256-byte boundary (an odd row count M would otherwise leave the
+    // tensors after the float2 statistics 8-byte aligned under float4 accesses and rocBLAS)
+    auto al = [](size_t n) { return (n + 63) & ~(size_t)63; };
+    const size_t MH = al((size_t)M * H), MF = al((size_t)M * F), M2 = al((size_t)M * 2), PS = al((size_t)pofs[S]);
+    const size_t QKV = al((size_t)M * 3 * H);
+    const size_t MV = mlm ? al((size_t)M * cf.vocab) : 0;
+    const size_t per_layer = MH + QKV + PS + MH + MH + M2 + MH + 2 * MF + MH + M2;
     const size_t n_head = mlm ? 3 * MH + M2 + MV : 0;
     const size_t n_act = MH + M2 + NL * per_layer + MH + n_head;
     TRY_HIP(t->act.ensure(n_act * 4));
     const int widest = std::max(std::max(3 * H, F), mlm ? cf.vocab : 0);
-    const size_t n_part = tr_colsum_scratch(M, widest) / 4;
-    const size_t n_grad = 2 * MH + 3 * MH + MF + n_part + 2 * (size_t)S + aux.size() + M + 64;
+    const size_t n_part = al(tr_colsum_scratch(M, widest) / 4);
+    const size_t n_grad = 2 * MH + QKV + MF + n_part + 2 * (size_t)S + aux.size() + M + 64;
     TRY_HIP(t->grad.ensure(n_grad * 4));
     float* A = t->act.f();
     c.x0 = A;
     c.st0 = (float2*)(c.x0 + MH);
-    float* lbase = (float*)(c.st0 + M);
+    float* lbase = c.x0 + MH + M2;
     c.la.assign(NL + 1, StepCtx::LA{});
     for (int l = 0; l <= NL; ++l) {
         float* b = lbase + (size_t)l * per_layer;
@@ -347,11 +351,11 @@ int prepare(StepCtx& c, const int32_t* d_tok, const int32_t* h_off, int n_seq, c
         a.hin = b;
         if (l == NL) break;
         a.qkv = b + MH;
-        a.P = a.qkv + 3 * MH;
+        a.P = a.qkv + QKV;
         a.ctx = a.P + PS;
         a.x1 = a.ctx + MH;
         a.st1 = (float2*)(a.x1 + MH);
-        a.h1 = (float*)(a.st1 + M);
+        a.h1 = a.x1 + MH + M2;
         a.pre = a.h1 + MH;
         a.act = a.pre + MF;
         a.x2 = a.act + MF;
@@ -362,13 +366,13 @@ int prepare(StepCtx& c, const int32_t* d_tok, const int32_t* h_off, int n_seq, c
         c.tx = c.tpre + MH;
         c.th = c.tx + MH;
         c.tst = (float2*)(c.th + MH);
-        c.logits = (float*)(c.tst + M);
+        c.logits = c.th + MH + M2;
     }
     float* G = t->grad.f();
     c.dA = G;
     c.dB = c.dA + MH;
     c.dQKV = c.dB + MH;
-    c.dF = c.dQKV + 3 * MH;
+    c.dF = c.dQKV + QKV;
     c.part = c.dF + MF;
     c.tail = c.part + n_part;        // per-sequence / per-row small arrays
     return RS_OK;
