@@ -672,6 +672,149 @@ attn16_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
     }
 }
 
+// fp16x3 precision mode (fp32 Q/K/V from the split-operand QKV GEMM): attn16_kernel's tiling
+// with every MFMA operand split into fp16 hi + lo parts and three MFMAs per product
+// (hi.hi + hi.lo + lo.hi, the lo.lo term is below fp32 rounding): Xt = K.Qt and Ot = Vt.Pt to
+// fp32-level accuracy on the matrix cores instead of the fp32 VALU attention.  The f16 MFMA
+// flushes subnormal inputs, and lo = x - hi is subnormal for |x| < 0.25, so lo parts are
+// stored scaled by 2^12 (LO_SCALE) and their products go to separate accumulators scaled back
+// by 2^-12: 1e-7-level error instead of 3e-5 (tools/diag/attn_split_check.py).  P is split
+// after the exponential; the softmax row sum adds the fp32 P.  V is staged as two fp16 images
+// (hi, scaled lo) with the same 80-half rows.  T <= 64 (one key block; the host routes longer
+// sequences to attn_full_kernel<float>).
+constexpr float LO_SCALE = 4096.f, LO_UNSCALE = 1.f / 4096.f;
+__device__ __forceinline__ void split8(const float* p, half8& hi, half8& lo) {
+    const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        hi[e] = (f16)v[e];
+        lo[e] = (f16)((v[e] - (float)hi[e]) * LO_SCALE);
+    }
+}
+
+__global__ void __launch_bounds__(64, 2)
+attn16x3_kernel(const float* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
+                f16* __restrict__ ctx, int kx) {
+    typedef __fp16 fp16x4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
+    constexpr int VR = 80;
+    __shared__ __attribute__((aligned(16))) f16 sVh[64 * VR];
+    __shared__ __attribute__((aligned(16))) f16 sVl[64 * VR];
+    const int s = s0 + blockIdx.x, hd = blockIdx.y;
+    const int T = sm.len[s], rs = sm.row[s] - row0;
+    const int lane = threadIdx.x, r16 = lane & 15, g = lane >> 4;
+    const int ld = 3 * H;
+    const float* base = qkv + (size_t)rs * ld + hd * 64;
+    const float scale = 0.125f;
+    const int tr_off = (4 * g + ((lane & 15) >> 2)) * VR + 4 * (lane & 3);
+    auto tr_read = [&](const f16* p) {
+        const fp16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) fp16x4*)p);
+        return __builtin_bit_cast(half4, v);
+    };
+    // V rows (fp32) -> hi / lo fp16 images: 16 float4 per row, 4 rows per pass of the wave
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+        const int kr = it * 4 + (lane >> 4), c4 = (lane & 15) * 4;
+        const float4 v = kr < T ? *(const float4*)(base + (size_t)kr * ld + 2 * H + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const half4 h = {(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
+        const half4 l = {(f16)((v.x - (float)h[0]) * LO_SCALE), (f16)((v.y - (float)h[1]) * LO_SCALE),
+                         (f16)((v.z - (float)h[2]) * LO_SCALE), (f16)((v.w - (float)h[3]) * LO_SCALE)};
+        *(half4*)(sVh + kr * VR + c4) = h;
+        *(half4*)(sVl + kr * VR + c4) = l;
+    }
+    half8 kfh[4][2], kfl[4][2];
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int key = kt * 16 + r16;
+            if (key < T) split8(base + (size_t)key * ld + H + ks * 32 + g * 8, kfh[kt][ks], kfl[kt][ks]);
+            else kfh[kt][ks] = kfl[kt][ks] = (half8){};
+        }
+    __syncthreads();
+    half8 vfh[4][2], vfl[4][2];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+        for (int m2 = 0; m2 < 2; ++m2) {
+            const int o = (32 * m2) * VR + 16 * dt + tr_off;
+            half4 lo = tr_read(sVh + o), hi = tr_read(sVh + o + 16 * VR);
+            vfh[dt][m2] = (half8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+            lo = tr_read(sVl + o);
+            hi = tr_read(sVl + o + 16 * VR);
+            vfl[dt][m2] = (half8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        }
+    const int nkt = min(4, (T + 15) >> 4), nm = (nkt + 1) >> 1;
+    for (int q0 = 0; q0 < T; q0 += 16) {
+        const int t = q0 + r16;
+        half8 qh[2], ql[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            if (t < T) split8(base + (size_t)t * ld + ks * 32 + g * 8, qh[ks], ql[ks]);
+            else qh[ks] = ql[ks] = (half8){};
+        }
+        f32x4 x[4];
+        float bm = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+            x[kt] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+            if (kt < nkt) {
+                f32x4 a = {}, al = {};
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    al = __builtin_amdgcn_mfma_f32_16x16x32_f16(kfl[kt][ks], qh[ks], al, 0, 0, 0);
+                    al = __builtin_amdgcn_mfma_f32_16x16x32_f16(kfh[kt][ks], ql[ks], al, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kfh[kt][ks], qh[ks], a, 0, 0, 0);
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int key = kt * 16 + 4 * g + e;
+                    const float v = key < T ? __builtin_fmaf(al[e], LO_UNSCALE, a[e]) * scale : -INFINITY;
+                    x[kt][e] = v;
+                    bm = fmaxf(bm, v);
+                }
+            }
+        }
+        bm = fmaxf(bm, __shfl_xor(bm, 16));
+        bm = fmaxf(bm, __shfl_xor(bm, 32));
+        half8 ph[2], pl[2];
+        float ls = 0.f;
+#pragma unroll
+        for (int m2 = 0; m2 < 2; ++m2)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float p = __expf(x[2 * m2 + (j >> 2)][j & 3] - bm);
+                ph[m2][j] = (f16)p;
+                pl[m2][j] = (f16)((p - (float)ph[m2][j]) * LO_SCALE);
+                ls += p;
+            }
+        ls += __shfl_xor(ls, 16);
+        ls += __shfl_xor(ls, 32);
+        f32x4 o[4];
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            f32x4 oh = {}, ol = {};
+#pragma unroll
+            for (int m2 = 0; m2 < 2; ++m2)
+                if (m2 < nm) {
+                    ol = __builtin_amdgcn_mfma_f32_16x16x32_f16(vfl[dt][m2], ph[m2], ol, 0, 0, 0);
+                    ol = __builtin_amdgcn_mfma_f32_16x16x32_f16(vfh[dt][m2], pl[m2], ol, 0, 0, 0);
+                    oh = __builtin_amdgcn_mfma_f32_16x16x32_f16(vfh[dt][m2], ph[m2], oh, 0, 0, 0);
+                }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[dt][e] = __builtin_fmaf(ol[e], LO_UNSCALE, oh[e]);
+        }
+        if (t < T) {
+            const float il = 1.0f / ls;
+            f16* orow = ctx + (size_t)(rs + t) * kx * H;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+                put_split4(orow, hd * 64 + dt * 16 + 4 * g, H, kx,
+                           make_float4(o[dt][0] * il, o[dt][1] * il, o[dt][2] * il, o[dt][3] * il));
+        }
+    }
+}
+
 // Last layer: one wave per (sequence, head), only the scored query row.  Lanes over keys
 // for QK^T, lanes over the 64 head dims for P.V.
 template <class QT>
@@ -938,7 +1081,12 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
         if (v && !strcmp(v, "mfma")) return 1;
         return 0;
     }();
-    if (qkv32)
+    // RS_ATTN16X3=0: fp32 VALU attention in the fp16x3 mode instead of the split-MFMA kernel
+    const char* a16x3 = getenv("RS_ATTN16X3");
+    const bool use16x3 = !(a16x3 && !strcmp(a16x3, "0")) && max_len > 0 && max_len <= 64 && H % 64 == 0;
+    if (qkv32 && use16x3)
+        hipLaunchKernelGGL(attn16x3_kernel, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
+    else if (qkv32)
         hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
     else if (kind == 0 && use16)
         hipLaunchKernelGGL(attn16_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
@@ -1032,6 +1180,10 @@ extern "C" int rs_debug_attention(int kind, const void* qkv, const int* len, con
     hipStream_t st = (hipStream_t)stream;
     if (kind == 0)      // (sequence, head) grid
         hipLaunchKernelGGL(attn_tr_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1, 0);
+    else if (kind == 8) // split-precision 16x16x32 attention over fp32 qkv [rows, 3H], ctx fp16 image [rows, 3H]
+        hipLaunchKernelGGL(attn16x3_kernel, grid, dim3(64), 0, st, (const float*)qkv, sm, 0, 0, H, (f16*)ctx, 3);
+    else if (kind == 9) // fp32 VALU attention (same I/O as kind 8)
+        hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, 0, 0, H, (f16*)ctx, 3);
     else if (kind == 6) // 16x16x32 attention
         hipLaunchKernelGGL(attn16_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
     else if (kind == 5) // head-fastest 1-D grid

@@ -20,7 +20,7 @@ pytestmark = pytest.mark.gpu
 LENGTHS = [1, 2, 3, 15, 16, 17, 31, 32, 33, 34, 47, 48, 49, 63, 64, 65, 96, 100, 128, 130, 200]
 
 
-def _run(kind, qkv, T, row, H, heads):
+def _run(kind, qkv, T, row, H, heads, kx=1):
     lib = _lib.load()
     fn = lib.rs_debug_attention
     fn.restype = ctypes.c_int
@@ -28,7 +28,7 @@ def _run(kind, qkv, T, row, H, heads):
     dev = qkv.device
     d_len = torch.from_numpy(T).to(dev)
     d_row = torch.from_numpy(row).to(dev)
-    ctx = torch.full((qkv.shape[0], H), float("nan"), device=dev, dtype=torch.float16)
+    ctx = torch.full((qkv.shape[0], kx * H), float("nan"), device=dev, dtype=torch.float16)
     assert fn(kind, qkv.data_ptr(), d_len.data_ptr(), d_row.data_ptr(), len(T), H, heads, ctx.data_ptr(),
               torch.cuda.current_stream().cuda_stream) == 0
     torch.cuda.synchronize()
@@ -71,3 +71,29 @@ def test_attention_kernels_agree():
     a = _run(0, qkv, T, row, H, heads).float()
     b = _run(6, qkv, T, row, H, heads).float()
     assert (a - b).abs().max().item() < 2e-3
+
+
+@pytest.mark.parametrize("kind", [8, 9])
+def test_split_precision_attention_vs_torch(kind):
+    """fp16x3 mode: fp32 Q/K/V, ctx written as the [hi | hi | lo] operand image.  kind 8 =
+    attn16x3_kernel (three fp16 MFMAs per product), kind 9 = fp32 VALU kernel; both at
+    fp32-level accuracy: |hi + lo - ref| <= 2e-6 on O(1) outputs.  T <= 64 (kind 8's range)."""
+    H, heads = 768, 12
+    rng = np.random.default_rng(4)
+    T = np.array([t for t in LENGTHS if t <= 64] * 2, np.int32)
+    rng.shuffle(T)
+    row = np.concatenate([[0], np.cumsum(T)[:-1]]).astype(np.int32)
+    dev = torch.device("cuda", 0)
+    g = torch.Generator(device=dev).manual_seed(13)
+    qkv = torch.randn(int(T.sum()), 3 * H, device=dev, generator=g) * 0.6
+    ctx = _run(kind, qkv, T, row, H, heads, kx=3).float()
+    got_all = ctx[:, :H] + ctx[:, 2 * H:]
+    assert torch.equal(ctx[:, :H], ctx[:, H:2 * H])
+    worst = 0.0
+    for r0, t in zip(row.tolist(), T.tolist()):
+        x = qkv[r0:r0 + t].double().view(t, 3, heads, 64)
+        q, k, v = x[:, 0].transpose(0, 1), x[:, 1].transpose(0, 1), x[:, 2].transpose(0, 1)
+        p = torch.softmax(q @ k.transpose(1, 2) * 0.125, dim=-1)
+        ref = (p @ v).transpose(0, 1).reshape(t, H)
+        worst = max(worst, (got_all[r0:r0 + t].double() - ref).abs().max().item())
+    assert worst < 2e-6, worst

@@ -63,10 +63,16 @@ def c2():
     for prec in ("fp16x3", "fp16"):
         sc = RescoreBertScorer(w, BERT_BASE, device=0, max_rows=131072, precision=prec)
         dt = _timed(lambda: sc.score_nbest(d_tok, nb.hyp_off))
+        sc.profile(True)
+        sc.score_nbest(d_tok, nb.hyp_off)
+        torch.cuda.synchronize()
+        kinds = sc.profile_read()
+        sc.profile(False)
         sc.close()
         out.append({"workload": "C2 RescoreBert U=1000 N=50", "precision": prec, "value": round(nb.n_hyp / dt, 1),
                     "unit": "hypothesis fwd/s", "ms_per_step": round(dt * 1e3, 2),
-                    "achieved_tflops_canonical": round(fl / dt / 1e12, 1)})
+                    "achieved_tflops_canonical": round(fl / dt / 1e12, 1),
+                    "kinds_ms": {k: round(v[0], 2) for k, v in kinds.items()}})
     return out
 
 
