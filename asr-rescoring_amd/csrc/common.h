@@ -43,25 +43,31 @@ struct EpiArgs {
 };
 
 // fp16 operand image of an fp32 activation row with logical width K:
-//   kx == 1: [hi]                  (RS_PREC_FP16)
-//   kx == 3: [hi | hi | lo]        (RS_PREC_FP16X3, lo = fp16(x - hi))
-// paired with the weight image [W_hi | W_lo | W_hi] the K-concatenated MFMA product is
-// A_hi.W_hi + A_hi.W_lo + A_lo.W_hi: fp32-level accuracy from fp16 MFMA in one accumulator.
+//   kx == 1: [hi]                          (RS_PREC_FP16)
+//   kx == 3: [hi | hi/64 | (x - hi)*64]    (RS_PREC_FP16X3)
+// paired with the weight image [W_hi | W_lo*64 | W_hi/64] the K-concatenated MFMA product is
+// A_hi.W_hi + A_hi.W_lo + A_lo.W_hi (the power-of-two factors cancel exactly): fp32-level
+// accuracy from fp16 MFMA in one accumulator.  The factors keep the lo parts out of the fp16
+// subnormal range, which the f16 MFMA flushes: lo = x - hi is subnormal for |x| < 0.25, and
+// weights of |W| ~ 0.05 have W_lo ~ 1e-5 (unscaled, those products were lost).
+constexpr float X3_UP = 64.f, X3_DOWN = 1.f / 64.f;
+__device__ __forceinline__ f16 x3_mid(f16 hi) { return (f16)((float)hi * X3_DOWN); }
+__device__ __forceinline__ f16 x3_lo(float v, f16 hi) { return (f16)((v - (float)hi) * X3_UP); }
 __device__ __forceinline__ void put_split(f16* row, int c, int K, int kx, float v) {
     const f16 hi = (f16)v;
     row[c] = hi;
     if (kx == 3) {
-        row[K + c] = hi;
-        row[2 * K + c] = (f16)(v - (float)hi);
+        row[K + c] = x3_mid(hi);
+        row[2 * K + c] = x3_lo(v, hi);
     }
 }
 __device__ __forceinline__ void put_split4(f16* row, int c, int K, int kx, float4 v) {
     const half4 hi = {(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
     *(half4*)(row + c) = hi;
     if (kx == 3) {
-        *(half4*)(row + K + c) = hi;
-        const half4 lo = {(f16)(v.x - (float)hi[0]), (f16)(v.y - (float)hi[1]),
-                          (f16)(v.z - (float)hi[2]), (f16)(v.w - (float)hi[3])};
+        const half4 mid = {x3_mid(hi[0]), x3_mid(hi[1]), x3_mid(hi[2]), x3_mid(hi[3])};
+        *(half4*)(row + K + c) = mid;
+        const half4 lo = {x3_lo(v.x, hi[0]), x3_lo(v.y, hi[1]), x3_lo(v.z, hi[2]), x3_lo(v.w, hi[3])};
         *(half4*)(row + 2 * K + c) = lo;
     }
 }

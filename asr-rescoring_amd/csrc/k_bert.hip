@@ -14,7 +14,7 @@
 //  segsum_f64      per-hypothesis PLL, float64, in row order (MLM_PLL/main.py:106-107)
 //
 // Every producer of a GEMM operand writes the fp16 operand image (put_split: [hi] or
-// [hi | hi | lo]).  The residual stream stays PRE-LayerNorm in fp32 (x32) with per-row
+// [hi | hi/64 | lo*64]).  The residual stream stays PRE-LayerNorm in fp32 (x32) with per-row
 // (mean, rstd): its consumers (the next residual GEMM's accumulator init, attention_query)
 // rebuild LN(x) with ln_apply, so no LN kernel writes an fp32 copy of its output.
 #include "common.h"

@@ -529,14 +529,19 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         if (ok) st16<VAR>((uint4*)(orow + col), sv);
                         if constexpr (EPI == EPI_GELU_F16) {
                             if (ep.kx == 3) {
-                                half8 l;
+                                half8 l, md;
 #pragma unroll
-                                for (int e = 0; e < 8; ++e) l[e] = (f16)(x[e] - (float)h[e]);
-                                uint4 lv = __builtin_bit_cast(uint4, l);
+                                for (int e = 0; e < 8; ++e) {
+                                    l[e] = x3_lo(x[e], h[e]);
+                                    md[e] = x3_mid(h[e]);
+                                }
+                                uint4 lv = __builtin_bit_cast(uint4, l), mv = __builtin_bit_cast(uint4, md);
                                 auto t0 = __builtin_amdgcn_permlane32_swap(lv.x, lv.z, false, false);
                                 auto t1 = __builtin_amdgcn_permlane32_swap(lv.y, lv.w, false, false);
+                                auto u0 = __builtin_amdgcn_permlane32_swap(mv.x, mv.z, false, false);
+                                auto u1 = __builtin_amdgcn_permlane32_swap(mv.y, mv.w, false, false);
                                 if (ok) {
-                                    st16<VAR>((uint4*)(orow + ep.nlog + col), sv);
+                                    st16<VAR>((uint4*)(orow + ep.nlog + col), make_uint4(u0[0], u1[0], u0[1], u1[1]));
                                     st16<VAR>((uint4*)(orow + 2 * ep.nlog + col), make_uint4(t0[0], t1[0], t0[1], t1[1]));
                                 }
                             }
@@ -613,15 +618,16 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         st16<VAR>((uint4*)((f16*)ep.out + o), __builtin_bit_cast(uint4, h));
                     } else if constexpr (EPI == EPI_GELU_F16) {
                         f16* orow = (f16*)ep.out + (size_t)row * ep.ldc;
-                        half8 h, l;
+                        half8 h, l, md;
 #pragma unroll
                         for (int e = 0; e < 8; ++e) {
                             h[e] = (f16)x[e];
-                            l[e] = (f16)(x[e] - (float)h[e]);
+                            l[e] = x3_lo(x[e], h[e]);
+                            md[e] = x3_mid(h[e]);
                         }
                         st16<VAR>((uint4*)(orow + col), __builtin_bit_cast(uint4, h));
                         if (ep.kx == 3) {
-                            st16<VAR>((uint4*)(orow + ep.nlog + col), __builtin_bit_cast(uint4, h));
+                            st16<VAR>((uint4*)(orow + ep.nlog + col), __builtin_bit_cast(uint4, md));
                             st16<VAR>((uint4*)(orow + 2 * ep.nlog + col), __builtin_bit_cast(uint4, l));
                         }
                     } else {  // fp32 outputs (residual already in acc)

@@ -105,7 +105,8 @@ struct rs_model {
 namespace {
 
 // Weight W [rows, cols] (nn.Linear [out, in]) -> fp16 operand image [rows_pad, kx*cols]:
-// kx == 1: [hi]; kx == 3: [hi | lo | hi] (pairs with the activation image [hi | hi | lo]).
+// kx == 1: [hi]; kx == 3: [hi | lo*64 | hi/64] (pairs with the activation image
+// [hi | hi/64 | lo*64], common.h put_split: the factors keep lo out of the fp16 subnormals).
 f16* upload_f16(rs_model* m, const std::vector<float>& src, size_t rows_pad, size_t cols, int kx,
                 hipError_t* err) {
     std::vector<f16> tmp(rows_pad * cols * kx, (f16)0.0f);
@@ -117,8 +118,8 @@ f16* upload_f16(rs_model* m, const std::vector<float>& src, size_t rows_pad, siz
             f16* row = tmp.data() + r * cols * kx;
             row[c] = hi;
             if (kx == 3) {
-                row[cols + c] = (f16)(v - (float)hi);
-                row[2 * cols + c] = hi;
+                row[cols + c] = (f16)((v - (float)hi) * 64.f);
+                row[2 * cols + c] = (f16)((float)hi * (1.f / 64.f));
             }
         }
     void* p = nullptr;

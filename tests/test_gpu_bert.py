@@ -90,8 +90,10 @@ def test_pll_fp16x3_golden(w_base, golden_dir):
     s = PLLScorer(w_base, BERT_BASE, device=0, max_rows=4096, precision="fp16x3")
     pll, rows = s.score_nbest(g["tokens"], g["hyp_off"], return_rows=True)
     s.close()
-    assert rel_err(pll.cpu().numpy(), g["pll"]).max() < 2e-5
-    assert rel_err(rows.cpu().numpy(), g["row_lp"]).max() < 2e-5      # well inside 1e-3 per row
+    # measured 1.9e-7 (PLL) / 1.1e-6 (rows) with the lo parts scaled out of the fp16 subnormal
+    # range (common.h put_split); 2e-5 / 2e-5 before, when the f16 MFMA flushed them
+    assert rel_err(pll.cpu().numpy(), g["pll"]).max() < 1e-6
+    assert rel_err(rows.cpu().numpy(), g["row_lp"]).max() < 5e-6
 
 
 def test_cls_golden(w_base, w_tiny, golden_dir):
