@@ -34,14 +34,15 @@ def weight_grid(mode: str = "norm") -> np.ndarray:
 
 
 def _strings(nb: NBest):
-    chars = nb.tokens.copy()
-    # strip [CLS]/[SEP]: hypothesis words only
-    off = nb.hyp_off
-    words = [nb.tokens[off[h] + 1:off[h + 1] - 1] for h in range(nb.n_hyp)]
-    flat = np.concatenate(words).astype(np.int32) if words else np.zeros(0, np.int32)
+    """Hypothesis words only ([CLS]/[SEP] stripped), flat int32 + offsets (vectorised)."""
+    off = np.asarray(nb.hyp_off, np.int64)
+    keep = np.ones(len(nb.tokens), bool)
+    if nb.n_hyp:
+        keep[off[:-1]] = False           # [CLS]
+        keep[off[1:] - 1] = False        # [SEP]
+    flat = np.ascontiguousarray(nb.tokens[keep], np.int32)
     soff = np.zeros(nb.n_hyp + 1, np.int32)
-    soff[1:] = np.cumsum([len(w) for w in words])
-    del chars
+    soff[1:] = np.cumsum(np.diff(off) - 2)
     return flat, soff
 
 
