@@ -40,6 +40,13 @@ struct EpiArgs {
     int kx;                // fp16 operand image width factor of the output (EPI_GELU_F16): 1 or 3
     int nlog;              // logical N (column offset of the image sections)
     int group_m;           // tile order: row panels per group (set by launch_gemm)
+    // EPI_RESLN_F32 with res_o16 != null (deferred BertSelfOutput residual): the residual is
+    // LN(LN0(res) + o16) with LN0 = (res_stats0, res_g0, res_b0) and LN = (res_stats, res_g,
+    // res_b), i.e. the post-attention stream ln_res_rows did not write back (WX = false)
+    const f16* res_o16;    // [M, ldc] fp16 O-projection output (bias included)
+    const float2* res_stats0;
+    const float* res_g0;
+    const float* res_b0;
 };
 
 // fp16 operand image of an fp32 activation row with logical width K:
@@ -121,10 +128,15 @@ hipError_t launch_embed_ln(const int* tok, SeqMeta sm, int s0, int s1, int row0,
                            float2* stats, f16* h16, int kx, hipStream_t st);
 hipError_t launch_ln_rows(const float* x, int rows, const float* g, const float* b, float eps,
                           int H, float* y32, float2* stats, f16* y16, int kx, hipStream_t st);
-// x32 <- LN(x32; stats, pg, pb) + o16, then stats / fp16 image of LN(x32; g, b) (kx == 1)
-hipError_t launch_ln_res_rows(float* x32, float2* stats, const float* pg, const float* pb, const f16* o16,
-                             int rows, const float* g, const float* b, float eps, int H, f16* y16,
-                             hipStream_t st);
+// x = LN(x32; stats, pg, pb) + o16, then stats_out / fp16 image of LN(x; g, b) (kx == 1);
+// write_x: x written back into x32 (else x32 is left as is and the consumer rebuilds x from
+// x32, stats, o16: EpiArgs.res_o16 or a second ln_res_rows).  o16b != null (needs write_x):
+// two residual blocks, x = LN(LN(x32; stats, pg, pb) + o16; stats1, g1, b1) + o16b.
+// stats_out may alias stats.
+hipError_t launch_ln_res_rows(float* x32, const float2* stats, float2* stats_out, const float* pg, const float* pb,
+                             const f16* o16, int rows, const float* g, const float* b, float eps, int H,
+                             f16* y16, bool write_x, hipStream_t st, const float2* stats1 = nullptr,
+                             const float* g1 = nullptr, const float* b1 = nullptr, const f16* o16b = nullptr);
 // Unique layer-0 rows (dedup): for every hypothesis of the chunk its T rows, and every
 // sequence's [MASK] row, as the fp16 operand image of LN(embedding) (rows of SeqMeta.urow_*)
 hipError_t launch_embed_unique(const int* tok, SeqMeta sm, int s0, int s1, int mask_id, int vocab,

@@ -144,17 +144,20 @@ ln_rows_kernel(const float* __restrict__ xin, int rows, const float* __restrict_
 // so the GEMM neither reads nor writes the fp32 stream.  x32 <- LN_prev(x32) + o16 (LN_prev
 // rebuilt from the row statistics in `stats` and (pg, pb)), then its statistics and the fp16
 // operand image of LN(x32) with (g, b).  fp16 precision mode (kx == 1) only.
-template <int NV>
+template <int NV, bool WX, bool TWO>
 __global__ void __launch_bounds__(256)
-ln_res_rows_kernel(float* __restrict__ x32, float2* __restrict__ stats, const float* __restrict__ pg,
+ln_res_rows_kernel(float* __restrict__ x32, const float2* stats, float2* stats_out, const float* __restrict__ pg,
                    const float* __restrict__ pb, const f16* __restrict__ o16, int rows,
                    const float* __restrict__ g, const float* __restrict__ b, float eps,
-                   f16* __restrict__ y16) {
+                   f16* __restrict__ y16, const float2* __restrict__ stats1, const float* __restrict__ g1,
+                   const float* __restrict__ b1, const f16* __restrict__ o16b) {
     constexpr int H = NV * 256;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (row >= rows) return;
     const float2 st0 = stats[row];
+    float2 st1 = make_float2(0.f, 0.f);
+    if constexpr (TWO) st1 = stats1[row];
     float4 x[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
@@ -165,9 +168,18 @@ ln_res_rows_kernel(float* __restrict__ x32, float2* __restrict__ stats, const fl
         const half4 o = *(const half4*)(o16 + (size_t)row * H + c);
         x[v] = make_float4(ln_apply(r.x, st0, gg.x, bb.x) + (float)o[0], ln_apply(r.y, st0, gg.y, bb.y) + (float)o[1],
                            ln_apply(r.z, st0, gg.z, bb.z) + (float)o[2], ln_apply(r.w, st0, gg.w, bb.w) + (float)o[3]);
-        *(float4*)(x32 + (size_t)row * H + c) = x[v];
+        if constexpr (TWO) {
+            // second residual block: x <- LN1(x; st1, g1, b1) + o16b (BertOutput after a deferred
+            // BertSelfOutput: x is the post-attention stream the first pass did not store)
+            const float4 g4 = *(const float4*)(g1 + c);
+            const float4 b4 = *(const float4*)(b1 + c);
+            const half4 ob = *(const half4*)(o16b + (size_t)row * H + c);
+            x[v] = make_float4(ln_apply(x[v].x, st1, g4.x, b4.x) + (float)ob[0], ln_apply(x[v].y, st1, g4.y, b4.y) + (float)ob[1],
+                               ln_apply(x[v].z, st1, g4.z, b4.z) + (float)ob[2], ln_apply(x[v].w, st1, g4.w, b4.w) + (float)ob[3]);
+        }
+        if constexpr (WX) *(float4*)(x32 + (size_t)row * H + c) = x[v];
     }
-    ln_store<NV>(x, g, b, eps, lane, nullptr, stats + row, y16 + (size_t)row * H, 1);
+    ln_store<NV>(x, g, b, eps, lane, nullptr, stats_out + row, y16 + (size_t)row * H, 1);
 }
 
 __device__ __forceinline__ void load8(const f16* p, float (&o)[8]) {
@@ -1036,16 +1048,34 @@ hipError_t launch_ln_rows(const float* x, int rows, const float* g, const float*
     return hipGetLastError();
 }
 
-hipError_t launch_ln_res_rows(float* x32, float2* stats, const float* pg, const float* pb, const f16* o16,
-                             int rows, const float* g, const float* b, float eps, int H, f16* y16,
-                             hipStream_t st) {
+hipError_t launch_ln_res_rows(float* x32, const float2* stats, float2* stats_out, const float* pg, const float* pb,
+                             const f16* o16, int rows, const float* g, const float* b, float eps, int H,
+                             f16* y16, bool write_x, hipStream_t st, const float2* stats1, const float* g1,
+                             const float* b1, const f16* o16b) {
     if (rows <= 0) return hipSuccess;
     const dim3 grid((rows + 3) / 4), block(256);
-    if (H == 768) hipLaunchKernelGGL(ln_res_rows_kernel<3>, grid, block, 0, st, x32, stats, pg, pb, o16, rows, g, b, eps, y16);
-    else if (H == 256) hipLaunchKernelGGL(ln_res_rows_kernel<1>, grid, block, 0, st, x32, stats, pg, pb, o16, rows, g, b, eps, y16);
-    else if (H == 512) hipLaunchKernelGGL(ln_res_rows_kernel<2>, grid, block, 0, st, x32, stats, pg, pb, o16, rows, g, b, eps, y16);
-    else if (H == 1024) hipLaunchKernelGGL(ln_res_rows_kernel<4>, grid, block, 0, st, x32, stats, pg, pb, o16, rows, g, b, eps, y16);
-    else return hipErrorInvalidValue;
+    const bool two = o16b != nullptr;
+    if (two && !write_x) return hipErrorInvalidValue;
+#define RS_LNR(NV)                                                                                                   \
+    do {                                                                                                             \
+        if (two)                                                                                                     \
+            hipLaunchKernelGGL((ln_res_rows_kernel<NV, true, true>), grid, block, 0, st, x32, stats, stats_out, pg,  \
+                               pb, o16, rows, g, b, eps, y16, stats1, g1, b1, o16b);                                 \
+        else if (write_x)                                                                                            \
+            hipLaunchKernelGGL((ln_res_rows_kernel<NV, true, false>), grid, block, 0, st, x32, stats, stats_out, pg, \
+                               pb, o16, rows, g, b, eps, y16, stats1, g1, b1, o16b);                                 \
+        else                                                                                                         \
+            hipLaunchKernelGGL((ln_res_rows_kernel<NV, false, false>), grid, block, 0, st, x32, stats, stats_out,    \
+                               pg, pb, o16, rows, g, b, eps, y16, stats1, g1, b1, o16b);                             \
+    } while (0)
+    switch (H) {
+        case 256: RS_LNR(1); break;
+        case 512: RS_LNR(2); break;
+        case 768: RS_LNR(3); break;
+        case 1024: RS_LNR(4); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef RS_LNR
     return hipGetLastError();
 }
 

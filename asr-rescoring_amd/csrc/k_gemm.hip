@@ -162,10 +162,14 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     {
         const int arow = m0 + wm * WTM + (lane % MS);
         const int acol = n0 + wn * WTN;
-        float2 rst[TM];                       // EPI_RESLN_F32: LN statistics of the residual rows
+        float2 rst[TM], rst0[TM];             // EPI_RESLN_F32: LN statistics of the residual rows
+        const bool defer = EPI == EPI_RESLN_F32 && ep.res_o16 != nullptr;
         if constexpr (EPI == EPI_RESLN_F32) {
 #pragma unroll
-            for (int i = 0; i < TM; ++i) rst[i] = ep.res_stats[arow + MS * i];
+            for (int i = 0; i < TM; ++i) {
+                rst[i] = ep.res_stats[arow + MS * i];
+                rst0[i] = defer ? ep.res_stats0[arow + MS * i] : make_float2(0.f, 0.f);
+            }
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j)
@@ -173,10 +177,14 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             for (int g = 0; g < NQ; ++g) {
                 const int col = acol + MS * j + qcol<MS>(g, lane);
                 const float4 b4 = (VAR & 2) ? make_float4(0.f, 0.f, 0.f, 0.f) : *(const float4*)(ep.bias + col);
-                float4 lg4, lb4;
+                float4 lg4, lb4, lg04, lb04;
                 if constexpr (EPI == EPI_RESLN_F32) {
                     lg4 = *(const float4*)(ep.res_g + col);
                     lb4 = *(const float4*)(ep.res_b + col);
+                    if (defer) {
+                        lg04 = *(const float4*)(ep.res_g0 + col);
+                        lb04 = *(const float4*)(ep.res_b0 + col);
+                    }
                 }
 #pragma unroll
                 for (int i = 0; i < TM; ++i) {
@@ -184,6 +192,13 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                     if constexpr ((EPI == EPI_RES_F32 || EPI == EPI_RESLN_F32) && !(VAR & 2)) {
                         float4 r4 = *(const float4*)(ep.res + (size_t)(arow + MS * i) * ep.ldc + col);
                         if constexpr (EPI == EPI_RESLN_F32) {
+                            if (defer) {   // post-attention stream: LN0(res) + o16 (ln_res_rows' x)
+                                const half4 o = *(const half4*)(ep.res_o16 + (size_t)(arow + MS * i) * ep.ldc + col);
+                                r4.x = ln_apply(r4.x, rst0[i], lg04.x, lb04.x) + (float)o[0];
+                                r4.y = ln_apply(r4.y, rst0[i], lg04.y, lb04.y) + (float)o[1];
+                                r4.z = ln_apply(r4.z, rst0[i], lg04.z, lb04.z) + (float)o[2];
+                                r4.w = ln_apply(r4.w, rst0[i], lg04.w, lb04.w) + (float)o[3];
+                            }
                             r4.x = ln_apply(r4.x, rst[i], lg4.x, lb4.x);
                             r4.y = ln_apply(r4.y, rst[i], lg4.y, lb4.y);
                             r4.z = ln_apply(r4.z, rst[i], lg4.z, lb4.z);

@@ -80,6 +80,7 @@ struct rs_model {
     int s_cap = 0, r_pad = 0, m_pad = 0;
     int kx = 1;                 // fp16 operand image width (1: fp16, 3: fp16x3)
     DevBuf xst, h16, t32, qkv, ctx, inter;   // xst: (mean, rstd) of the pre-LN rows in t32
+    DevBuf xst1;                // statistics of the post-attention stream (deferred residual)
     DevBuf ctxq, resq, tq32, hq32, hq16, interq, lab, llog, part, rowlp_tmp;
     DevBuf meta, hypoff;
     f16* emb_dst = nullptr;     // MODE_EMB output (rs_token_embed / rs_bertscore_recall)
@@ -154,6 +155,7 @@ int reserve_impl(rs_model* m, int64_t max_rows) {
     HIPTRY(hipSetDevice(m->device));
     const size_t kx = m->kx;
     HIPTRY(m->xst.ensure(M * sizeof(float2)));
+    HIPTRY(m->xst1.ensure(M * sizeof(float2)));
     HIPTRY(m->h16.ensure(M * H * 2 * kx));
     HIPTRY(m->t32.ensure(M * H * 4));
     HIPTRY(m->qkv.ensure(M * 3 * H * (kx == 3 ? 4 : 2)));
@@ -177,6 +179,7 @@ int reserve_impl(rs_model* m, int64_t max_rows) {
     HIPTRY(hipMemset(m->interq.p, 0, m->interq.bytes));
     HIPTRY(hipMemset(m->t32.p, 0, m->t32.bytes));    // pad rows of the residual stream stay finite
     HIPTRY(hipMemset(m->xst.p, 0, m->xst.bytes));
+    HIPTRY(hipMemset(m->xst1.p, 0, m->xst1.bytes));
     return RS_OK;
 }
 
@@ -244,6 +247,18 @@ enum Mode { MODE_MLM = 0, MODE_CLS = 1, MODE_EMB = 2 };
 bool oproj_f16() {
     const char* e = getenv("RS_OPROJ");
     return !(e && !strcmp(e, "resln"));
+}
+// RS_LNRES_DEFER (fp16 mode, O-projection split): ln_res_rows writes only the statistics and
+// the fp16 image of the post-attention stream x = LN0(x32) + o1 (o1 = fp16 O-projection
+// output), so x never round-trips through HBM in fp32, and x is rebuilt downstream:
+//   2 (default): BertOutput is a lean fp16-output GEMM (o2) and one second ln_res_rows pass
+//                forms LN2(LN1(LN0(x32) + o1) + o2) — no residual traffic in any GEMM epilogue;
+//   1: the BertOutput GEMM rebuilds x in its accumulator init (EpiArgs.res_o16) — slower: the
+//      extra loads sit in front of the tile's first MFMA;
+//   0: ln_res_rows writes x back into x32 and BertOutput reads it (EPI_RESLN_F32).
+int lnres_defer() {
+    const char* e = getenv("RS_LNRES_DEFER");
+    return e ? atoi(e) : 2;
 }
 // RS_FFN2: "resln" (default) or "f16" (the O-projection split applied to BertOutput)
 bool ffn2_f16() {
@@ -325,13 +340,20 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
                 ProfScope ps(m, st, RS_K_ATTN, 0);
                 HIPTRY(launch_attention_full(qkv, q32, sm, c.s0, c.s1, 0, H, nh, ctx, kx, st, uq, c.max_len));
             }
-            if (kx == 1 && oproj_f16()) {
-                // O projection as a persistent fp16-output GEMM into the (free) FFN1 buffer; the
-                // residual add + LayerNorm move into ln_res_rows, off the GEMM's critical path
-                ep = EpiArgs{}; ep.bias = L.bo; ep.out = inter; ep.ldc = H;
+            const bool fp16_split = kx == 1 && oproj_f16();
+            const int dmode = fp16_split && !ffn2_f16() ? lnres_defer() : 0;
+            const bool defer = dmode != 0;
+            // O-projection output (fp16): the dead QKV buffer when the BertOutput GEMM reads it
+            // back (deferred residual: it must survive FFN1), else the (free) FFN1 buffer
+            f16* o16 = defer ? (f16*)qkv : inter;
+            if (fp16_split) {
+                // O projection as a persistent fp16-output GEMM; the residual add + LayerNorm
+                // move into ln_res_rows, off the GEMM's critical path
+                ep = EpiArgs{}; ep.bias = L.bo; ep.out = o16; ep.ldc = H;
                 if (int r = gemm(m, st, RS_K_OPROJ, EPI_BIAS_F16, ctx, L.wo, rows, H, H, ep, H)) return r;
                 ProfScope ps(m, st, RS_K_OTHER, 0);
-                HIPTRY(launch_ln_res_rows(t32, xst, pg, pb, inter, rows, L.g1, L.be1, cf.ln_eps, H, h16, st));
+                HIPTRY(launch_ln_res_rows(t32, xst, defer ? m->xst1.as<float2>() : xst, pg, pb, o16, rows, L.g1, L.be1,
+                                          cf.ln_eps, H, h16, !defer, st));
             } else {
                 ep = resln_ep(L.bo, pg, pb);
                 if (int r = gemm(m, st, RS_K_OPROJ, EPI_RESLN_F32, ctx, L.wo, rows, H, kx * H, ep, H)) return r;
@@ -340,14 +362,26 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
             }
             ep = gelu_ep(L.b1, inter);
             if (int r = gemm(m, st, RS_K_FFN1, EPI_GELU_F16, h16, L.w1, rows, F, kx * H, ep, F)) return r;
-            if (kx == 1 && ffn2_f16()) {
+            if (dmode == 2) {
+                // BertOutput as a persistent fp16-output GEMM into the (free) ctx buffer; both
+                // residual blocks of the layer are closed by one ln_res_rows pass
+                ep = EpiArgs{}; ep.bias = L.b2; ep.out = ctx; ep.ldc = H;
+                if (int r = gemm(m, st, RS_K_FFN2, EPI_BIAS_F16, inter, L.w2, rows, H, F, ep, H)) return r;
+                ProfScope ps(m, st, RS_K_OTHER, 0);
+                HIPTRY(launch_ln_res_rows(t32, xst, xst, pg, pb, o16, rows, L.g2, L.be2, cf.ln_eps, H, h16, true, st,
+                                          m->xst1.as<float2>(), L.g1, L.be1, ctx));
+            } else if (kx == 1 && ffn2_f16()) {
                 // same split for BertOutput: fp16-output GEMM into the (free) ctx buffer
                 ep = EpiArgs{}; ep.bias = L.b2; ep.out = ctx; ep.ldc = H;
                 if (int r = gemm(m, st, RS_K_FFN2, EPI_BIAS_F16, inter, L.w2, rows, H, F, ep, H)) return r;
                 ProfScope ps(m, st, RS_K_OTHER, 0);
-                HIPTRY(launch_ln_res_rows(t32, xst, L.g1, L.be1, ctx, rows, L.g2, L.be2, cf.ln_eps, H, h16, st));
+                HIPTRY(launch_ln_res_rows(t32, xst, xst, L.g1, L.be1, ctx, rows, L.g2, L.be2, cf.ln_eps, H, h16, true, st));
             } else {
                 ep = resln_ep(L.b2, L.g1, L.be1);
+                if (defer) {
+                    ep.res_stats = m->xst1.as<float2>();
+                    ep.res_o16 = o16; ep.res_stats0 = xst; ep.res_g0 = pg; ep.res_b0 = pb;
+                }
                 if (int r = gemm(m, st, RS_K_FFN2, EPI_RESLN_F32, inter, L.w2, rows, H, kx * F, ep, H)) return r;
                 ProfScope ps(m, st, RS_K_OTHER, 0);
                 HIPTRY(launch_ln_rows(t32, rows, L.g2, L.be2, cf.ln_eps, H, nullptr, xst, h16, kx, st));
@@ -818,7 +852,7 @@ void rs_model_destroy(rs_model* m) {
     (void)hipSetDevice(m->device);
     (void)hipDeviceSynchronize();
     for (void* p : m->allocs) (void)hipFree(p);
-    for (DevBuf* b : {&m->xst, &m->h16, &m->t32, &m->qkv, &m->ctx, &m->inter, &m->ctxq, &m->resq,
+    for (DevBuf* b : {&m->xst, &m->xst1, &m->h16, &m->t32, &m->qkv, &m->ctx, &m->inter, &m->ctxq, &m->resq,
                       &m->tq32, &m->hq32, &m->hq16, &m->interq, &m->lab, &m->llog, &m->part,
                       &m->rowlp_tmp, &m->meta, &m->hypoff, &m->emb, &m->plan})
         b->release();

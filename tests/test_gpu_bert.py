@@ -213,11 +213,14 @@ def test_layer0_dedup_is_exact(w_tiny, w_base, max_rows, monkeypatch):
         assert np.array_equal(a, b), np.abs(a - b).max()
 
 
-@pytest.mark.parametrize("env", [{"RS_OPROJ": "resln"}, {"RS_FFN2": "f16"}])
-def test_residual_paths_golden(pll_base, golden_dir, env, monkeypatch):
+@pytest.mark.parametrize("env,same", [({"RS_OPROJ": "resln"}, False), ({"RS_FFN2": "f16"}, True),
+                                      ({"RS_LNRES_DEFER": "0"}, False), ({"RS_LNRES_DEFER": "1"}, False)])
+def test_residual_paths_golden(pll_base, golden_dir, env, same, monkeypatch):
     """The residual-block variants against the F1 fixture: O projection with the residual +
     LayerNorm rebuilt in the GEMM accumulators (RS_OPROJ=resln; default: fp16-output GEMM +
-    ln_res_rows), and FFN2 split the same way as the O projection (RS_FFN2=f16)."""
+    ln_res_rows), FFN2 split the same way as the O projection (RS_FFN2=f16), and the
+    post-attention stream written back (RS_LNRES_DEFER=0) or rebuilt in the BertOutput GEMM's
+    accumulators (=1) instead of the default single two-block ln_res_rows pass (=2)."""
     g = _load(golden_dir, "pll_base.npz")
     base = pll_base.score_nbest(g["tokens"], g["hyp_off"]).cpu().numpy()
     for k, v in env.items():
@@ -227,4 +230,10 @@ def test_residual_paths_golden(pll_base, golden_dir, env, monkeypatch):
     assert rel_err(pll, g["pll"]).max() < REL
     e = rel_err(rows.cpu().numpy(), g["row_lp"])
     assert e.max() < ROW_REL_FP16 and np.percentile(e, 99) < REL
-    assert not np.array_equal(pll, base)          # the variant really ran a different path
+    if same:
+        # RS_FFN2=f16 stores the post-attention stream x in fp32 and forms LN(x) + o2 in a
+        # second pass; the default forms the same expression from (x32, o1) in one pass:
+        # bit-identical by construction
+        assert np.array_equal(pll, base)
+    else:
+        assert not np.array_equal(pll, base)      # the variant really ran a different path
