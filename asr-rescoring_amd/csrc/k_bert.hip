@@ -1228,3 +1228,49 @@ extern "C" int rs_debug_attention(int kind, const void* qkv, const int* len, con
         hipLaunchKernelGGL(attn_memskel_kernel, dim3(n_seq, heads / 4), dim3(256), 0, st, (const f16*)qkv, sm, H, (f16*)ctx, 4);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+namespace {
+// memory skeleton of the two-block ln_res_rows pass: the same loads and stores per row
+// (x32 fp32, two fp16 rows, stats; x32 + fp16 image written), no arithmetic beyond a sum
+__global__ void __launch_bounds__(256)
+lnres_memskel_kernel(float* __restrict__ x32, const f16* __restrict__ o1, const f16* __restrict__ o2, int rows,
+                     f16* __restrict__ y16) {
+    constexpr int H = 768;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+#pragma unroll
+    for (int v = 0; v < 3; ++v) {
+        const int c = v * 256 + lane * 4;
+        float4 r = *(const float4*)(x32 + (size_t)row * H + c);
+        const half4 a = *(const half4*)(o1 + (size_t)row * H + c);
+        const half4 b = *(const half4*)(o2 + (size_t)row * H + c);
+        r = make_float4(r.x + (float)a[0] + (float)b[0], r.y + (float)a[1] + (float)b[1], r.z + (float)a[2] + (float)b[2],
+                        r.w + (float)a[3] + (float)b[3]);
+        *(float4*)(x32 + (size_t)row * H + c) = r;
+        *(half4*)(y16 + (size_t)row * H + c) = half4{(f16)r.x, (f16)r.y, (f16)r.z, (f16)r.w};
+    }
+}
+}  // namespace
+
+// Timing/diagnostic entry (not part of the scoring path): one LayerNorm-family launch over
+// `rows` rows of H = 768.  kind 0 ln_rows, 1 ln_res_rows (x written back), 2 ln_res_rows
+// (deferred: stats + image only), 3 two-block ln_res_rows, 4 memory skeleton of kind 3.
+extern "C" int rs_debug_ln(int kind, int rows, float* x32, float2* stats, float2* stats1, const void* o1,
+                           const void* o2, const float* g, const float* b, void* y16, void* stream) {
+    hipStream_t st = (hipStream_t)stream;
+    const int H = 768;
+    hipError_t e = hipSuccess;
+    if (kind == 0) e = launch_ln_rows(x32, rows, g, b, 1e-12f, H, nullptr, stats, (f16*)y16, 1, st);
+    else if (kind == 1) e = launch_ln_res_rows(x32, stats, stats, g, b, (const f16*)o1, rows, g, b, 1e-12f, H, (f16*)y16, true, st);
+    else if (kind == 2) e = launch_ln_res_rows(x32, stats, stats1, g, b, (const f16*)o1, rows, g, b, 1e-12f, H, (f16*)y16, false, st);
+    else if (kind == 3)
+        e = launch_ln_res_rows(x32, stats, stats, g, b, (const f16*)o1, rows, g, b, 1e-12f, H, (f16*)y16, true, st, stats1,
+                               g, b, (const f16*)o2);
+    else {
+        hipLaunchKernelGGL(lnres_memskel_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, x32, (const f16*)o1,
+                           (const f16*)o2, rows, (f16*)y16);
+        e = hipGetLastError();
+    }
+    return e == hipSuccess ? 0 : -2;
+}

@@ -862,6 +862,45 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
         f16* slab = (f16*)(smem + STAGE) + wave * 32 * LDH;
         const int rr0 = lane >> 3, cc = (lane & 7) * 8;
         uint4 ov[WTM / 32][4];
+        if constexpr (MS == 32 && !(VAR & 32768)) {
+            // 32x32x16 accumulators: v_permlane32_swap packs 8 consecutive columns per lane
+            // (lanes 0-31 the low, 32-63 the high 8 of each 16-column pair), stored as one
+            // ds_write_b128 into 128-B slab rows with the 16-B chunk XOR-swizzled by (row & 7):
+            // the 8-lane write groups (8 rows, one chunk) and the 16-lane read groups (two rows,
+            // all chunks) are both conflict-free (the padded layout below: 2-way on both)
+            static_assert(WTN == 64, "slab rows of 8 chunks");
+            char* slb = smem + STAGE + wave * 32 * 128;
+#pragma unroll
+            for (int i32 = 0; i32 < WTM / 32; ++i32) {
+#pragma unroll
+                for (int j = 0; j < TN; ++j)
+#pragma unroll
+                    for (int gp = 0; gp < 2; ++gp) {
+                        float x[8];
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) x[e] = acc[i32][j][8 * gp + e];
+                        if constexpr (EPI == EPI_GELU_F16) {
+#pragma unroll
+                            for (int e = 0; e < 8; e += 2) {
+                                const f32x2 gv = gelu2((f32x2){x[e], x[e + 1]});
+                                x[e] = gv.x;
+                                x[e + 1] = gv.y;
+                            }
+                        }
+                        half8 h;
+#pragma unroll
+                        for (int e = 0; e < 8; ++e) h[e] = (f16)x[e];
+                        const uint4 hv = __builtin_bit_cast(uint4, h);   // .xy group 2gp, .zw group 2gp+1
+                        const auto s0 = __builtin_amdgcn_permlane32_swap(hv.x, hv.z, false, false);
+                        const auto s1 = __builtin_amdgcn_permlane32_swap(hv.y, hv.w, false, false);
+                        const int c = 4 * j + 2 * gp + fh;               // 16-B chunk of the row
+                        *(uint4*)(slb + frow * 128 + ((c ^ (frow & 7)) << 4)) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+                    }
+#pragma unroll
+                for (int it = 0; it < 4; ++it)
+                    ov[i32][it] = *(const uint4*)(slb + (it * 8 + rr0) * 128 + (((lane & 7) ^ rr0) << 4));
+            }
+        } else
 #pragma unroll
         for (int i32 = 0; i32 < WTM / 32; ++i32) {     // 32-row slices of the wave tile
 #pragma unroll
@@ -1093,6 +1132,11 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         default: return -1;                                                                           \
     }
     if (M % 256 || N % 256 || K % 64) return -1;
+    if (cfg == 13 || cfg == 14) {  // persistent, padded (pre-swizzle) epilogue slab: 13 bias, 14 GELU
+        e = cfg == 13 ? launch_persist<EPI_BIAS_F16, 32768>(a, w, M, N, K, ep, st)
+                      : launch_persist<EPI_GELU_F16, 32768>(a, w, M, N, K, ep, st);
+        return e == hipSuccess ? 0 : -2;
+    }
     if (cfg >= 9 && cfg <= 12) {   // persistent fp16-output kernel (11/12: GELU; 10/12: 16x16x32)
         e = cfg == 9 ? launch_persist<EPI_BIAS_F16>(a, w, M, N, K, ep, st)
           : cfg == 10 ? (dbg ? launch_persist<EPI_BIAS_F16, 8192 | 16384>(a, w, M, N, K, ep, st)
@@ -1138,6 +1182,7 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 8384: RS_DBG16(8384); break;
         case 8323: RS_DBG16(8323); break;
         case 8322: RS_DBG16(8322); break;
+        case 8321: RS_DBG16(8321); break;
         default: RS_DBG(3); break;
     }
 #undef RS_DBG
