@@ -106,7 +106,8 @@ __device__ __forceinline__ float wave_max(float v) {
 
 // ---- launchers (defined in k_gemm.hip / k_bert.hip / k_rerank.hip) ---------------------
 // tag != 0: the same kernel instantiated under a distinct VAR tag bit (kernel name only), so
-// rocprofv3 separates the O-projection launches from the QKV launches of the same epilogue
+// rocprofv3 separates the O-projection (tag 1) and BertOutput (tag 2) launches from the QKV
+// launches of the same epilogue
 hipError_t launch_gemm(int epi, const f16* A, const f16* W, int M_pad, int N_pad, int K,
                        const EpiArgs& ep, hipStream_t st, int tag = 0);
 int gemm_row_align();   // M padding granularity required by launch_gemm

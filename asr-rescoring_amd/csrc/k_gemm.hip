@@ -1050,8 +1050,9 @@ hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
     if constexpr (EPI == EPI_BIAS_F16 || EPI == EPI_GELU_F16) {
         if (persist && cfg == 0 && (EPI == EPI_BIAS_F16 || ep.kx == 1))
             return (ms_p == 16 || (ms_p == 0 && K >= 2048)) ? launch_persist<EPI, 8192>(A, W, M_pad, N_pad, K, ep, st)
-                 : tag ? launch_persist<EPI, 65536>(A, W, M_pad, N_pad, K, ep, st)   // VAR 65536: name tag only
-                       : launch_persist<EPI>(A, W, M_pad, N_pad, K, ep, st);
+                 : tag == 1 ? launch_persist<EPI, 65536>(A, W, M_pad, N_pad, K, ep, st)    // name tags only:
+                 : tag == 2 ? launch_persist<EPI, 131072>(A, W, M_pad, N_pad, K, ep, st)   // O-proj / FFN2
+                            : launch_persist<EPI>(A, W, M_pad, N_pad, K, ep, st);
     }
     if ((nt_mask >> EPI) & 1u) {
         if constexpr (EPI != EPI_LSE) {

@@ -235,7 +235,7 @@ int gemm(rs_model* m, hipStream_t st, int kind, int epi, const f16* A, const f16
     const int M_pad = (m_valid + al - 1) / al * al;
     ep.m_valid = m_valid;
     ProfScope ps(m, st, kind, 2.0 * m_valid * (double)n_flop_cols * K);
-    HIPTRY(launch_gemm(epi, A, W, M_pad, N_pad, K, ep, st, kind == RS_K_OPROJ));
+    HIPTRY(launch_gemm(epi, A, W, M_pad, N_pad, K, ep, st, kind == RS_K_OPROJ ? 1 : kind == RS_K_FFN2 ? 2 : 0));
     return RS_OK;
 }
 

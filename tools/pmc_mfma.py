@@ -21,6 +21,8 @@ def kname(n):
     m = re.search(r"gemm_persist_kernelILi(\d+)ELi(\d+)E", n)
     if m and int(m.group(2)) & 65536:
         return "gemm_persist:oproj"
+    if m and int(m.group(2)) & 131072:
+        return "gemm_persist:ffn2"
     if m:
         return "gemm_persist:" + EPI.get(int(m.group(1)), m.group(1))
     m = re.search(r"gemm_f16_kernelILi\d+ELi\d+ELi\d+ELi\d+ELi\d+ELi\d+ELi(\d+)E", n)

@@ -21,6 +21,7 @@ import sys
 EPI_N = {0: ("qkv", 2304), 1: ("ffn1", 3072), 3: ("res_f32", 768), 6: ("ffn2", 768),
          2: ("head_transform", 768), 4: ("decoder", 21248)}
 OPROJ_TAG = 65536          # VAR bit of the O-projection instance of the persistent kernel
+FFN2_TAG = 131072          # VAR bit of the BertOutput instance (fp16-output FFN2, RS_LNRES_DEFER=2)
 RE_GEMM = re.compile(r"gemm_f16_kernelILi(\d+)ELi(\d+)ELi\d+ELi\d+ELi\d+ELi\d+ELi(\d+)E")
 RE_PERSIST = re.compile(r"gemm_persist_kernelILi(\d+)ELi(\d+)E")
 
@@ -46,7 +47,8 @@ def main():
                 blocks = int(r["Grid_Size"]) // int(r["Workgroup_Size"])
                 rows = blocks // (n // bn) * bm if n else None
             elif mp:
-                name, n = ("oproj", 768) if int(mp.group(2)) & OPROJ_TAG else \
+                tagv = int(mp.group(2))
+                name, n = ("oproj", 768) if tagv & OPROJ_TAG else ("ffn2", 768) if tagv & FFN2_TAG else \
                     EPI_N.get(int(mp.group(1)), (f"epi{mp.group(1)}", None))
                 rows = None                      # filled from the WRITE pass below
             else:
