@@ -973,8 +973,10 @@ hipError_t launch_persist(const f16* A, const f16* W, int M_pad, int N_pad, int 
     const int grid = n_tiles <= cus ? n_tiles : cus;
     // 8 row panels per group (QKV -3 % vs 4, end to end; profiles/r1_ab_session2.txt)
     static const int gm_env = getenv("RS_GEMM_GROUP_M_P") ? atoi(getenv("RS_GEMM_GROUP_M_P")) : 0;
+    // BertOutput (VAR tag 131072, K = 3072): RS_GEMM_GROUP_M_FFN2 row panels per group
+    static const int gm_ffn2 = getenv("RS_GEMM_GROUP_M_FFN2") ? atoi(getenv("RS_GEMM_GROUP_M_FFN2")) : 0;
     EpiArgs e2 = ep;
-    e2.group_m = gm_env > 0 ? gm_env : 8;
+    e2.group_m = (VAR & 131072) && gm_ffn2 > 0 ? gm_ffn2 : gm_env > 0 ? gm_env : 8;
     hipLaunchKernelGGL((gemm_persist_kernel<EPI, VAR>), dim3(grid), dim3(512), smem, st, A, W, K, ntn, n_tiles, e2);
     return hipGetLastError();
 }
