@@ -176,6 +176,35 @@ def test_edge_lengths(pll_tiny, w_tiny):
     assert rel_err(got, ref).max() < REL
 
 
+def test_max_position_length(pll_tiny, w_tiny):
+    """T = max_position_embeddings (512, L = 510): every position embedding, 8 key blocks of
+    online-softmax attention, the scored-row attention over 512 keys — PLL and RescoreBert vs the
+    oracle; T = 513 is rejected like the reference's position-embedding lookup would fail."""
+    from asr_rescoring_amd._lib import RescoreError
+    from asr_rescoring_amd.scorer import RescoreBertScorer
+    from oracle.bert_ref import TorchBert, cls_reference_pattern, pll_reference_pattern
+    rng = np.random.default_rng(5)
+    L = BERT_TINY.max_pos - 2
+    nb = D.from_lists([[rng.integers(106, BERT_TINY.vocab, size=L).tolist(),
+                        rng.integers(106, BERT_TINY.vocab, size=7).tolist()]], [[0.0, 0.0]])
+    tb = TorchBert(w_tiny, BERT_TINY)
+    got = pll_tiny.score(nb)
+    _, ref = pll_reference_pattern(tb, nb.tokens, nb.hyp_off, batch_size=64, full_head=False)
+    assert rel_err(got, ref).max() < REL
+    cs = RescoreBertScorer(w_tiny, BERT_TINY, device=0, max_rows=2048)
+    try:
+        c = cs.score_nbest(nb.tokens, nb.hyp_off).cpu().numpy()
+        cref = cls_reference_pattern(tb, nb.tokens, nb.hyp_off)
+        assert (np.abs(c - cref) <= np.maximum(REL * np.abs(cref), 1e-4)).all(), np.abs(c - cref).max()
+        long_nb = D.from_lists([[rng.integers(106, BERT_TINY.vocab, size=L + 1).tolist()]], [[0.0]])
+        with pytest.raises(RescoreError):
+            cs.score_nbest(long_nb.tokens, long_nb.hyp_off)
+    finally:
+        cs.close()
+    with pytest.raises(RescoreError):
+        pll_tiny.score_nbest(long_nb.tokens, long_nb.hyp_off)
+
+
 def test_empty_and_bad_input(pll_tiny):
     from asr_rescoring_amd._lib import RescoreError
     out = pll_tiny.score_nbest(np.zeros(0, np.int32), np.zeros(1, np.int32))
