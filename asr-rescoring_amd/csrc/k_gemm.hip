@@ -21,6 +21,7 @@
 #include "common.h"
 #include <stdlib.h>
 #include <string.h>
+#include <type_traits>
 
 namespace {
 
@@ -780,14 +781,18 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
                     acc[i][j][4 * g + 2] = bz[j * NQ + g].z;
                     acc[i][j][4 * g + 3] = bz[j * NQ + g].w;
                 }
-        // ---- K loop: stage kt landed (this tile's stage 0 was waited with the bias)
+        // ---- K loop: stage kt landed (this tile's stage 0 was waited with the bias).  STAG:
+        // this wave runs the staggered schedule (VAR 524288, younger half); one loop body per
+        // schedule, chosen once per tile, so each is register-allocated on its own.
+        auto kloop = [&](auto stag_tag) {
+        constexpr bool STAG = decltype(stag_tag)::value;
+        half8 af0[TM], bf0[TN], af1[TM], bf1[TN];   // (staggered waves carry af1/bf1 across steps)
         for (int kt = 0; kt < nk; ++kt) {
             if (kt > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             asm volatile("s_barrier" ::: "memory");
             if (kt + 1 < nk) stage((kt + 1) & 1, (kt + 1) * BK);
             __builtin_amdgcn_sched_barrier(0);
             const char* sb = smem + (kt & 1) * STAGE;
-            half8 af0[TM], bf0[TN], af1[TM], bf1[TN];
             // substep s covers chunks CPS*s .. CPS*s + CPS-1: one XOR of the per-lane base
             auto load_frags = [&](int s, half8 (&af)[TM], half8 (&bf)[TN]) {
                 const int xa = offA ^ ((CPS * s) << 4), xb = offB ^ ((CPS * s) << 4);
@@ -838,6 +843,49 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
                 __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
                 continue;
             }
+            if constexpr (NSUB == 4 && STAG) {
+                {
+                    // Stagger (MI355X_MICROARCH 'Two waves per SIMD' item 9): the younger wave
+                    // half runs one substep behind — its last substep's MFMAs (fragments already
+                    // in af1/bf1, read before this K-step's barrier) issue after the barrier,
+                    // beside the next K-step's substep-0 reads, so the two waves of a SIMD do not
+                    // reach their MFMA bursts and LDS read bursts in lockstep.
+                    if (kt > 0) {
+                        mfmas(af1, bf1);
+                        load_frags(0, af0, bf0);
+#pragma unroll
+                        for (int r = 0; r < NR; ++r) {
+                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        }
+                        __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
+                    } else {
+                        load_frags(0, af0, bf0);
+                        __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    load_frags(1, af1, bf1);
+                    mfmas(af0, bf0);
+                    load_frags(2, af0, bf0);
+                    mfmas(af1, bf1);
+                    load_frags(3, af1, bf1);
+                    mfmas(af0, bf0);
+#pragma unroll
+                    for (int q = 0; q < 3; ++q) {
+#pragma unroll
+                        for (int r = 0; r < NR; ++r) {
+                            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+                            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+                        }
+                        __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
+                    }
+                    if (kt + 1 == nk) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        mfmas(af1, bf1);          // the deferred last substep of the tile
+                    }
+                    continue;
+                }
+            }
             load_frags(0, af0, bf0);
             load_frags(1, af1, bf1);
             mfmas(af0, bf0);
@@ -859,6 +907,13 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
                 __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
             }
             __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
+        }
+        };
+        if constexpr (NSUB == 4 && (VAR & 524288) != 0) {
+            if (wave >= NW / 2) kloop(std::true_type{});
+            else kloop(std::false_type{});
+        } else {
+            kloop(std::false_type{});
         }
         // ---- transition: next tile's stage 0 + bias, then this tile's epilogue
         asm volatile("s_barrier" ::: "memory");      // every wave is done reading the ring
@@ -1055,11 +1110,22 @@ hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
     // RS_GEMM_PERSIST=0 disables the persistent kernel (fp16-output epilogues, kx = 1)
     static const int persist = getenv("RS_GEMM_PERSIST") ? atoi(getenv("RS_GEMM_PERSIST")) : 1;
     // RS_GEMM_PRIO (default 1): the persistent kernel's younger wave half runs at s_setprio 1
-    // (+1-3 % per GEMM shape, tools/gemm_bench.py cfg 9/15, 11/16)
+    // (+1-3 % per GEMM shape, tools/gemm_bench.py cfg 9/15, 11/16); RS_GEMM_STAGGER=1 (default):
+    // that half also runs one MFMA substep behind (cfg 17-20; +1.5 % end to end over the
+    // priority alone), 2: stagger without the priority (no gain), 0: priority only
     static const int prio = getenv("RS_GEMM_PRIO") ? atoi(getenv("RS_GEMM_PRIO")) : 1;
+    static const int stag = getenv("RS_GEMM_STAGGER") ? atoi(getenv("RS_GEMM_STAGGER")) : (prio ? 1 : 0);
     if constexpr (EPI == EPI_BIAS_F16 || EPI == EPI_GELU_F16) {
         if (persist && cfg == 0 && (EPI == EPI_BIAS_F16 || ep.kx == 1)) {
             if (ms_p == 16 || (ms_p == 0 && K >= 2048)) return launch_persist<EPI, 8192>(A, W, M_pad, N_pad, K, ep, st);
+            if (stag == 1)
+                return tag == 1 ? launch_persist<EPI, 65536 | 786432>(A, W, M_pad, N_pad, K, ep, st)
+                     : tag == 2 ? launch_persist<EPI, 131072 | 786432>(A, W, M_pad, N_pad, K, ep, st)
+                                : launch_persist<EPI, 786432>(A, W, M_pad, N_pad, K, ep, st);
+            if (stag == 2)
+                return tag == 1 ? launch_persist<EPI, 65536 | 524288>(A, W, M_pad, N_pad, K, ep, st)
+                     : tag == 2 ? launch_persist<EPI, 131072 | 524288>(A, W, M_pad, N_pad, K, ep, st)
+                                : launch_persist<EPI, 524288>(A, W, M_pad, N_pad, K, ep, st);
             if (prio)
                 return tag == 1 ? launch_persist<EPI, 65536 | 262144>(A, W, M_pad, N_pad, K, ep, st)
                      : tag == 2 ? launch_persist<EPI, 131072 | 262144>(A, W, M_pad, N_pad, K, ep, st)
@@ -1148,6 +1214,16 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         default: return -1;                                                                           \
     }
     if (M % 256 || N % 256 || K % 64) return -1;
+    if (cfg == 17 || cfg == 18) {  // persistent, prio + staggered younger half: 17 bias, 18 GELU
+        e = cfg == 17 ? launch_persist<EPI_BIAS_F16, 262144 | 524288>(a, w, M, N, K, ep, st)
+                      : launch_persist<EPI_GELU_F16, 262144 | 524288>(a, w, M, N, K, ep, st);
+        return e == hipSuccess ? 0 : -2;
+    }
+    if (cfg == 19 || cfg == 20) {  // persistent, staggered younger half without prio: 19 bias, 20 GELU
+        e = cfg == 19 ? launch_persist<EPI_BIAS_F16, 524288>(a, w, M, N, K, ep, st)
+                      : launch_persist<EPI_GELU_F16, 524288>(a, w, M, N, K, ep, st);
+        return e == hipSuccess ? 0 : -2;
+    }
     if (cfg == 15 || cfg == 16) {  // persistent, younger wave half at s_setprio 1: 15 bias, 16 GELU
         e = cfg == 15 ? launch_persist<EPI_BIAS_F16, 262144>(a, w, M, N, K, ep, st)
                       : launch_persist<EPI_GELU_F16, 262144>(a, w, M, N, K, ep, st);
