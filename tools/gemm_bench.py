@@ -44,7 +44,7 @@ def main():
             if ref is None:
                 ref = (A[:4096].float() @ W.float().t() + b).half()
             for dbg in dbgs:
-                if cfg in (11, 12, 14, 16, 18, 20):      # GELU epilogue: compare against gelu(ref)
+                if cfg in (11, 12, 14, 16, 18, 20, 22):      # GELU epilogue: compare against gelu(ref)
                     _time(fn, cfg, dbg, A, W, b, out, M, N, K, reps=1)
                     gl = torch.nn.functional.gelu(ref.float()).half()
                     assert (out[:4096].float() - gl.float()).abs().max().item() < 0.05 * K ** 0.5
