@@ -129,6 +129,9 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
+    if constexpr ((VAR & 262144) != 0) {      // younger wave half at s_setprio 1 (as the persistent kernel)
+        if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    }
 
     // per-lane global source pointers of the pieces this wave stages (k0 = 0)
     const f16* src[PPW];
@@ -924,6 +927,22 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
         // slabs have their own LDS, and with an even K-step count the next tile's stage 0
         // (buffer 0) was last read before the final K-step's barrier, so no wave waits here
         if (!((VAR & 1048576) && MS == 32) || (nk & 1)) asm volatile("s_barrier" ::: "memory");
+        // VAR 2097152 (with the private slabs): the next tile's stage 0 and bias are issued
+        // before this tile's epilogue math instead of after it (more time to land)
+        const int cm0 = m0, cn0 = n0;
+        bool more = false;
+        constexpr bool EARLY = (VAR & 2097152) && (VAR & 1048576) && MS == 32;
+        auto issue_next = [&]() {
+            t += gridDim.x;
+            more = t < n_tiles;
+            if (more) {
+                tile_of(t, m0, n0);
+                set_src(m0, n0);
+                stage(0, 0);     // buffer 0: free (barrier above, or last read before the final K-step's)
+                load_bias(n0);
+            }
+        };
+        if constexpr (EARLY) issue_next();
         // epilogue part 1: bias/GELU, fp16, transposed through the wave's slab (buffer 1) into
         // whole-row registers; no LDS access follows the next tile's DMA issue below
         f16* slab = (f16*)(smem + STAGE) + wave * 32 * LDH;
@@ -990,15 +1009,7 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
             for (int it = 0; it < 4; ++it) ov[i32][it] = *(const uint4*)(slab + (it * 8 + rr0) * LDH + cc);
         }
         // part 2: the next tile's stage 0 (buffer 0) and bias
-        const int cm0 = m0, cn0 = n0;
-        t += gridDim.x;
-        const bool more = t < n_tiles;
-        if (more) {
-            tile_of(t, m0, n0);
-            set_src(m0, n0);
-            stage(0, 0);
-            load_bias(n0);
-        }
+        if constexpr (!EARLY) issue_next();
         // part 3: this tile's stores (whole 128-B row segments, non-temporal)
         f16* obase = (f16*)ep.out + (size_t)(cm0 + wm * WTM + rr0) * ep.ldc + cn0 + wn * WTN + cc;
 #pragma unroll
@@ -1226,6 +1237,11 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         default: return -1;                                                                           \
     }
     if (M % 256 || N % 256 || K % 64) return -1;
+    if (cfg == 23 || cfg == 24) {  // + next tile's DMA issued before the epilogue math: 23 bias, 24 GELU
+        e = cfg == 23 ? launch_persist<EPI_BIAS_F16, 786432 | 1048576 | 2097152>(a, w, M, N, K, ep, st)
+                      : launch_persist<EPI_GELU_F16, 786432 | 1048576 | 2097152>(a, w, M, N, K, ep, st);
+        return e == hipSuccess ? 0 : -2;
+    }
     if (cfg == 21 || cfg == 22) {  // + private epilogue slabs, no epilogue barrier: 21 bias, 22 GELU
         e = cfg == 21 ? launch_persist<EPI_BIAS_F16, 786432 | 1048576>(a, w, M, N, K, ep, st)
                       : launch_persist<EPI_GELU_F16, 786432 | 1048576>(a, w, M, N, K, ep, st);
@@ -1297,6 +1313,7 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         case 8323: RS_DBG16(8323); break;
         case 8322: RS_DBG16(8322); break;
         case 8321: RS_DBG16(8321); break;
+        case 270464: RS_DBG16(270464); break;     // 8320 + younger half at s_setprio 1
         default: RS_DBG(3); break;
     }
 #undef RS_DBG
