@@ -689,6 +689,10 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
     constexpr int NSTORE = (WTM / 32) * 4;        // 16-B stores per wave per tile
     constexpr int NSUB = BK / KPS, NR = TM + TN, NM = TM * TN;
     static_assert(EPI == EPI_BIAS_F16 || EPI == EPI_GELU_F16, "fp16-output epilogues only");
+    // VAR 4194304: fp16x3 precision mode (kx = 3) — the GELU output is written as the
+    // three-part operand image [hi | hi/64 | lo·64] of the next GEMM (ep.nlog columns apart)
+    constexpr bool X3 = (VAR & 4194304) != 0;
+    static_assert(!X3 || (EPI == EPI_GELU_F16 && MS == 32 && !(VAR & 32768)), "x3 image: GELU, 32x32 slab path");
     static_assert(NW * 32 * LDH * 2 <= STAGE, "epilogue slab fits in one buffer");
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
@@ -948,6 +952,7 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
         f16* slab = (f16*)(smem + STAGE) + wave * 32 * LDH;
         const int rr0 = lane >> 3, cc = (lane & 7) * 8;
         uint4 ov[WTM / 32][4];
+        f16* obase = (f16*)ep.out + (size_t)(cm0 + wm * WTM + rr0) * ep.ldc + cn0 + wn * WTN + cc;
         if constexpr (MS == 32 && !(VAR & 32768)) {
             // 32x32x16 accumulators: v_permlane32_swap packs 8 consecutive columns per lane
             // (lanes 0-31 the low, 32-63 the high 8 of each 16-column pair), stored as one
@@ -956,6 +961,24 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
             // all chunks) are both conflict-free (the padded layout below: 2-way on both)
             static_assert(WTN == 64, "slab rows of 8 chunks");
             char* slb = smem + ((VAR & 1048576) ? 2 * STAGE : STAGE) + wave * 32 * 128;
+            if constexpr (X3) {
+                // fp16x3 image [hi | hi/64 | lo·64] (common.h put_split): GELU once, in place
+#pragma unroll
+                for (int i32 = 0; i32 < WTM / 32; ++i32)
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+#pragma unroll
+                        for (int e = 0; e < 16; e += 2) {
+                            const f32x2 gv = gelu2((f32x2){acc[i32][j][e], acc[i32][j][e + 1]});
+                            acc[i32][j][e] = gv.x;
+                            acc[i32][j][e + 1] = gv.y;
+                        }
+            }
+            // image img (0: hi, 1: hi/64, 2: lo·64) of the tile through the slab into ov;
+            // STORE_NOW: each 32-row slice is stored as soon as it is read back (images 0/1:
+            // only 16 registers of ov live beside the 128 accumulators)
+            auto build_img = [&](int img, auto store_now) {
+                constexpr bool STORE_NOW = decltype(store_now)::value;
 #pragma unroll
             for (int i32 = 0; i32 < WTM / 32; ++i32) {
 #pragma unroll
@@ -965,7 +988,7 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
                         float x[8];
 #pragma unroll
                         for (int e = 0; e < 8; ++e) x[e] = acc[i32][j][8 * gp + e];
-                        if constexpr (EPI == EPI_GELU_F16) {
+                        if constexpr (EPI == EPI_GELU_F16 && !X3) {
 #pragma unroll
                             for (int e = 0; e < 8; e += 2) {
                                 const f32x2 gv = gelu2((f32x2){x[e], x[e + 1]});
@@ -976,6 +999,15 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
                         half8 h;
 #pragma unroll
                         for (int e = 0; e < 8; ++e) h[e] = (f16)x[e];
+                        if constexpr (X3) {
+                            if (img == 1) {
+#pragma unroll
+                                for (int e = 0; e < 8; ++e) h[e] = x3_mid(h[e]);
+                            } else if (img == 2) {
+#pragma unroll
+                                for (int e = 0; e < 8; ++e) h[e] = x3_lo(x[e], h[e]);
+                            }
+                        }
                         const uint4 hv = __builtin_bit_cast(uint4, h);   // .xy group 2gp, .zw group 2gp+1
                         const auto s0 = __builtin_amdgcn_permlane32_swap(hv.x, hv.z, false, false);
                         const auto s1 = __builtin_amdgcn_permlane32_swap(hv.y, hv.w, false, false);
@@ -984,7 +1016,24 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
                     }
 #pragma unroll
                 for (int it = 0; it < 4; ++it)
-                    ov[i32][it] = *(const uint4*)(slb + (it * 8 + rr0) * 128 + (((lane & 7) ^ rr0) << 4));
+                    ov[STORE_NOW ? 0 : i32][it] = *(const uint4*)(slb + (it * 8 + rr0) * 128 + (((lane & 7) ^ rr0) << 4));
+                if constexpr (STORE_NOW) {
+#pragma unroll
+                    for (int it = 0; it < 4; ++it)
+                        st16<64>((uint4*)(obase + img * ep.nlog + (size_t)(i32 * 32 + it * 8) * ep.ldc), ov[0][it]);
+                }
+            }
+            };
+            if constexpr (X3) {
+                // images 0 and 1 are stored before the next tile's DMA issue (the slab is
+                // wave-private: LDS ops of a wave run in order, so the rewrite after the reads
+                // is safe); image 2 takes the overlapped store slot below
+                build_img(0, std::true_type{});
+                build_img(1, std::true_type{});
+                build_img(2, std::false_type{});
+                obase += 2 * ep.nlog;
+            } else {
+                build_img(0, std::false_type{});
             }
         } else
 #pragma unroll
@@ -1011,7 +1060,6 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
         // part 2: the next tile's stage 0 (buffer 0) and bias
         if constexpr (!EARLY) issue_next();
         // part 3: this tile's stores (whole 128-B row segments, non-temporal)
-        f16* obase = (f16*)ep.out + (size_t)(cm0 + wm * WTM + rr0) * ep.ldc + cn0 + wn * WTN + cc;
 #pragma unroll
         for (int i = 0; i < WTM / 32; ++i)
 #pragma unroll
@@ -1143,6 +1191,13 @@ hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
     // priority alone), 2: stagger without the priority (no gain), 0: priority only
     static const int prio = getenv("RS_GEMM_PRIO") ? atoi(getenv("RS_GEMM_PRIO")) : 1;
     static const int stag = getenv("RS_GEMM_STAGGER") ? atoi(getenv("RS_GEMM_STAGGER")) : (prio ? 1 : 0);
+    // RS_GEMM_PERSIST_X3 (default 1): BertIntermediate of the fp16x3 mode on the persistent
+    // kernel too (GELU output written as the three-part operand image)
+    static const int persist_x3 = getenv("RS_GEMM_PERSIST_X3") ? atoi(getenv("RS_GEMM_PERSIST_X3")) : 1;
+    if constexpr (EPI == EPI_GELU_F16) {
+        if (persist && persist_x3 && cfg == 0 && ep.kx == 3)
+            return launch_persist<EPI, 786432 | 4194304>(A, W, M_pad, N_pad, K, ep, st);
+    }
     if constexpr (EPI == EPI_BIAS_F16 || EPI == EPI_GELU_F16) {
         if (persist && cfg == 0 && (EPI == EPI_BIAS_F16 || ep.kx == 1)) {
             if (ms_p == 16 || (ms_p == 0 && K >= 2048)) return launch_persist<EPI, 8192>(A, W, M_pad, N_pad, K, ep, st);
