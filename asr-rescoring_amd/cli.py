@@ -82,7 +82,7 @@ def mlm_pll(cfg) -> Dict[str, str]:
     rows (``*_data_path``: do_job output) or raw ``*_hyps_text_path`` JSON."""
     from .scorer import PLLScorer
     scorer = PLLScorer(_weights(cfg, "mlm"), BERT_BASE, device=_dev(cfg), max_rows=get(cfg, "max_rows", 65536),
-                       precision=get(cfg, "precision", "fp16"))
+                       precision=get(cfg, "precision", "fp16x3"))
     out_files = {}
     for split in ("train", "dev", "test"):
         rows_path = get(cfg, f"{split}_data_path")
@@ -290,7 +290,7 @@ def rmbr(cfg) -> Dict[str, float]:
         from . import bertscore as BS
         scorer = BS.BertScorer(_weights(cfg, "mlm"), BERT_BASE, num_layers=get(cfg, "bertscore_layers", 8),
                                device=_dev(cfg), max_rows=get(cfg, "max_rows", 65536),
-                               precision=get(cfg, "precision", "fp16"))
+                               precision=get(cfg, "precision", "fp16x3"))
         which = str(get(cfg, "bertscore_component", "R")).upper()
 
     def split_nb(prefix):

@@ -23,12 +23,29 @@ from .data import NBest
 from .weights import BertShape, BERT_BASE
 
 
+def _prefix_lengths(attention_mask: torch.Tensor) -> np.ndarray:
+    """Row lengths of a right-padded 0/1 attention mask (``pad_sequence`` output).
+
+    A left-padded, holed or non-binary mask would make the ragged scorers score other
+    tokens than the reference's additive-mask forward, so it is rejected."""
+    am = attention_mask.detach().to("cpu", torch.int64)
+    if am.dim() != 2:
+        raise ValueError("attention_mask must be [B, T]")
+    if not bool(((am == 0) | (am == 1)).all()):
+        raise ValueError("attention_mask must hold only 0 and 1")
+    lens = am.sum(-1)
+    pos = torch.arange(am.shape[1])[None, :]
+    if not bool((am.bool() == (pos < lens[:, None])).all()):
+        raise ValueError("attention_mask must be prefix ones (right padding)")
+    return lens.numpy().astype(np.int32)
+
+
 class BertEngine:
     """One ``rs_model`` handle: packed weights + workspace on one GPU."""
 
     def __init__(self, weights: Dict[str, np.ndarray], shape: BertShape = BERT_BASE,
                  heads: int = _lib.RS_HEAD_MLM, device: int | str | torch.device = 0,
-                 max_rows: int = 65536, precision: str = "fp16"):
+                 max_rows: int = 65536, precision: str = "fp16x3"):
         if not torch.cuda.is_available():
             raise RuntimeError("librescore needs a HIP GPU (no CPU fallback)")
         self.lib = _lib.load()
@@ -88,7 +105,9 @@ class PLLScorer(BertEngine):
     """MLM_PLL scorer (BertForMaskedLM head)."""
 
     def __init__(self, weights, shape: BertShape = BERT_BASE, device=0, max_rows: int = 65536,
-                 precision: str = "fp16"):
+                 precision: str = "fp16x3"):
+        # fp16x3 (default): fp32-accurate split-fp16 operands, like the reference's fp32
+        # BertForMaskedLM; "fp16" is an opt-in reduced-precision fast mode
         super().__init__(weights, shape, _lib.RS_HEAD_MLM, device, max_rows, precision)
 
     def score_nbest(self, tokens, hyp_off, return_rows: bool = False):
@@ -113,10 +132,7 @@ class PLLScorer(BertEngine):
         """``token_score`` of MLM_PLL/main.py:101-105 for a padded batch [B, T].
 
         ``attention_mask`` rows must be a prefix of ones (``pad_sequence`` output)."""
-        am = attention_mask.detach().to("cpu", torch.int64)
-        lens = am.sum(-1).numpy().astype(np.int32)
-        if not bool((am.cumsum(-1) == am.sum(-1, keepdim=True)).logical_or(am.bool()).all()):
-            raise ValueError("attention_mask must be prefix ones (right padding)")
+        lens = _prefix_lengths(attention_mask)
         B = input_ids.shape[0]
         mp = np.asarray([int(x) for x in mask_pos], np.int32)
         ids = input_ids.to(self.device)
@@ -189,8 +205,9 @@ class RescoreBertHIP(torch.nn.Module):
         self.engine = RescoreBertScorer(weights, shape, device, max_rows, precision)
 
     def forward(self, input_ids: torch.Tensor, attention_mask: torch.Tensor) -> torch.Tensor:
-        am = attention_mask.detach().to("cpu", torch.int64)
-        lens = am.sum(-1).numpy().astype(np.int32)
+        lens = _prefix_lengths(attention_mask)
+        if (lens == 0).any():
+            raise ValueError("every row needs at least one attended token")
         dev = self.engine.device
         ids = input_ids.to(dev)
         T = ids.shape[1]

@@ -36,6 +36,20 @@ PEAK_FP16_TFLOPS = 2500.0   # MI355X dense FP16/BF16 MFMA (MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0
 
 
+DTYPE = {"fp16x3": "fp16x3-split (fp32-accurate: hi/lo fp16 operand split on fp16 MFMA, fp32 accumulate)",
+         "fp16": "fp16 (reduced precision: fp16 MFMA operands, fp32 accumulate)"}
+
+
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def forward_flops(T: int, s=BERT_BASE) -> float:
     """Canonical algorithmic FLOPs of one MLM_PLL masked forward at length T."""
     H, F, V, nl = s.hidden, s.intermediate, s.vocab, s.layers
@@ -54,6 +68,11 @@ def main():
     ap.add_argument("--max-rows", type=int, default=262144, help="token rows per launch chunk (262144: +0.5 %% over 131072)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0, help="CPU-baseline budget (0 = skip)")
     ap.add_argument("--no-profile", action="store_true")
+    ap.add_argument("--precision", default="fp16x3", choices=("fp16x3", "fp16"),
+                    help="fp16x3 (default): split-fp16 operands, fp32-accurate (the reference computes "
+                         "in fp32); fp16: fp16 operands (reduced precision, reported as a secondary field)")
+    ap.add_argument("--fp16-steps", type=int, default=2,
+                    help="secondary leg: steps of the reduced-precision fp16 mode (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -66,7 +85,8 @@ def main():
 
     from asr_rescoring_amd.scorer import PLLScorer
     weights = make_weights(BERT_BASE, seed=1234)
-    scorer = PLLScorer(weights, BERT_BASE, device=local, max_rows=args.max_rows)
+    scorer = PLLScorer(weights, BERT_BASE, device=local, max_rows=args.max_rows, precision=args.precision)
+    kx = 3 if args.precision == "fp16x3" else 1
 
     nb = D.synthetic_nbest(args.utts, args.nbest, seed=1 + 1000 * rank)
     d_tok = torch.from_numpy(nb.tokens).to(dev)                 # resident in HBM
@@ -127,29 +147,36 @@ def main():
         gemm_kinds = {k: v for k, v in kinds.items() if v[2] > 0}
         dom = max(gemm_kinds, key=lambda k: gemm_kinds[k][0])
         ms, n, fl = gemm_kinds[dom]
+        # fl = MFMA work (2*M*N*K over the kx-wide operand images); algorithmic = fl / kx
         achieved = fl / (ms * 1e-3) / 1e12
+        achieved_alg = achieved / kx
         # HBM(+MALL) bytes per launch from the committed rocprofv3 PMC summary (FETCH_SIZE x2
         # gfx950 correction + WRITE_SIZE, per row), scaled to this run's rows per launch
         traffic, tsrc = None, None
         nk = {"qkv": (2304, 768, "qkv"), "oproj": (768, 768, "oproj"), "ffn1": (3072, 768, "ffn1"),
               "ffn2": (768, 3072, "ffn2")}.get(dom)
-        pmc_files = sorted(f for f in os.listdir(os.path.join(REPO, "profiles")) if f.endswith("_pmc_gemm_traffic.json"))
+        suffix = f"_pmc_gemm_traffic_{args.precision}.json"
+        pmc_files = sorted(f for f in os.listdir(os.path.join(REPO, "profiles")) if f.endswith(suffix))
+        rows_per_launch = fl / kx / max(n, 1) / (2.0 * nk[0] * nk[1]) if nk else None
         if nk and pmc_files:
             pm = json.load(open(os.path.join(REPO, "profiles", pmc_files[-1])))
             e = pm.get(nk[2], {})
             if e.get("fetch_size_bytes_per_row") and e.get("write_size_bytes_per_row"):
-                rows_per_launch = fl / max(n, 1) / (2.0 * nk[0] * nk[1])
                 traffic = (e["fetch_size_bytes_per_row"] + e["write_size_bytes_per_row"]) * rows_per_launch
                 tsrc = f"profiles/{pmc_files[-1]}"
         alg_bytes = None
         if nk:
-            rows_per_launch = fl / max(n, 1) / (2.0 * nk[0] * nk[1])
-            alg_bytes = rows_per_launch * (nk[1] + nk[0]) * 2 + nk[0] * nk[1] * 2
-        roof = {"kernel": f"gemm_f16_{dom}", "bound": "mfma", "achieved": round(achieved, 2),
+            # operand images in (kx fp16 parts of A and W), output out (fp16 image / fp32)
+            out_b = {"qkv": 4 if kx == 3 else 2, "ffn1": 2 * kx}.get(dom, 4 if kx == 3 else 2)
+            alg_bytes = rows_per_launch * (kx * nk[1] * 2 + nk[0] * out_b) + kx * nk[0] * nk[1] * 2
+        roof = {"kernel": f"gemm_{args.precision}_{dom}", "bound": "mfma", "achieved": round(achieved, 2),
                 "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP16_TFLOPS, 4),
+                "achieved_basis": ("MFMA work: 2*M*N*K over the kx-wide fp16 operand images "
+                                   f"(kx={kx}) / HIP-event launch time, vs the dense fp16 MFMA peak"),
+                "achieved_algorithmic": round(achieved_alg, 2),
                 "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes": alg_bytes,
                 "launches": n, "avg_launch_ms": round(ms / max(n, 1), 4),
-                "flops_per_launch": fl / max(n, 1)}
+                "flops_per_launch": fl / max(n, 1), "algorithmic_flops_per_launch": fl / kx / max(n, 1)}
 
     # ---- reranked 1-best CER (second half of BASELINE.json's metric), rank-0 shard -------
     # HIP fusion over the 101-weight grid + corpus CER on this step's LM scores, checked
@@ -168,39 +195,60 @@ def main():
               "argmax_equal_oracle": bool(np.array_equal(np.asarray(arg), oarg))}
 
     # ---- CPU baseline: oracle restatement of the reference work pattern ------------------
+    # Also a scoring-parity spot check at bench scale: the PLL of every sampled hypothesis
+    # (reference work pattern, fp32 CPU) against the HIP lm of the timed steps.
     cpu = None
     if rank == 0 and args.cpu_seconds > 0:
-        from oracle.bert_ref import TorchBert, set_cpu_threads, pll_rows
+        from oracle.bert_ref import TorchBert, set_cpu_threads
         import oracle.bert_ref as OB
         threads = set_cpu_threads()
         model = TorchBert(weights, BERT_BASE)
-        rows_done, t_cpu = 0, 0.0
-        h = 0
+        lm_np = lm.double().cpu().numpy()
+        rows_done, t_cpu, h, rel = 0, 0.0, 0, []
         while t_cpu < args.cpu_seconds and h < nb.n_hyp:
             sub_off = nb.hyp_off[h:h + 2] - nb.hyp_off[h]
             toks = nb.tokens[nb.hyp_off[h]:nb.hyp_off[h + 1]]
             t1 = time.perf_counter()
-            OB.pll_reference_pattern(model, toks, sub_off, batch_size=32, full_head=True)
+            _, ref_pll = OB.pll_reference_pattern(model, toks, sub_off, batch_size=32, full_head=True)
             t_cpu += time.perf_counter() - t1
+            rel.append(abs(lm_np[h] - ref_pll[0]) / abs(ref_pll[0]))
             rows_done += int(sub_off[-1]) - 2
             h += 1
         cpu = {"value": round(rows_done / t_cpu, 2), "unit": "masked fwd/s", "cores": threads,
-               "kind": "port", "sample": f"{h} hypotheses ({rows_done} masked forwards) of rank-0 step "
+               "cpu_model": _cpu_model(), "kind": "port",
+               "sample": f"{h} hypotheses ({rows_done} masked forwards) of rank-0 step "
                f"input, reference work pattern (batch 32 padded rows, all-position logits + CE, "
-               f"fp64 accumulation), torch {torch.__version__} CPU"}
-        _ = pll_rows
+               f"fp64 accumulation), torch {torch.__version__} CPU",
+               "pll_max_rel_err_vs_gpu": float(max(rel)) if rel else None}
+
+    # ---- secondary leg: the reduced-precision fp16 mode on the same input (labelled) ------
+    fp16 = None
+    if rank == 0 and args.precision != "fp16" and args.fp16_steps > 0:
+        s16 = PLLScorer(weights, BERT_BASE, device=local, max_rows=args.max_rows, precision="fp16")
+        lm16 = s16.score_nbest(d_tok, nb.hyp_off)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.fp16_steps):
+            lm16 = s16.score_nbest(d_tok, nb.hyp_off)
+        torch.cuda.synchronize()
+        dt16 = time.perf_counter() - t1
+        rel16 = ((lm16 - lm).abs() / lm.abs()).max().item()
+        fp16 = {"value": round(n_fwd * args.fp16_steps / dt16, 2), "unit": "masked fwd/s",
+                "dtype": "fp16 operands / fp32 accumulate (reduced precision; not the headline)",
+                "steps": args.fp16_steps, "pll_max_rel_vs_headline": rel16}
+        s16.close()
 
     if rank == 0:
         mean_T = float(np.average(lens, weights=lens - 2))
         rec = {"metric": "masked-token BERT forwards/sec (MLM_PLL, N=50, L~32)", "value": round(value, 2),
                "unit": "masked fwd/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": None, "dtype": "fp16-mfma/fp32-acc", "data": "synthetic (PCG64 seed 1; random-init bert-base weights seed 1234)",
+               "vs_baseline": None, "dtype": DTYPE[args.precision], "data": "synthetic (PCG64 seed 1; random-init bert-base weights seed 1234)",
                "config": {"workload": "C3 MLM_PLL full PLL", "model": "bert-base-chinese shape (12L/768/12H/3072/V21128)",
                           "utts_per_rank": args.utts, "n_best": args.nbest, "forwards_per_rank_step": n_fwd,
                           "mean_T": round(mean_T, 2), "parallelism": f"dp{world} (utterance shards + RCCL all_gather)"},
                "achieved_tflops_canonical": round(flops_step * world * args.steps / dt / 1e12, 2),
-               "roofline": roof, "cpu_baseline": cpu, "rerank": rr,
+               "roofline": roof, "cpu_baseline": cpu, "rerank": rr, "fp16_secondary": fp16,
                "kinds_ms": {k: round(v[0], 3) for k, v in kinds.items()}}
         print(json.dumps(rec))
     scorer.close()

@@ -1,8 +1,10 @@
 """GPU parity: HIP BERT scorers vs the golden fixtures (reference outputs) and the oracle.
 
 Tolerance (BASELINE.json north_star): scores within 1e-3 relative of the reference
-PyTorch-CPU fp32 path.  The HIP path computes GEMMs with fp16 MFMA inputs and fp32
-accumulation; LayerNorm, softmax, GELU, logsumexp in fp32; PLL sums in fp64.
+PyTorch-CPU fp32 path, per masked row as well as per hypothesis.  The default precision
+(fp16x3) splits every fp32 GEMM operand into fp16 hi/lo parts on the fp16 MFMA with fp32
+accumulation (fp32-level accuracy); LayerNorm, softmax, GELU, logsumexp in fp32; PLL sums
+in fp64.  The opt-in "fp16" mode (fp16 operands) is reduced precision and is tested as such.
 """
 import os
 
@@ -36,6 +38,15 @@ def w_tiny():
 def pll_base(w_base):
     from asr_rescoring_amd.scorer import PLLScorer
     s = PLLScorer(w_base, BERT_BASE, device=0, max_rows=8192)
+    assert s.precision == "fp16x3"
+    yield s
+    s.close()
+
+
+@pytest.fixture(scope="module")
+def pll_base16(w_base):
+    from asr_rescoring_amd.scorer import PLLScorer
+    s = PLLScorer(w_base, BERT_BASE, device=0, max_rows=8192, precision="fp16")
     yield s
     s.close()
 
@@ -53,20 +64,15 @@ def rel_err(a, b):
     return np.abs(a - b) / np.maximum(np.abs(b), 1e-30)
 
 
-# fp16 mode, per masked row (token_score, an intermediate of the score): measured max
-# 1.07e-3 / p99 8e-4 relative on F1; the scores themselves (per-hypothesis PLL) stay
-# <= 2e-4.  Strict 1e-3 rows: the fp16x3 mode (test_pll_fp16x3_golden, <= 2e-6).
-ROW_REL_FP16 = 2e-3
-
-
 def test_pll_base_golden(pll_base, golden_dir):
+    """Default precision against the reference-run F1 fixture: every masked row's
+    token_score (MLM_PLL/main.py:105) and every PLL within 1e-3 relative (measured ~1e-6)."""
     g = _load(golden_dir, "pll_base.npz")
     pll, rows = pll_base.score_nbest(g["tokens"], g["hyp_off"], return_rows=True)
     rows = rows.cpu().numpy()
     pll = pll.cpu().numpy()
     assert rel_err(pll, g["pll"]).max() < REL
-    e = rel_err(rows, g["row_lp"])
-    assert e.max() < ROW_REL_FP16 and np.percentile(e, 99) < REL and e.mean() < 5e-4
+    assert rel_err(rows, g["row_lp"]).max() < REL
     # per-hypothesis sum of the returned rows in row order, fp64 == pll (bit-exact)
     off = np.concatenate([[0], np.cumsum(np.diff(g["hyp_off"]) - 2)])
     for h in range(len(pll)):
@@ -74,6 +80,16 @@ def test_pll_base_golden(pll_base, golden_dir):
         for x in rows[off[h]:off[h + 1]]:
             acc += float(x)
         assert acc == pll[h]
+
+
+def test_pll_fp16_mode_golden(pll_base16, golden_dir):
+    """Opt-in reduced-precision mode (fp16 operands): the per-hypothesis PLL stays within
+    1e-3 relative; per-row log-probs are NOT held to 1e-3 in this mode (measured max ~1.1e-3
+    on F1) — that is why fp16x3 is the default and the bench headline."""
+    g = _load(golden_dir, "pll_base.npz")
+    pll, rows = pll_base16.score_nbest(g["tokens"], g["hyp_off"], return_rows=True)
+    assert rel_err(pll.cpu().numpy(), g["pll"]).max() < REL
+    assert np.percentile(rel_err(rows.cpu().numpy(), g["row_lp"]), 99) < REL
 
 
 def test_pll_tiny_golden(pll_tiny, golden_dir):
@@ -223,15 +239,16 @@ def test_oracle_parity_base_synthetic(pll_base, w_base):
     assert rel_err(got, ref).max() < REL
 
 
+@pytest.mark.parametrize("prec", ["fp16", "fp16x3"])
 @pytest.mark.parametrize("max_rows", [512, 65536])
-def test_layer0_dedup_is_exact(w_tiny, w_base, max_rows, monkeypatch):
+def test_layer0_dedup_is_exact(w_tiny, w_base, max_rows, prec, monkeypatch):
     """Layer-0 Q/K/V over unique rows (RS_DEDUP=1, default) vs over every masked copy
     (RS_DEDUP=0): the same rows go through the same GEMM, so scores are bitwise equal.
     max_rows=512 splits hypotheses across chunks (a hypothesis' rows re-planned per chunk)."""
     from asr_rescoring_amd.scorer import PLLScorer
     for w, cfg, seed in ((w_tiny, BERT_TINY, 5), (w_base, BERT_BASE, 6)):
         nb = D.synthetic_nbest(5, 4, seed=seed, vocab=cfg.vocab, len_lo=1, len_hi=70)
-        s = PLLScorer(w, cfg, device=0, max_rows=max_rows)
+        s = PLLScorer(w, cfg, device=0, max_rows=max_rows, precision=prec)
         try:
             monkeypatch.setenv("RS_DEDUP", "1")
             a = s.score(nb)
@@ -244,21 +261,21 @@ def test_layer0_dedup_is_exact(w_tiny, w_base, max_rows, monkeypatch):
 
 @pytest.mark.parametrize("env,same", [({"RS_OPROJ": "resln"}, False), ({"RS_FFN2": "f16"}, True),
                                       ({"RS_LNRES_DEFER": "0"}, False), ({"RS_LNRES_DEFER": "1"}, False)])
-def test_residual_paths_golden(pll_base, golden_dir, env, same, monkeypatch):
+def test_residual_paths_golden(pll_base16, golden_dir, env, same, monkeypatch):
     """The residual-block variants against the F1 fixture: O projection with the residual +
     LayerNorm rebuilt in the GEMM accumulators (RS_OPROJ=resln; default: fp16-output GEMM +
     ln_res_rows), FFN2 split the same way as the O projection (RS_FFN2=f16), and the
     post-attention stream written back (RS_LNRES_DEFER=0) or rebuilt in the BertOutput GEMM's
     accumulators (=1) instead of the default single two-block ln_res_rows pass (=2)."""
     g = _load(golden_dir, "pll_base.npz")
-    base = pll_base.score_nbest(g["tokens"], g["hyp_off"]).cpu().numpy()
+    base = pll_base16.score_nbest(g["tokens"], g["hyp_off"]).cpu().numpy()
     for k, v in env.items():
         monkeypatch.setenv(k, v)
-    pll, rows = pll_base.score_nbest(g["tokens"], g["hyp_off"], return_rows=True)
+    pll, rows = pll_base16.score_nbest(g["tokens"], g["hyp_off"], return_rows=True)
     pll = pll.cpu().numpy()
     assert rel_err(pll, g["pll"]).max() < REL
     e = rel_err(rows.cpu().numpy(), g["row_lp"])
-    assert e.max() < ROW_REL_FP16 and np.percentile(e, 99) < REL
+    assert np.percentile(e, 99) < REL
     if same:
         # RS_FFN2=f16 stores the post-attention stream x in fp32 and forms LN(x) + o2 in a
         # second pass; the default forms the same expression from (x32, o1) in one pass:

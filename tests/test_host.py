@@ -68,3 +68,14 @@ def test_config_yaml_roundtrip(tmp_path):
     c = parse_config(load_yaml(str(p)))
     assert c.task == "scoring" and c.dataloader.batch_size == 32 and c.model.bert == "x"
     _ = np
+
+
+def test_attention_mask_validation():
+    """RescoreBertHIP.forward / masked_logprob accept only right-padded 0/1 masks."""
+    import torch
+    from asr_rescoring_amd.scorer import _prefix_lengths
+    ok = torch.tensor([[1, 1, 1, 0], [1, 1, 1, 1], [1, 0, 0, 0]])
+    assert _prefix_lengths(ok).tolist() == [3, 4, 1]
+    for bad in ([[0, 1, 1, 1]], [[1, 0, 1, 0]], [[1, 2, 0, 0]]):
+        with pytest.raises(ValueError):
+            _prefix_lengths(torch.tensor(bad))
