@@ -79,9 +79,16 @@ def _nbest_tokens(hyps_text: Dict[str, Dict[str, str]], tok, max_utt=1 << 30, n_
 # --------------------------------------------------------------------------------------
 def mlm_pll(cfg) -> Dict[str, str]:
     """MLM_PLL/main.py:164-203 (pll_bert_scoring).  Accepts the reference's preprocessed
-    rows (``*_data_path``: do_job output) or raw ``*_hyps_text_path`` JSON."""
+    rows (``*_data_path``: do_job output) or raw ``*_hyps_text_path`` JSON.
+
+    Launched with torchrun (WORLD_SIZE > 1): one process per GPU, each scores a contiguous,
+    cost-balanced utterance range (``shard.plan_shards``); the scores meet in one all-gather
+    (RCCL) and rank 0 writes the JSON (the reference is single-process)."""
+    from . import shard
     from .scorer import PLLScorer
-    scorer = PLLScorer(_weights(cfg, "mlm"), BERT_BASE, device=_dev(cfg), max_rows=get(cfg, "max_rows", 65536),
+    rank, world, local = shard.init_from_env()
+    device = local if world > 1 else _dev(cfg)
+    scorer = PLLScorer(_weights(cfg, "mlm"), BERT_BASE, device=device, max_rows=get(cfg, "max_rows", 65536),
                        precision=get(cfg, "precision", "fp16x3"))
     out_files = {}
     for split in ("train", "dev", "test"):
@@ -89,27 +96,60 @@ def mlm_pll(cfg) -> Dict[str, str]:
         text_path = get(cfg, f"{split}_hyps_text_path")
         if rows_path and os.path.exists(rows_path):
             rows = _load(rows_path)[:get(cfg, "num_of_data", 1 << 62)]
-            output_score: Dict[str, Dict[str, float]] = {}
-            for r in rows:                                   # MLM_PLL/main.py:189-193
-                if r["hyp_id"] == "hyp_1":
-                    output_score[r["utt_id"]] = {}
-                output_score[r["utt_id"]][r["hyp_id"]] = 0
-            output_score = scorer.run_one_epoch(rows, output_score)
+            output_score = _score_rows_sharded(scorer, rows, rank, world)
         elif text_path and os.path.exists(text_path):
             hyps = _load(text_path)
             tok = _tokenizer(cfg, [t for h in hyps.values() for t in h.values()])
             nb, keys = _nbest_tokens(hyps, tok)
-            pll = scorer.score(nb)
+            both = shard.score_sharded(nb, lambda sub: scorer.score_nbest(sub.tokens, sub.hyp_off))
+            pll = both[1].cpu().numpy()
             output_score = {}
             for (u, h), s in zip(keys, pll):
                 output_score.setdefault(u, {})[h] = float(s)
         else:
             continue
         path = cfg.output_path + f"{split}_lm.json"          # MLM_PLL/main.py:203 naming
-        json_saving(path, output_score)
+        if rank == 0:
+            json_saving(path, output_score)
         out_files[split] = path
     scorer.close()
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
     return out_files
+
+
+def _score_rows_sharded(scorer, rows, rank: int, world: int) -> Dict[str, Dict[str, float]]:
+    """do_job rows (MLM_PLL/preprocess.py:9-30) scored by ``PLLScorer.run_one_epoch``; with
+    several ranks each takes a contiguous, cost-balanced run of whole utterances and the
+    per-row log-probs are exchanged once; every rank then forms ``output_score`` in the
+    reference's row order (MLM_PLL/main.py:106-107)."""
+    from . import shard
+    output_score: Dict[str, Dict[str, float]] = {}
+    for r in rows:                                       # MLM_PLL/main.py:189-193
+        if r["hyp_id"] == "hyp_1":
+            output_score[r["utt_id"]] = {}
+        output_score[r["utt_id"]][r["hyp_id"]] = 0
+    import torch
+    if world == 1:
+        allv = scorer.row_logprobs(rows).cpu().tolist() if rows else []
+        for r, s in zip(rows, allv):
+            output_score[r["utt_id"]][r["hyp_id"]] += s
+        return output_score
+    import torch.distributed as dist
+    # utterance runs of consecutive rows; cost = token rows
+    starts = [i for i, r in enumerate(rows) if i == 0 or r["utt_id"] != rows[i - 1]["utt_id"]] + [len(rows)]
+    costs = [sum(len(rows[i]["input_ids"]) for i in range(a, b)) for a, b in zip(starts, starts[1:])]
+    parts = shard.plan_shards(costs, world)
+    bounds = [(starts[a], starts[b]) for a, b in parts]
+    r0, r1 = bounds[rank]
+    lp = scorer.row_logprobs(rows[r0:r1]) if r1 > r0 else torch.zeros(0, device=scorer.device)
+    counts = [b - a for a, b in bounds]
+    dev = torch.device("cpu") if dist.get_backend() == "gloo" else scorer.device
+    allv = shard.gather_scores(lp.to(dev, torch.float32)[None], counts)[0].cpu().tolist()
+    for r, s in zip(rows, allv):
+        output_score[r["utt_id"]][r["hyp_id"]] += s
+    return output_score
 
 
 def mlm_finetune(cfg) -> Dict[str, object]:

@@ -56,6 +56,16 @@ class NBest:
         """Number of masked forwards R = sum_h L_h (one per masked position)."""
         return int(self.hyp_len().sum())
 
+    def slice_utts(self, u0: int, u1: int) -> "NBest":
+        """Contiguous utterance range [u0, u1) (vectorised; a rank's shard)."""
+        h0, h1 = int(self.utt_off[u0]), int(self.utt_off[u1])
+        t0, t1 = int(self.hyp_off[h0]), int(self.hyp_off[h1])
+        return NBest(np.ascontiguousarray(self.tokens[t0:t1], np.int32),
+                     (np.asarray(self.hyp_off[h0:h1 + 1], np.int64) - t0).astype(np.int32),
+                     (np.asarray(self.utt_off[u0:u1 + 1], np.int64) - h0).astype(np.int32),
+                     np.asarray(self.am[h0:h1], np.float64), list(self.refs[u0:u1]),
+                     list(self.utt_ids[u0:u1]), list(self.hyp_ids[h0:h1]))
+
     def subset(self, utts: Sequence[int]) -> "NBest":
         toks, hoff, uoff, am, hyp_ids, refs, uids = [], [0], [0], [], [], [], []
         for u in utts:
@@ -131,11 +141,14 @@ def _edit(rng: np.random.Generator, base: List[int], k: int, vocab: int) -> List
 
 def synthetic_nbest(n_utt: int, n_best: int, seed: int = 1, vocab: int = 21128,
                     len_lo: int = 24, len_hi: int = 40, max_edits: int = 3,
-                    lengths: Optional[np.ndarray] = None) -> NBest:
+                    lengths: Optional[np.ndarray] = None, hard: bool = False) -> NBest:
     """Seeded synthetic N-best lists.
 
     ``lengths`` (optional) is a histogram sample of base lengths (real-length variant).
     Hypotheses within an utterance are distinct where possible (like ESPnet beams).
+    ``hard``: the reference-identical hypothesis is not first and the AM scores are not
+    sorted (hypotheses permuted, AM drawn per hypothesis), so the fused argmax moves with the
+    weight and the reranked CER is not simply the AM-only CER (parity tests of the rerank).
     """
     rng = np.random.Generator(np.random.PCG64(seed))
     hyps, ams, refs = [], [], []
@@ -151,7 +164,12 @@ def synthetic_nbest(n_utt: int, n_best: int, seed: int = 1, vocab: int = 21128,
             seen.add(tuple(w))
             utt.append(w)
         am = -np.abs(rng.normal(5.8, 4.0, size=n_best))
-        ams.append(np.sort(am)[::-1].tolist())
+        if hard:
+            perm = rng.permutation(n_best)
+            utt = [utt[int(i)] for i in perm]
+            ams.append(am.tolist())
+        else:
+            ams.append(np.sort(am)[::-1].tolist())
         hyps.append(utt)
         refs.append(base)
     return from_lists(hyps, ams, refs)

@@ -151,13 +151,9 @@ class PLLScorer(BertEngine):
                                               _lib.stream_ptr(self.device)))
         return out
 
-    def run_one_epoch(self, rows, output_score: dict) -> dict:
-        """Mirror of ``run_one_epoch(..., train_mode=False, do_scoring=True)``
-        (MLM_PLL/main.py:73-114) over ``do_job`` rows (dicts with utt_id, hyp_id,
-        input_ids, labels, mask_pos): scores all rows in one ragged launch sequence and
-        adds them to ``output_score[utt][hyp]`` in row order (float64, like ``+=``)."""
-        if not rows:
-            return output_score
+    def row_logprobs(self, rows) -> torch.Tensor:
+        """``token_score`` (MLM_PLL/main.py:101-105) of every do_job row, float32 [R] (device),
+        all rows in one ragged launch sequence."""
         seqs = [r["input_ids"] for r in rows]
         off = np.zeros(len(rows) + 1, np.int32)
         off[1:] = np.cumsum([len(s) for s in seqs])
@@ -168,7 +164,16 @@ class PLLScorer(BertEngine):
         _lib.check(self.lib.rs_masked_logprob(self.handle, _lib.ptr(d_ids), off.ctypes.data, mp.ctypes.data,
                                               _lib.ptr(lab), len(rows), _lib.ptr(out),
                                               _lib.stream_ptr(self.device)))
-        for r, s in zip(rows, out.cpu().tolist()):
+        return out
+
+    def run_one_epoch(self, rows, output_score: dict) -> dict:
+        """Mirror of ``run_one_epoch(..., train_mode=False, do_scoring=True)``
+        (MLM_PLL/main.py:73-114) over ``do_job`` rows (dicts with utt_id, hyp_id,
+        input_ids, labels, mask_pos): scores all rows in one ragged launch sequence and
+        adds them to ``output_score[utt][hyp]`` in row order (float64, like ``+=``)."""
+        if not rows:
+            return output_score
+        for r, s in zip(rows, self.row_logprobs(rows).cpu().tolist()):
             output_score[r["utt_id"]][r["hyp_id"]] += s
         return output_score
 

@@ -57,3 +57,52 @@ def gather_scores(local: torch.Tensor, counts: Sequence[int], group=None) -> tor
     dist.all_gather_into_tensor(out, buf.reshape(-1, width).contiguous(), group=group)
     out = out.view(world, C, width)
     return torch.cat([out[r, :, :counts[r]] for r in range(world)], dim=1)
+
+
+def init_from_env(device_index: int | None = None):
+    """torchrun / torch.distributed.run launch: (rank, world, local_rank).  Initialises the
+    default process group once (backend "nccl" = RCCL when a GPU is visible, else "gloo")."""
+    import os
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) if device_index is None else device_index
+    # RS_DIST_BACKEND=gloo: CPU exchange (e.g. several ranks sharing one GPU in a test)
+    backend = os.environ.get("RS_DIST_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
+    if world > 1 and not dist.is_initialized():
+        if backend == "nccl":
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
+    return rank, world, local
+
+
+def shard_of(nb: NBest, world: int, rank: int, mode: str = "pll") -> Tuple[int, int]:
+    """This rank's contiguous utterance range [u0, u1) (cost-balanced, ``plan_shards``)."""
+    return plan_shards(utterance_costs(nb, mode), world)[rank]
+
+
+def score_sharded(nb: NBest, score_fn, mode: str = "pll", device=None, group=None) -> torch.Tensor:
+    """Utterance-sharded scoring with one all-gather (MLM_PLL/main.py:164-203 on
+    N ranks).  ``score_fn(sub_nbest) -> lm [H_local]`` scores this rank's utterances (the HIP
+    scorer in the product; any callable in tests).  Returns the (am, lm) float64 block
+    [2, H] of EVERY hypothesis, in global order, on every rank."""
+    world = dist.get_world_size(group) if dist.is_initialized() else 1
+    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    parts = plan_shards(utterance_costs(nb, mode), world)
+    u0, u1 = parts[rank]
+    sub = nb.slice_utts(u0, u1)
+    h0, h1 = int(nb.utt_off[u0]), int(nb.utt_off[u1])
+    lm = score_fn(sub) if h1 > h0 else torch.zeros(0, dtype=torch.float64)
+    lm = torch.as_tensor(lm).to(torch.float64)
+    dev = lm.device if device is None else torch.device(device)
+    if world > 1 and dist.get_backend(group) == "gloo":
+        dev = torch.device("cpu")
+    am = torch.from_numpy(np.ascontiguousarray(nb.am[h0:h1], np.float64)).to(dev)
+    local = torch.stack([am, lm.to(dev)])
+    if world == 1:
+        return local
+    counts = [int(nb.utt_off[b] - nb.utt_off[a]) for a, b in parts]
+    if max(counts) == 0:
+        return local
+    return gather_scores(local, counts, group)

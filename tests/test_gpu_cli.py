@@ -143,3 +143,41 @@ def test_cli_mlm_finetune_then_pll(c1):
         "model": {"bert": "bert-base-chinese", "vocab": str(d / "vocab.txt")}})]) == 0
     lm = json.load(open(str(out) + "/train_lm.json", encoding="utf-8"))
     assert list(lm) == g["utt_ids"] and all(np.isfinite(v) and v < 0 for u in lm.values() for v in u.values())
+
+
+def test_cli_mlm_pll_two_ranks(c1, tmp_path):
+    """``cli mlm_pll`` launched as 2 ranks (torchrun-style env, both on this box's GPU, gloo
+    exchange since one GPU cannot host two RCCL ranks): utterance shards + one all-gather give
+    the single-process scores (the C4 path of SURVEY §8e at toy scale)."""
+    import socket
+    import subprocess
+    import sys
+    from conftest import REPO
+    g, d = c1
+    outs = {}
+    for world in (1, 2):
+        out = tmp_path / f"w{world}"
+        out.mkdir()
+        cfg = _cfg(d, f"score_w{world}.yaml", {
+            "task": "scoring", "device": "cuda:0", "random_init_seed": 1234,
+            "train_hyps_text_path": str(d / "hyps_text.json"), "output_path": str(out) + "/",
+            "model": {"bert": "bert-base-chinese", "vocab": str(d / "vocab.txt")}})
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        code = ("import sys; sys.path.insert(0, %r); import __graft_entry__ as g; g._import_pkg(); "
+                "from asr_rescoring_amd import cli; sys.exit(cli.main(['mlm_pll', '--config', %r]))" % (REPO, cfg))
+        procs = []
+        for r in range(world):
+            env = dict(os.environ, WORLD_SIZE=str(world), RANK=str(r), LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+                       MASTER_PORT=str(port), RS_DIST_BACKEND="gloo")
+            procs.append(subprocess.Popen([sys.executable, "-c", code], env=env))
+        for p in procs:
+            assert p.wait(timeout=300) == 0
+        outs[world] = json.load(open(out / "train_lm.json", encoding="utf-8"))
+    assert list(outs[1]) == list(outs[2]) == g["utt_ids"]
+    a = np.array([v for u in outs[1].values() for v in u.values()])
+    b = np.array([v for u in outs[2].values() for v in u.values()])
+    # the scores of a hypothesis do not depend on which rank / launch chunk computed them
+    assert np.array_equal(a, b), np.abs(a - b).max()

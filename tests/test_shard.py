@@ -72,5 +72,99 @@ def test_gloo_world2_gather_matches_single_process():
     assert np.array_equal(got[1], lm)
 
 
+def _oracle_pll_fn(model):
+    """Per-hypothesis oracle PLL (CPU fp32, batch = one hypothesis' rows): independent of how
+    utterances are split, so sharded and single-process scores must be bitwise equal."""
+    from oracle.bert_ref import pll_reference_pattern
+
+    def fn(sub):
+        out = []
+        for h in range(sub.n_hyp):
+            toks = sub.tokens[sub.hyp_off[h]:sub.hyp_off[h + 1]]
+            out.append(pll_reference_pattern(model, toks, np.array([0, len(toks)]), batch_size=64,
+                                             full_head=False)[1][0])
+        return torch.tensor(out, dtype=torch.float64)
+    return fn
+
+
+class _OracleRowScorer:
+    """Stand-in for PLLScorer.row_logprobs on CPU (oracle masked_logprob_ref per row)."""
+    device = torch.device("cpu")
+
+    def __init__(self, model):
+        self.model = model
+
+    def row_logprobs(self, rows):
+        from oracle.bert_ref import masked_logprob_ref
+        out = [masked_logprob_ref(self.model, np.asarray([r["input_ids"]]), np.ones((1, len(r["input_ids"]))),
+                                  np.asarray([r["labels"]]), np.asarray([r["mask_pos"]]))[0] for r in rows]
+        return torch.tensor(out, dtype=torch.float32)
+
+
+def _tiny_case():
+    from asr_rescoring_amd.weights import BERT_TINY, make_weights
+    from oracle.bert_ref import TorchBert
+    torch.set_num_threads(1)
+    nb = D.synthetic_nbest(5, 4, seed=12, vocab=BERT_TINY.vocab, len_lo=2, len_hi=9, hard=True)
+    return nb, TorchBert(make_weights(BERT_TINY, seed=7), BERT_TINY)
+
+
+def _rows_of(nb):
+    from oracle.bert_ref import pll_rows
+    rows = []
+    for h, ids, mp, lab in pll_rows(nb.tokens, nb.hyp_off):
+        u = int(np.searchsorted(nb.utt_off, h, side="right") - 1)
+        rows.append({"utt_id": f"u{u}", "hyp_id": f"hyp_{h - nb.utt_off[u] + 1}", "input_ids": ids,
+                     "mask_pos": mp, "labels": lab})
+    return rows
+
+
+def _worker_score(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank),
+                      LOCAL_RANK="0", RS_DIST_BACKEND="gloo")
+    from asr_rescoring_amd import cli
+    from asr_rescoring_amd.shard import init_from_env, score_sharded
+    from oracle import rescore_ref as RR
+    init_from_env()
+    nb, model = _tiny_case()
+    both = score_sharded(nb, _oracle_pll_fn(model))
+    rows_out = cli._score_rows_sharded(_OracleRowScorer(model), _rows_of(nb), rank, world)
+    if rank == 0:
+        N = 4
+        hyps = [[nb.hyp_words(nb.utt_off[u] + i) for i in range(N)] for u in range(nb.n_utt)]
+        lm = both[1].numpy().reshape(nb.n_utt, N)
+        fused = RR.find_best_weight(both[0].numpy().reshape(nb.n_utt, N), lm, hyps, nb.refs, n_best=N)
+        q.put((both.numpy(), fused[0], fused[1], fused[2], rows_out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_score_gather_fuse_bitwise():
+    """Split -> score (oracle PLL as the scorer) -> one all-gather -> rank-0 fusion sweep
+    (rescore.py:25-45), and the do_job-rows path of ``cli mlm_pll`` on 2 ranks: bitwise equal
+    to the single-process results."""
+    from asr_rescoring_amd import cli
+    from oracle import rescore_ref as RR
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_score, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got, bw, bcer, arg, rows_out = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nb, model = _tiny_case()
+    lm = _oracle_pll_fn(model)(nb).numpy()
+    assert np.array_equal(got[0], nb.am) and np.array_equal(got[1], lm)
+    N = 4
+    hyps = [[nb.hyp_words(nb.utt_off[u] + i) for i in range(N)] for u in range(nb.n_utt)]
+    bw1, bcer1, arg1 = RR.find_best_weight(nb.am.reshape(nb.n_utt, N), lm.reshape(nb.n_utt, N), hyps, nb.refs,
+                                           n_best=N)
+    assert bw == bw1 and bcer == bcer1 and np.array_equal(arg, arg1)
+    assert rows_out == cli._score_rows_sharded(_OracleRowScorer(model), _rows_of(nb), 0, 1)
+
+
 if __name__ == "__main__":
     pytest.main([__file__, "-q"])
