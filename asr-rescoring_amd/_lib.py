@@ -34,7 +34,7 @@ RS_LOSS = {"MD": 0, "MD_MWER": 1, "MD_MWED": 2}
 
 
 class RsTrainOpts(ctypes.Structure):
-    _fields_ = [("loss", ctypes.c_int32), ("lambda_", ctypes.c_float), ("lr", ctypes.c_float),
+    _fields_ = [("loss", ctypes.c_int32), ("md_loss_weight", ctypes.c_float), ("lr", ctypes.c_float),
                 ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float),
                 ("weight_decay", ctypes.c_float), ("update", ctypes.c_int32)]
 
@@ -69,7 +69,7 @@ _SIGS = {
     "rs_trainer_set_tensor": (ctypes.c_int, [P, ctypes.c_char_p, P, ctypes.c_int, ctypes.POINTER(I64), ctypes.c_int]),
     "rs_trainer_finalize": (ctypes.c_int, [P]),
     "rs_train_step_cls": (ctypes.c_int, [P, P, P, I32, P, I32, P, P, P, ctypes.POINTER(RsTrainOpts), P, P, P]),
-    "rs_train_step_mlm": (ctypes.c_int, [P, P, P, I32, P, ctypes.POINTER(RsTrainOpts), P, P]),
+    "rs_train_step_mlm": (ctypes.c_int, [P, P, P, I32, P, P, ctypes.POINTER(RsTrainOpts), P, P]),
     "rs_trainer_get_tensor": (ctypes.c_int, [P, ctypes.c_char_p, P, I64]),
     "rs_trainer_get_grad": (ctypes.c_int, [P, ctypes.c_char_p, P, I64]),
     "rs_trainer_reset_optimizer": (ctypes.c_int, [P]),

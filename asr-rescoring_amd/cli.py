@@ -152,55 +152,71 @@ def _score_rows_sharded(scorer, rows, rank: int, world: int) -> Dict[str, Dict[s
     return output_score
 
 
+def _save_checkpoint(output_path: str, state: Dict[str, np.ndarray], n: int) -> str:
+    """util/saving.py:7-11 model_saving: ``checkpoint_{n}.pth`` (torch.save of the HF-keyed
+    state_dict; loadable with ``torch.load(weights_only=True)`` as ``checkpoint_path``)."""
+    import torch
+    path = os.path.join(output_path, f"checkpoint_{n}.pth")
+    torch.save({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in state.items()}, path)
+    return path
+
+
 def mlm_finetune(cfg) -> Dict[str, object]:
     """MLM_PLL/main.py:117-161 (mlm_finetune_bert) on the native trainer (``train.MLMTrainer``).
 
-    Data: ``train_data_path`` (preprocessed ``do_job`` rows: input_ids / labels) or
-    ``train_ref_text_path`` ({utt: text}; tokenised and expanded by ``do_job_rows``).  Keys:
-    ``epochs``, ``batch_size`` (rows per step, 32), ``lr``, ``weight_decay``, ``shuffle`` +
-    ``seed``; AdamW is re-created every epoch as the reference does (``:76``,
-    ``reset_optimizer`` false keeps it).  Writes ``checkpoint_{epoch}.pt`` per epoch (``:157``)."""
+    Reference keys (MLM_PLL/config/train.yaml): ``train_data_path`` / ``dev_data_path``
+    (preprocessed do_job rows), ``num_of_data``, ``epoch``, ``lr``, ``dataloader.batch_size``
+    (rows, 32), ``dataloader.shuffle`` (False), ``output_path``.  Batches are the reference's
+    padded batches (``train.pad_rows``; CE over every position, [PAD] labels included); AdamW
+    is re-created every epoch (``:76``); per epoch the dev loss (no update), then
+    ``checkpoint_{epoch}.pth`` and ``loss.json`` (``{"train": [...], "dev": [...]}``, zeros for
+    epochs not run yet, as ``:131-161`` writes it).  Extra: ``checkpoint_path`` /
+    ``random_init_seed`` (initial weights: bert-base-chinese cannot be fetched offline),
+    ``train_ref_text_path`` ({utt: text}, expanded by ``do_job_rows``), ``weight_decay``.
+    ``dataloader.shuffle: True`` draws the order from torch.randperm seeded by ``seed`` (not the
+    reference's sampler stream)."""
     import torch
-    from .train import MLMTrainer, do_job_rows
+    from .train import MLMTrainer, do_job_rows, mlm_epoch
     os.makedirs(cfg.output_path, exist_ok=True)
-    log = _logger(os.path.join(cfg.output_path, "train.log"))
-    rows_path, ref_path = get(cfg, "train_data_path"), get(cfg, "train_ref_text_path")
-    if rows_path and os.path.exists(rows_path):
-        rows = _load(rows_path)
-        seqs = [r["input_ids"] for r in rows]
-        labs = [r["labels"] for r in rows]
-    else:
-        refs = _load(ref_path)
-        tok = _tokenizer(cfg, list(refs.values()))
-        hyps = [[101] + list(tok.encode_words(t)) + [102] for t in refs.values()]
-        ids, off, lab = do_job_rows(hyps)
-        seqs = [ids[off[i]:off[i + 1]].tolist() for i in range(len(off) - 1)]
-        labs = [lab[off[i]:off[i + 1]].tolist() for i in range(len(off) - 1)]
+    n_data = int(get(cfg, "num_of_data", 1 << 62))
+
+    def rows_of(split):
+        rows_path, ref_path = get(cfg, f"{split}_data_path"), get(cfg, f"{split}_ref_text_path")
+        if rows_path and os.path.exists(rows_path):
+            rows = _load(rows_path)[:n_data]
+            return [r["input_ids"] for r in rows], [r["labels"] for r in rows]
+        if ref_path and os.path.exists(ref_path):
+            refs = _load(ref_path)
+            tok = _tokenizer(cfg, list(refs.values()))
+            ids, off, lab = do_job_rows([[D.CLS_ID] + list(tok.encode_words(t)) + [D.SEP_ID] for t in refs.values()])
+            n = min(len(off) - 1, n_data)
+            return ([ids[off[i]:off[i + 1]].tolist() for i in range(n)],
+                    [lab[off[i]:off[i + 1]].tolist() for i in range(n)])
+        return None
+    train_d, dev_d = rows_of("train"), rows_of("dev")
+    if train_d is None:
+        raise FileNotFoundError("train_data_path (do_job rows) or train_ref_text_path is required")
     tr = MLMTrainer(_weights(cfg, "mlm"), BERT_BASE, device=_dev(cfg), lr=float(get(cfg, "lr", 1e-5)),
                     weight_decay=float(get(cfg, "weight_decay", 0.01)))
-    bs = int(get(cfg, "batch_size", 32))
-    rng = np.random.default_rng(int(get(cfg, "seed", 0)))
-    losses, ckpts = [], []
-    for ep in range(int(get(cfg, "epochs", 1))):
-        if ep and get(cfg, "reset_optimizer", True):
+    bs = int(get(cfg, "dataloader.batch_size", get(cfg, "batch_size", 32)))
+    shuffle = bool(get(cfg, "dataloader.shuffle", False))
+    gen = torch.Generator().manual_seed(int(get(cfg, "seed", 0)))
+    epochs = int(get(cfg, "epoch", 1))
+    train_rec, dev_rec, ckpts = [0] * epochs, [0] * epochs, []
+    try:
+        for ep in range(1, epochs + 1):
             tr.reset_optimizer()
-        order = rng.permutation(len(seqs)) if get(cfg, "shuffle", True) else np.arange(len(seqs))
-        tot, nb_ = 0.0, 0
-        for b0 in range(0, len(order), bs):
-            idx = order[b0:b0 + bs]
-            off = np.zeros(len(idx) + 1, np.int32)
-            off[1:] = np.cumsum([len(seqs[i]) for i in idx])
-            ids = np.concatenate([np.asarray(seqs[i], np.int32) for i in idx])
-            lab = np.concatenate([np.asarray(labs[i], np.int32) for i in idx])
-            tot += tr.step(ids, off, lab)
-            nb_ += 1
-        losses.append(tot / max(nb_, 1))
-        log.info(f"epoch {ep + 1} loss {losses[-1]}")
-        path = os.path.join(cfg.output_path, f"checkpoint_{ep + 1}.pt")
-        torch.save({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in tr.state_dict().items()}, path)
-        ckpts.append(path)
-    tr.close()
-    return {"losses": losses, "checkpoints": ckpts}
+            order = torch.randperm(len(train_d[0]), generator=gen).numpy() if shuffle else None
+            train_rec[ep - 1] = mlm_epoch(tr, *train_d, bs, update=True, order=order)
+            print("epoch ", ep, " train loss: ", train_rec[ep - 1])
+            if dev_d is not None:
+                dev_rec[ep - 1] = mlm_epoch(tr, *dev_d, bs, update="loss")
+                print("epoch ", ep, " dev loss: ", dev_rec[ep - 1], "\n")
+            ckpts.append(_save_checkpoint(cfg.output_path, tr.state_dict(), ep))
+            D.json_saving(os.path.join(cfg.output_path, "loss.json"), {"train": train_rec, "dev": dev_rec})
+    finally:
+        tr.close()
+    return {"train_loss": train_rec, "dev_loss": dev_rec, "checkpoints": ckpts}
 
 
 def rescorebert(cfg) -> Dict[str, str]:
@@ -230,52 +246,89 @@ def rescorebert(cfg) -> Dict[str, str]:
     return out_files
 
 
+def _rb_features(cfg, split: str):
+    """RescoreBert/preprocess.py:8-55 get_feature: rows (utt, hyp) from the FIRST feature's
+    JSON in key order (``max_utt`` utterances, ``n_best`` hypotheses each), then every named
+    feature looked up per row: ``hyps_token_ids`` ([CLS] tokens [SEP] of the hypothesis text),
+    ``mlm_pll_score``, ``hyps_am_score``, ``hyps_cer``.  Returns None without the split."""
+    feats, paths = get(cfg, f"{split}_feature"), get(cfg, f"{split}_feature_path")
+    if not feats or not paths:
+        return None
+    src = {f: _load(p) for f, p in zip(feats, paths)}
+    max_utt, n_best = int(get(cfg, "max_utt", 1 << 30)), int(get(cfg, "n_best", 1 << 30))
+    keys = []
+    for u, (uid, hyps) in enumerate(src[feats[0]].items()):
+        if u == max_utt:
+            break
+        for k, hid in enumerate(hyps):
+            if k == n_best:
+                break
+            keys.append((uid, hid))
+    out = {"keys": keys, "features": list(feats)}
+    if "hyps_token_ids" in src:
+        texts = src["hyps_token_ids"]
+        tok = _tokenizer(cfg, [t for h in texts.values() for t in h.values()])
+        seqs = [[D.CLS_ID] + list(tok.encode_words(texts[u][h])) + [D.SEP_ID] for u, h in keys]
+        out["tokens"] = np.asarray([x for sq in seqs for x in sq], np.int32)
+        out["hyp_off"] = np.concatenate([[0], np.cumsum([len(sq) for sq in seqs])]).astype(np.int32)
+    for f in ("mlm_pll_score", "hyps_am_score", "hyps_cer"):
+        if f in src:
+            out[f] = np.asarray([src[f][u][h] for u, h in keys], np.float32)
+    return out
+
+
 def rescorebert_train(cfg) -> Dict[str, object]:
     """RescoreBert/main.py:166-229 (train) on the native trainer (``train.RescoreBertTrainer``).
 
-    ``train_feature`` / ``train_feature_path`` name ``hyps_text``, ``ref_text``, ``hyps_score``
-    (AM) and ``mlm_score`` (the MLM_PLL teacher JSON written by ``mlm_pll``).  Keys:
-    ``loss_type`` (MD / MD_MWER / MD_MWED), ``lambda``, ``epochs``, ``batch_size``
-    (utterances per step), ``lr``, ``weight_decay``, ``n_best``, ``reset_optimizer`` (a fresh
-    AdamW each epoch).  Writes ``checkpoint_{epoch}.pt`` (HF keys, torch.save of tensors:
-    loadable with ``torch.load(weights_only=True)`` as ``checkpoint_path``) and ``train.log``."""
-    import torch
-    from . import rerank
-    from .train import RescoreBertTrainer
+    Reference keys (RescoreBert/config/MD*_train.yaml): ``method`` (MD / MD_MWER / MD_MWED),
+    ``md_loss_weight``, ``lr``, ``epoch``, ``batch_size`` (utterances: batch_size * n_best
+    rows), ``n_best``, ``max_utt``, ``train_feature`` / ``train_feature_path`` and ``dev_*``
+    (hyps_token_ids = the hypothesis text JSON, mlm_pll_score, hyps_am_score, hyps_cer),
+    ``output_path``, ``resume.start_from`` / ``resume.checkpoint_path``.  Per epoch: a fresh
+    AdamW (``:83-86``), the train pass, the dev loss (no update), ``checkpoint_{epoch}.pth``
+    and ``loss.json``.  Extra: ``checkpoint_path`` / ``random_init_seed`` (initial weights:
+    bert-base-chinese cannot be fetched offline), ``weight_decay``."""
+    from .train import RescoreBertTrainer, rescorebert_epoch
     os.makedirs(cfg.output_path, exist_ok=True)
-    log = _logger(os.path.join(cfg.output_path, "train.log"))
-    feats, paths = cfg.train_feature, cfg.train_feature_path
-    src = {f: _load(p) for f, p in zip(feats, paths)}
-    n_best, max_utt = get(cfg, "n_best", 1 << 30), get(cfg, "max_utt", 1 << 30)
-    hyps = src["hyps_text"]
-    nb_c = D.from_texts(hyps, src["ref_text"], src["hyps_score"], n_best=n_best, max_utt=max_utt)
-    tok = _tokenizer(cfg, [t for h in hyps.values() for t in h.values()])
-    nb, keys = _nbest_tokens(hyps, tok, max_utt, n_best)
-    target = np.asarray([src["mlm_score"][u][h] for u, h in keys], np.float32)
-    err = rerank.ref_edits(nb_c, device=_dev(cfg)).cpu().numpy().astype(np.float32)
-    am = nb_c.am.astype(np.float32)
-    tr = RescoreBertTrainer(_weights(cfg, "cls"), BERT_BASE, device=_dev(cfg), loss=get(cfg, "loss_type", "MD"),
-                            lam=float(get(cfg, "lambda", 1.0)), lr=float(get(cfg, "lr", 1e-5)),
+    method = str(get(cfg, "method", "MD"))
+    need = ["hyps_token_ids", "mlm_pll_score"] + (["hyps_am_score", "hyps_cer"] if method != "MD" else [])
+    train_f, dev_f = _rb_features(cfg, "train"), _rb_features(cfg, "dev")
+    for f in need:
+        if train_f is None or f not in train_f["features"]:
+            raise KeyError(f"train_feature must name {f} for method {method}")
+    start = get(cfg, "resume.start_from")
+    ck_resume = get(cfg, "resume.checkpoint_path")
+    resume = start is not None and ck_resume is not None
+    weights = load_state_dict_file(ck_resume) if resume else _weights(cfg, "cls")
+    if resume:
+        rec = _load(os.path.join(cfg.output_path, "loss.json"))
+        train_rec, dev_rec = list(rec["train"]), list(rec["dev"])
+    else:
+        train_rec, dev_rec = [], []
+    tr = RescoreBertTrainer(weights, BERT_BASE, device=_dev(cfg), method=method,
+                            md_loss_weight=float(get(cfg, "md_loss_weight", 1.0)), lr=float(get(cfg, "lr", 1e-5)),
                             weight_decay=float(get(cfg, "weight_decay", 0.01)))
-    bs = int(get(cfg, "batch_size", 3))
-    losses, ckpts = [], []
-    for ep in range(int(get(cfg, "epochs", 1))):
-        if ep and get(cfg, "reset_optimizer", False):
+    bs, n_best = int(get(cfg, "batch_size", 1)), int(get(cfg, "n_best", 1))
+
+    def epoch_pass(f, update):
+        z = np.zeros(len(f["hyp_off"]) - 1, np.float32)
+        return rescorebert_epoch(tr, f["tokens"], f["hyp_off"], f["mlm_pll_score"], f.get("hyps_am_score", z),
+                                 f.get("hyps_cer", z), bs, n_best, update=update)
+    ckpts = []
+    try:
+        for ep in range(int(start) if resume else 1, int(get(cfg, "epoch", 1)) + 1):
+            print("Epoch {}/{}".format(ep, get(cfg, "epoch", 1)))
             tr.reset_optimizer()
-        tot = 0.0
-        for b0 in range(0, nb.n_utt, bs):
-            utts = list(range(b0, min(nb.n_utt, b0 + bs)))
-            sub = nb.subset(utts)
-            h0, h1 = nb.utt_off[utts[0]], nb.utt_off[utts[-1] + 1]
-            loss, _ = tr.step(sub.tokens, sub.hyp_off, sub.utt_off, target[h0:h1], am[h0:h1], err[h0:h1])
-            tot += loss
-        losses.append(tot / max(1, -(-nb.n_utt // bs)))
-        log.info(f"epoch {ep + 1} loss {losses[-1]}")
-        path = os.path.join(cfg.output_path, f"checkpoint_{ep + 1}.pt")
-        torch.save({k: torch.from_numpy(v) for k, v in tr.state_dict().items()}, path)
-        ckpts.append(path)
-    tr.close()
-    return {"losses": losses, "checkpoints": ckpts}
+            train_rec.append(epoch_pass(train_f, True))
+            print("epoch ", ep, " train loss: ", train_rec[-1], "\n")
+            if dev_f is not None and all(f in dev_f["features"] for f in need):
+                dev_rec.append(epoch_pass(dev_f, "loss"))
+                print("epoch ", ep, " dev loss: ", dev_rec[-1], "\n")
+            ckpts.append(_save_checkpoint(cfg.output_path, tr.state_dict(), ep))
+            D.json_saving(os.path.join(cfg.output_path, "loss.json"), {"train": train_rec, "dev": dev_rec})
+    finally:
+        tr.close()
+    return {"train_loss": train_rec, "dev_loss": dev_rec, "checkpoints": ckpts}
 
 
 def rescore(cfg) -> Dict[str, float]:

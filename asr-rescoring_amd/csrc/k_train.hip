@@ -126,12 +126,15 @@ __global__ void tr_bias_kernel(float* __restrict__ y, const float* __restrict__ 
 // K and V of the head staged in LDS; P (softmax probabilities) saved for the backward.
 // Eager transformers order: scores = (q . k) * scale; softmax = exp(s - max) / sum.
 __global__ void __launch_bounds__(64)
-tr_attn_fwd_kernel(const float* __restrict__ qkv, const int* __restrict__ seq_off,
+tr_attn_fwd_kernel(const float* __restrict__ qkv, const int* __restrict__ seq_off, const int* __restrict__ klen,
                    const long long* __restrict__ pofs, int H, int heads, float* __restrict__ P,
                    float* __restrict__ ctx) {
     extern __shared__ __attribute__((aligned(16))) float sm_a[];
     const int s = blockIdx.x, hd = blockIdx.y, tid = threadIdx.x;
     const int r0 = seq_off[s], T = seq_off[s + 1] - r0;
+    // keys j >= TK are padding (attention_mask 0): probability exactly 0, as the additive
+    // finfo.min mask gives; the backward then carries no gradient to or through them
+    const int TK = klen ? min(max(klen[s], 1), T) : T;
     const int ld = 3 * H;
     float* sK = sm_a;                 // [T][64]
     float* sV = sm_a + T * 64;        // [T][64]
@@ -152,7 +155,7 @@ tr_attn_fwd_kernel(const float* __restrict__ qkv, const int* __restrict__ seq_of
             qv[c] = v.x; qv[c + 1] = v.y; qv[c + 2] = v.z; qv[c + 3] = v.w;
         }
         float m = -INFINITY;
-        for (int j = 0; j < T; ++j) {
+        for (int j = 0; j < TK; ++j) {
             float d = 0.f;
 #pragma unroll
             for (int c = 0; c < 64; ++c) d += qv[c] * sK[j * 64 + c];
@@ -160,9 +163,10 @@ tr_attn_fwd_kernel(const float* __restrict__ qkv, const int* __restrict__ seq_of
             Ph[(long long)i * T + j] = d;
             m = fmaxf(m, d);
         }
+        for (int j = TK; j < T; ++j) Ph[(long long)i * T + j] = -INFINITY;
         float sum = 0.f;
         for (int j = 0; j < T; ++j) {
-            const float e = __expf(Ph[(long long)i * T + j] - m);
+            const float e = j < TK ? __expf(Ph[(long long)i * T + j] - m) : 0.f;
             Ph[(long long)i * T + j] = e;
             sum += e;
         }
@@ -337,6 +341,9 @@ __global__ void tr_word_grad_kernel(const float* __restrict__ dx0, const int* __
                                     float* __restrict__ dword) {
     const int u = blockIdx.x;
     const int tk = utok[u], a = toff[u], b = toff[u + 1];
+    // nn.Embedding(padding_idx = pad_token_id = 0) in BertEmbeddings: the pad id's lookups
+    // pass no gradient to its row (the tied MLM decoder's part is added elsewhere)
+    if (tk == 0) return;
     for (int c = threadIdx.x; c < H; c += blockDim.x) {
         float acc = 0.f;
         for (int k = a; k < b; ++k) acc += dx0[(size_t)rows[k] * H + c];
@@ -390,48 +397,61 @@ __global__ void tr_cls_bwd_kernel(const float* __restrict__ dsc, const float* __
     }
 }
 
-// Distillation losses (single block; utterances strided over threads, totals summed by
-// thread 0 in order).  See train.h for the definitions.
+// Distillation losses (single block; groups strided over threads, totals summed by thread 0
+// in order).  See train.h for the definitions; every step follows the torch forward /
+// autograd sequence of RescoreBert/main.py:104-147 in fp32 (softmax = exp(x - max) / sum,
+// log of the softmax OUTPUT for MWED as torch.log(score_distribution) does).
 // dsc and uloss are written by one thread and read by another across __syncthreads(): no
 // __restrict__ on them, so the compiler cannot move those accesses over the barriers (see
 // tr_ce_kernel).
 __global__ void tr_loss_kernel(const float* __restrict__ sc, const float* __restrict__ tgt,
-                               const float* __restrict__ am, const float* __restrict__ err,
-                               const int* __restrict__ utt_off, int n_utt, int n_hyp, int kind, float lam,
+                               const float* __restrict__ am, const float* __restrict__ cer,
+                               const int* __restrict__ utt_off, int n_utt, int n_hyp, int kind, float md_w,
                                float* dsc, float* uloss, float* __restrict__ loss) {
-    const float inv_n = 1.0f / (float)n_hyp;
-    for (int h = threadIdx.x; h < n_hyp; h += blockDim.x) dsc[h] = 2.0f * (sc[h] - tgt[h]) * inv_n;
+    const float wmd = kind == RS_LOSS_MD ? 1.0f : md_w;
+    for (int h = threadIdx.x; h < n_hyp; h += blockDim.x) dsc[h] = wmd * (2.0f * (sc[h] - tgt[h]));
     __syncthreads();
-    const float inv_u = 1.0f / (float)max(n_utt, 1);
     if (kind != RS_LOSS_MD) {
         for (int u = threadIdx.x; u < n_utt; u += blockDim.x) {
             const int a = utt_off[u], b = utt_off[u + 1];
             float l = 0.f;
             if (b > a) {
-                float m = -INFINITY, eb = 0.f;
-                for (int i = a; i < b; ++i) { m = fmaxf(m, am[i] + sc[i]); eb += err[i]; }
-                eb /= (float)(b - a);
                 if (kind == RS_LOSS_MWER) {
+                    // P = softmax(mix); MWER_g = sum P (e - sum e / n); d mix = P (d - sum P d)
+                    float m = -INFINITY, es = 0.f;
+                    for (int i = a; i < b; ++i) { m = fmaxf(m, sc[i] + am[i]); es += cer[i]; }
+                    const float avg = es / (float)(b - a);
                     float z = 0.f;
-                    for (int i = a; i < b; ++i) z += __expf(am[i] + sc[i] - m);
-                    for (int i = a; i < b; ++i) l += __expf(am[i] + sc[i] - m) / z * (err[i] - eb);
+                    for (int i = a; i < b; ++i) z += expf(sc[i] + am[i] - m);
+                    for (int i = a; i < b; ++i) l += expf(sc[i] + am[i] - m) / z * (cer[i] - avg);
                     for (int i = a; i < b; ++i) {
-                        const float p = __expf(am[i] + sc[i] - m) / z;
-                        dsc[i] += lam * inv_u * p * ((err[i] - eb) - l);
+                        const float p = expf(sc[i] + am[i] - m) / z;
+                        dsc[i] += p * ((cer[i] - avg) - l);
                     }
-                } else {                              // MWED
-                    float cs = 0.f, es = 0.f, me = -INFINITY;
-                    for (int i = a; i < b; ++i) { cs += am[i] + sc[i]; es -= err[i]; me = fmaxf(me, -err[i]); }
-                    const float tau = (es != 0.f && cs / es > 0.f) ? cs / es : 1.0f;
-                    float zs = 0.f, ze = 0.f, ms = -INFINITY;
-                    for (int i = a; i < b; ++i) ms = fmaxf(ms, (am[i] + sc[i]) / tau);
-                    for (int i = a; i < b; ++i) { zs += __expf((am[i] + sc[i]) / tau - ms); ze += __expf(-err[i] - me); }
+                } else {
+                    // E = softmax(e); T = sum mix / sum e; Q = softmax(mix / T);
+                    // KL = sum E (log E - log Q); d z = Q sum E - E; d T = sum d z (-mix / T^2);
+                    // d mix = d z / T + d T / sum e
+                    float me = -INFINITY, ze = 0.f, smix = 0.f, se = 0.f;
+                    for (int i = a; i < b; ++i) { me = fmaxf(me, cer[i]); smix += sc[i] + am[i]; se += cer[i]; }
+                    for (int i = a; i < b; ++i) ze += expf(cer[i] - me);
+                    const float T = smix / se;
+                    float mz = -INFINITY, zq = 0.f;
+                    for (int i = a; i < b; ++i) mz = fmaxf(mz, (sc[i] + am[i]) / T);
+                    for (int i = a; i < b; ++i) zq += expf((sc[i] + am[i]) / T - mz);
+                    float sE = 0.f;
+                    for (int i = a; i < b; ++i) sE += expf(cer[i] - me) / ze;
+                    float gT = 0.f;
                     for (int i = a; i < b; ++i) {
-                        const float de = __expf(-err[i] - me) / ze;
-                        const float lds = (am[i] + sc[i]) / tau - ms - __logf(zs);
-                        l -= de * lds;
-                        dsc[i] += lam * inv_u * (__expf(lds) - de) / tau;
+                        const float mix = sc[i] + am[i];
+                        const float E = expf(cer[i] - me) / ze;
+                        const float Q = expf(mix / T - mz) / zq;
+                        if (E > 0.f) l += E * (logf(E) - logf(Q));
+                        const float gz = Q * sE - E;
+                        gT += gz * (-mix / (T * T));
+                        dsc[i] += gz / T;
                     }
+                    for (int i = a; i < b; ++i) dsc[i] += gT / se;
                 }
             }
             uloss[u] = l;
@@ -444,7 +464,7 @@ __global__ void tr_loss_kernel(const float* __restrict__ sc, const float* __rest
         float x = 0.f;
         if (kind != RS_LOSS_MD)
             for (int u = 0; u < n_utt; ++u) x += uloss[u];
-        loss[0] = md * inv_n + lam * x * inv_u;
+        loss[0] = kind == RS_LOSS_MD ? md : x + md_w * md;
     }
 }
 
@@ -566,13 +586,13 @@ hipError_t tr_bias(float* y, const float* bias, int M, int N, hipStream_t s) {
 
 static size_t attn_smem(int tmax, bool bwd) { return (size_t)(2 * tmax * 64 + (bwd ? tmax * tmax : 0)) * 4; }
 
-hipError_t tr_attn_fwd(const float* qkv, const int* seq_off, const long long* pofs, int S, int tmax, int H,
-                       int heads, float* P, float* ctx, hipStream_t s) {
+hipError_t tr_attn_fwd(const float* qkv, const int* seq_off, const int* klen, const long long* pofs, int S,
+                       int tmax, int H, int heads, float* P, float* ctx, hipStream_t s) {
     if (S <= 0) return hipSuccess;
     const size_t sm = attn_smem(tmax, false);
     hipError_t e = hipFuncSetAttribute((const void*)tr_attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(tr_attn_fwd_kernel, dim3(S, heads), dim3(64), sm, s, qkv, seq_off, pofs, H, heads, P, ctx);
+    hipLaunchKernelGGL(tr_attn_fwd_kernel, dim3(S, heads), dim3(64), sm, s, qkv, seq_off, klen, pofs, H, heads, P, ctx);
     return hipGetLastError();
 }
 
@@ -631,8 +651,8 @@ hipError_t tr_cls_bwd(const float* dsc, const float* h, const int* seq_off, int 
 }
 
 hipError_t tr_loss(const float* sc, const float* tgt, const float* am, const float* err, const int* utt_off,
-                   int n_utt, int n_hyp, int kind, float lam, float* dsc, float* uloss, float* loss, hipStream_t s) {
-    hipLaunchKernelGGL(tr_loss_kernel, dim3(1), dim3(256), 0, s, sc, tgt, am, err, utt_off, n_utt, n_hyp, kind, lam,
+                   int n_utt, int n_hyp, int kind, float md_w, float* dsc, float* uloss, float* loss, hipStream_t s) {
+    hipLaunchKernelGGL(tr_loss_kernel, dim3(1), dim3(256), 0, s, sc, tgt, am, err, utt_off, n_utt, n_hyp, kind, md_w,
                        dsc, uloss, loss);
     return hipGetLastError();
 }

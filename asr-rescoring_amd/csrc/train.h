@@ -1,14 +1,14 @@
 // Training kernels (k_train.hip) used by the trainer (train_api.hip).
 //
-// Distillation losses of RescoreBert training (RescoreBert/main.py:104-154: MD, MD_MWER,
-// MD_MWED), restated from the RescoreBERT paper (parity unpinned):
-//   s_i  = CLS score of hypothesis i, t_i = its MLM PLL target, c_i = am_i + s_i,
-//   eps_i = word errors of hypothesis i (utterance u holds hypotheses a..b-1)
-//   MD   = (1/N) sum_i (s_i - t_i)^2                                 (torch MSELoss)
-//   MWER = (1/U) sum_u sum_i softmax(c)_i (eps_i - mean_u eps)
-//   MWED = (1/U) sum_u -sum_i softmax(-eps)_i log softmax(c / tau)_i,
-//          tau = sum_i c_i / sum_i (-eps_i) (1 when that is not positive), held constant
-//   loss = MD + lambda * (MWER | MWED)
+// Distillation losses of RescoreBert training, as RescoreBert/main.py:104-147 computes them
+// (groups g of consecutive hypotheses = the reference's reshape(-1, n_best)):
+//   s_i = CLS score, t_i = mlm_pll_score, c_i = s_i + hyps_am_score_i, e_i = hyps_cer_i
+//   MD      = sum_i (s_i - t_i)^2                                   (MSELoss(reduction="sum"))
+//   MD_MWER = sum_g sum_i softmax(c_g)_i (e_i - sum_g e / n_g) + w * MD
+//   MD_MWED = sum_g sum_i E_i (log E_i - log Q_i) + w * MD,           (kl_div(reduction="sum"))
+//             E = softmax(e_g), Q = softmax(c_g / T_g), T_g = sum c_g / sum e_g (T depends
+//             on s: its gradient is carried, as torch autograd does)
+//   MD alone has weight 1; w = md_loss_weight.
 #pragma once
 #include <hip/hip_runtime.h>
 #include "../../include/rescore.h"
@@ -21,8 +21,9 @@ hipError_t tr_bias_res_ln(float* y, const float* bias, const float* res, int M, 
 hipError_t tr_bias_gelu(float* pre, const float* bias, float* act, int M, int N, hipStream_t s);
 hipError_t tr_gelu_bwd(float* d, const float* pre, long long n, hipStream_t s);
 hipError_t tr_bias(float* y, const float* bias, int M, int N, hipStream_t s);
-hipError_t tr_attn_fwd(const float* qkv, const int* seq_off, const long long* pofs, int S, int tmax, int H,
-                       int heads, float* P, float* ctx, hipStream_t s);
+// klen (nullable): sequence s attends to its first klen[s] tokens only (padded-batch rows)
+hipError_t tr_attn_fwd(const float* qkv, const int* seq_off, const int* klen, const long long* pofs, int S,
+                       int tmax, int H, int heads, float* P, float* ctx, hipStream_t s);
 hipError_t tr_attn_bwd(const float* qkv, const float* P, const float* dctx, const int* seq_off, const long long* pofs,
                        int S, int tmax, int H, int heads, float* dqkv, hipStream_t s);
 hipError_t tr_ln_bwd(const float* dy, const float* x, const float2* st, const float* g, float* dx, int M, int H,
@@ -38,7 +39,7 @@ hipError_t tr_cls_fwd(const float* h, const int* seq_off, int S, int H, const fl
 hipError_t tr_cls_bwd(const float* dsc, const float* h, const int* seq_off, int S, int H, const float* w, float* dh,
                       float* dw, float* db, hipStream_t s);
 hipError_t tr_loss(const float* sc, const float* tgt, const float* am, const float* err, const int* utt_off,
-                   int n_utt, int n_hyp, int kind, float lam, float* dsc, float* uloss, float* loss, hipStream_t s);
+                   int n_utt, int n_hyp, int kind, float md_w, float* dsc, float* uloss, float* loss, hipStream_t s);
 hipError_t tr_ce(float* logits, const int* labels, int M, int V, float* row_loss, float* loss, hipStream_t s);
 hipError_t tr_adamw(float* p, const float* g, float* m, float* v, long long n, float decay, float b1w, float b2,
                     float b2w, float step_size, float bc2_sqrt, float eps, hipStream_t s);

@@ -247,7 +247,7 @@ struct StepCtx {
     const int* dm = nullptr;
     const long long* pofs = nullptr;
     const int* seq = nullptr;
-    size_t i_tok = 0, i_pos = 0, i_aux = 0, i_utok = 0, i_toff = 0, i_ord = 0;
+    size_t i_tok = 0, i_pos = 0, i_aux = 0, i_utok = 0, i_toff = 0, i_ord = 0, i_klen = 0;
     float* x0 = nullptr;
     float2* st0 = nullptr;
     struct LA { float *hin, *qkv, *P, *ctx, *x1, *h1, *pre, *act, *x2; float2 *st1, *st2; };
@@ -258,8 +258,10 @@ struct StepCtx {
     float2* tst = nullptr;
 };
 
-// host metadata + buffers.  aux: extra int32 array uploaded with the metadata (utt_off).
-int prepare(StepCtx& c, const int32_t* d_tok, const int32_t* h_off, int n_seq, const std::vector<int>& aux) {
+// host metadata + buffers.  aux: extra int32 array uploaded with the metadata (utt_off);
+// h_klen (nullable): per-sequence key lengths (padded-batch rows, rs_train_step_mlm).
+int prepare(StepCtx& c, const int32_t* d_tok, const int32_t* h_off, int n_seq, const std::vector<int>& aux,
+            const int32_t* h_klen = nullptr) {
     rs_trainer* t = c.t;
     const rs_bert_cfg& cf = t->cfg;
     const int H = cf.hidden, F = cf.intermediate, nh = cf.heads, NL = cf.layers;
@@ -273,6 +275,10 @@ int prepare(StepCtx& c, const int32_t* d_tok, const int32_t* h_off, int n_seq, c
     }
     if (c.tmax > cf.max_pos) return rs_fail(RS_EUNSUP, "sequence longer than max_position_embeddings");
     if (c.tmax > 128) return rs_fail(RS_EUNSUP, "training sequences are limited to 128 tokens");
+    if (h_klen)
+        for (int s = 0; s < n_seq; ++s)
+            if (h_klen[s] < 1 || h_klen[s] > h_off[s + 1] - h_off[s])
+                return rs_fail(RS_EARG, "key length outside 1..row length");
     const int M = c.M, S = c.S;
     hipStream_t st = c.st;
     TRY_HIP(hipSetDevice(t->device));
@@ -301,7 +307,7 @@ int prepare(StepCtx& c, const int32_t* d_tok, const int32_t* h_off, int n_seq, c
         const long long T = h_off[s + 1] - h_off[s];
         pofs[s + 1] = pofs[s] + (long long)nh * T * T;
     }
-    // int layout: pofs (int64) | row_tok | row_pos | seq_off | aux | utok | toff | order
+    // int layout: pofs (int64) | row_tok | row_pos | seq_off | aux | utok | toff | order | klen
     std::vector<int>& hm = t->h_meta;
     hm.assign(2 * (S + 1), 0);
     std::memcpy(hm.data(), pofs.data(), (S + 1) * 8);
@@ -319,6 +325,11 @@ int prepare(StepCtx& c, const int32_t* d_tok, const int32_t* h_off, int n_seq, c
     hm.insert(hm.end(), toff.begin(), toff.end());
     c.i_ord = hm.size();
     hm.insert(hm.end(), order.begin(), order.end());
+    c.i_klen = 0;
+    if (h_klen) {
+        c.i_klen = hm.size();
+        hm.insert(hm.end(), h_klen, h_klen + S);
+    }
     TRY_HIP(t->meta.ensure(hm.size() * 4));
     TRY_HIP(hipMemcpyAsync(t->meta.p, hm.data(), hm.size() * 4, hipMemcpyHostToDevice, st));
     c.dm = (const int*)t->meta.p;
@@ -392,7 +403,8 @@ int encoder_forward(StepCtx& c) {
         StepCtx::LA& a = c.la[l];
         TRY_BLAS(gemm_nt(bh, M, 3 * H, H, a.hin, Pm + L.wqkv, a.qkv, 0.f));
         TRY_HIP(tr_bias(a.qkv, Pm + L.bqkv, M, 3 * H, st));
-        TRY_HIP(tr_attn_fwd(a.qkv, c.seq, c.pofs, c.S, c.tmax, H, nh, a.P, a.ctx, st));
+        TRY_HIP(tr_attn_fwd(a.qkv, c.seq, c.i_klen ? c.dm + c.i_klen : nullptr, c.pofs, c.S, c.tmax, H, nh, a.P,
+                            a.ctx, st));
         TRY_BLAS(gemm_nt(bh, M, H, H, a.ctx, Pm + L.wo, a.x1, 0.f));
         TRY_HIP(tr_bias_res_ln(a.x1, Pm + L.bo, a.hin, M, Pm + L.g1, Pm + L.be1, cf.ln_eps, H, a.st1, a.h1, st));
         TRY_BLAS(gemm_nt(bh, M, F, H, a.h1, Pm + L.w1, a.pre, 0.f));
@@ -452,7 +464,7 @@ int encoder_backward(StepCtx& c) {
 }
 
 int adamw(rs_trainer* t, const rs_train_opts* o, hipStream_t st) {
-    if (!o->update) return RS_OK;
+    if (o->update != 1) return RS_OK;
     t->step += 1;
     const double bc1 = 1.0 - std::pow((double)o->beta1, (double)t->step);
     const double bc2 = 1.0 - std::pow((double)o->beta2, (double)t->step);
@@ -494,7 +506,12 @@ int rs_train_step_cls(rs_trainer* t, const int32_t* d_tok, const int32_t* h_hyp_
     hipStream_t st = c.st;
     TRY_HIP(tr_cls_fwd(hfin, c.seq, S, H, Pm + t->o_wl, Pm + t->o_bl, sc, st));
     if (d_scores) TRY_HIP(hipMemcpyAsync(d_scores, sc, (size_t)S * 4, hipMemcpyDeviceToDevice, st));
-    TRY_HIP(tr_loss(sc, d_target, d_am, d_err, c.dm + c.i_aux, n_utt, S, o->loss, o->lambda_, dsc, uloss, d_loss, st));
+    TRY_HIP(tr_loss(sc, d_target, d_am, d_err, c.dm + c.i_aux, n_utt, S, o->loss, o->md_loss_weight, dsc, uloss,
+                    d_loss, st));
+    if (o->update < 0) {                      // loss only (the reference's dev pass)
+        TRY_HIP(hipStreamSynchronize(st));
+        return RS_OK;
+    }
     TRY_HIP(hipMemsetAsync(Gm, 0, t->n_params * 4, st));
     TRY_HIP(hipMemsetAsync(c.dA, 0, (size_t)c.M * H * 4, st));
     TRY_HIP(tr_cls_bwd(dsc, hfin, c.seq, S, H, Pm + t->o_wl, c.dA, Gm + t->o_wl, Gm + t->o_bl, st));
@@ -505,7 +522,8 @@ int rs_train_step_cls(rs_trainer* t, const int32_t* d_tok, const int32_t* h_hyp_
 }
 
 int rs_train_step_mlm(rs_trainer* t, const int32_t* d_ids, const int32_t* h_seq_off, int32_t n_seq,
-                      const int32_t* d_labels, const rs_train_opts* o, float* d_loss, void* stream) {
+                      const int32_t* h_key_len, const int32_t* d_labels, const rs_train_opts* o, float* d_loss,
+                      void* stream) {
     if (!t || !h_seq_off || !o || !d_loss || n_seq <= 0 || !d_ids || !d_labels)
         return rs_fail(RS_EARG, "null argument / empty batch");
     if (!t->finalized) return rs_fail(RS_ESTATE, "rs_trainer_finalize not called");
@@ -513,7 +531,7 @@ int rs_train_step_mlm(rs_trainer* t, const int32_t* d_ids, const int32_t* h_seq_
     StepCtx c;
     c.t = t;
     c.st = (hipStream_t)stream;
-    if (int r = prepare(c, d_ids, h_seq_off, n_seq, {})) return r;
+    if (int r = prepare(c, d_ids, h_seq_off, n_seq, {}, h_key_len)) return r;
     if (int r = encoder_forward(c)) return r;
     const rs_bert_cfg& cf = t->cfg;
     const int H = cf.hidden, V = cf.vocab, M = c.M;
@@ -529,6 +547,10 @@ int rs_train_step_mlm(rs_trainer* t, const int32_t* d_ids, const int32_t* h_seq_
     TRY_HIP(tr_bias(c.logits, Pm + t->o_db, M, V, st));
     float* rl = c.tail;
     TRY_HIP(tr_ce(c.logits, d_labels, M, V, rl, d_loss, st));       // logits <- dlogits
+    if (o->update < 0) {                      // loss only (the reference's dev pass)
+        TRY_HIP(hipStreamSynchronize(st));
+        return RS_OK;
+    }
     TRY_HIP(hipMemsetAsync(Gm, 0, t->n_params * 4, st));
     float* dT = c.dB;
     float* dT2 = c.dF;

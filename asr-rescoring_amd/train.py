@@ -1,4 +1,5 @@
-"""RescoreBert distillation training on the GPU (RescoreBert/main.py:104-229).
+"""RescoreBert distillation training and MLM fine-tuning on the GPU (SURVEY §8f item 2;
+RescoreBert/main.py:82-229, MLM_PLL/main.py:73-161).
 
 ``RescoreBertTrainer`` keeps the fp32 parameters, gradients and AdamW moments of a
 ``RescoreBert`` (BERT encoder + ``Linear(H, 1)`` on the CLS hidden state,
@@ -6,13 +7,20 @@ RescoreBert/model.py:4-21) resident on one GPU; ``step`` runs the native trainin
 (``rs_train_step_cls``): forward with saved activations, the distillation loss, the backward
 through head, encoder and embeddings, and one ``torch.optim.AdamW`` update.
 
-Losses (restated from the RescoreBERT paper; the reference's loss code was not consulted
-this round, so their parity is unpinned — the backward and the optimizer are checked against
-torch autograd + ``torch.optim.AdamW`` on the same loss, tests/test_gpu_train.py):
-  MD       mean_i (s_i - t_i)^2, t_i = the hypothesis' MLM PLL (the teacher)
-  MD_MWER  MD + lambda * mean_u sum_i softmax(am + s)_i (err_i - mean err)
-  MD_MWED  MD + lambda * mean_u -sum_i softmax(-err)_i log softmax((am + s) / tau)_i
-Dropout is not applied (the step is deterministic and bitwise reproducible).
+Losses exactly as RescoreBert/main.py:104-147 computes them (``csrc/train.h``), over groups of
+consecutive hypotheses (the reference's ``reshape(-1, n_best)``; ``reference_groups``):
+  MD       sum_i (s_i - t_i)^2                     (MSELoss(reduction="sum"); t = mlm_pll_score)
+  MD_MWER  sum_g sum_i softmax(s + am)_i (cer_i - mean_g cer) + md_loss_weight * MD
+  MD_MWED  sum_g KL(softmax(cer) || softmax((s + am) / T)) + md_loss_weight * MD,
+           T = sum(s + am) / sum(cer) per group, differentiated through
+Pinned against the reference's own training loop (tests/golden/make_golden_train.py, F6/F7:
+losses, dev scores and parameter updates after two epochs).  Dropout is not applied (the
+fixtures switch it off through the model config; the reference's p = 0.1 mask is RNG-bound).
+
+``MLMTrainer`` (BertForMaskedLM, decoder tied to the word embeddings) takes the reference's
+padded batches (``pad_rows``: collate of MLM_PLL/main.py:28-54 — ids and labels padded with
+0, pad positions are queries but not keys) and averages the CE over every position,
+[PAD]-labelled pads included, as BertForMaskedLM's loss does there.
 """
 from __future__ import annotations
 
@@ -59,15 +67,18 @@ class _Trainer:
     HEAD = "cls"
 
     def __init__(self, weights: Dict[str, np.ndarray], shape: BertShape = BERT_BASE, device=0,
-                 loss: str = "MD", lam: float = 1.0, lr: float = 1e-5, betas=(0.9, 0.999), eps: float = 1e-8,
-                 weight_decay: float = 0.01):
+                 method: str = "MD", md_loss_weight: float = 1.0, lr: float = 1e-5, betas=(0.9, 0.999),
+                 eps: float = 1e-8, weight_decay: float = 0.01):
         if not torch.cuda.is_available():
             raise RuntimeError("librescore needs a HIP GPU (no CPU fallback)")
         self.lib = _lib.load()
         self.shape = shape
         self.device = torch.device("cuda", device if isinstance(device, int) else torch.device(device).index)
         torch.cuda.set_device(self.device)
-        self.opts = _lib.RsTrainOpts(_lib.RS_LOSS[loss], lam, lr, betas[0], betas[1], eps, weight_decay, 1)
+        if method not in _lib.RS_LOSS:
+            raise ValueError(f"unknown method {method!r} (MD, MD_MWER, MD_MWED)")
+        self.opts = _lib.RsTrainOpts(_lib.RS_LOSS[method], md_loss_weight, lr, betas[0], betas[1], eps,
+                                     weight_decay, 1)
         self.shapes = param_shapes(shape, self.HEAD)
         self.extra = {k: np.asarray(v) for k, v in weights.items()
                       if k.startswith("bert.pooler.") or (self.HEAD == "mlm" and k.startswith("cls.predictions.decoder."))}
@@ -101,7 +112,14 @@ class _Trainer:
             pass
 
     def reset_optimizer(self):
+        """A fresh AdamW (moments and step count zeroed): the reference builds its optimizer
+        inside every run_one_epoch (RescoreBert/main.py:83-86, MLM_PLL/main.py:74-77)."""
         _lib.check(self.lib.rs_trainer_reset_optimizer(self.handle))
+
+    @staticmethod
+    def _update_flag(update) -> int:
+        """True: backward + AdamW step; False: backward only; "loss": forward + loss only."""
+        return -1 if update == "loss" else int(bool(update))
 
     def _get(self, fn, key: str) -> np.ndarray:
         shp = self.shapes[key]
@@ -130,19 +148,22 @@ class _Trainer:
 class RescoreBertTrainer(_Trainer):
     HEAD = "cls"
 
-    def step(self, tokens, hyp_off, utt_off, target, am=None, err=None, update: bool = True
+    def step(self, tokens, hyp_off, utt_off, target, am=None, cer=None, update=True
              ) -> Tuple[float, np.ndarray]:
-        """One training step on a batch of utterances; returns (loss, CLS scores before the update)."""
+        """One step on a batch (RescoreBert/main.py:98-154): ``utt_off`` groups the hypotheses
+        (``reference_groups``), ``target`` = mlm_pll_score, ``am`` = hyps_am_score, ``cer`` =
+        hyps_cer.  ``update``: True (backward + AdamW), False (gradients only) or "loss"
+        (forward only).  Returns (loss, CLS scores before the update)."""
         hoff = np.ascontiguousarray(hyp_off, np.int32)
         uoff = np.ascontiguousarray(utt_off, np.int32)
         n = len(hoff) - 1
         dev = self.device
         d_tok = torch.as_tensor(np.ascontiguousarray(tokens, np.int32)).to(dev)
         f32 = lambda a: None if a is None else torch.as_tensor(np.asarray(a, np.float32)).to(dev)
-        d_t, d_am, d_err = f32(target), f32(am), f32(err)
+        d_t, d_am, d_err = f32(target), f32(am), f32(cer)
         sc = torch.empty(n, dtype=torch.float32, device=dev)
         loss = torch.empty(1, dtype=torch.float32, device=dev)
-        self.opts.update = int(update)
+        self.opts.update = self._update_flag(update)
         _lib.check(self.lib.rs_train_step_cls(self.handle, _lib.ptr(d_tok), hoff.ctypes.data, n, uoff.ctypes.data,
                                               len(uoff) - 1, _lib.ptr(d_t), _lib.ptr(d_am), _lib.ptr(d_err),
                                               ctypes.byref(self.opts), _lib.ptr(sc), _lib.ptr(loss),
@@ -165,19 +186,83 @@ def do_job_rows(hyps: Sequence[Sequence[int]], mask_id: int = 103):
     return np.asarray(ids, np.int32), np.asarray(off, np.int32), np.asarray(labels, np.int32)
 
 
+def reference_groups(n_rows: int, n_best: int) -> np.ndarray:
+    """Group offsets of a RescoreBert training batch: consecutive runs of ``n_best`` rows, as
+    ``mix_score.reshape(-1, config.n_best)`` forms them (RescoreBert/main.py:116,132)."""
+    if n_best <= 0 or n_rows % n_best:
+        raise ValueError(f"batch of {n_rows} hypotheses does not reshape to (-1, {n_best})")
+    return np.arange(0, n_rows + 1, n_best, dtype=np.int32)
+
+
+def pad_rows(seqs: Sequence[Sequence[int]], labels: Sequence[Sequence[int]]):
+    """The reference's MLM batch (collate, MLM_PLL/main.py:28-54): every row padded to the
+    batch's longest with id 0 and label 0 (pad_sequence); the attention mask's zeros become
+    key lengths.  Returns (ids, row_off, labels, key_len) as int32."""
+    T = max(len(x) for x in seqs)
+    n = len(seqs)
+    ids = np.zeros((n, T), np.int32)
+    lab = np.zeros((n, T), np.int32)
+    klen = np.empty(n, np.int32)
+    for i, (x, y) in enumerate(zip(seqs, labels)):
+        ids[i, :len(x)] = x
+        lab[i, :len(y)] = y
+        klen[i] = len(x)
+    return ids.ravel(), np.arange(0, n * T + 1, T, dtype=np.int32), lab.ravel(), klen
+
+
 class MLMTrainer(_Trainer):
-    """MLM fine-tuning (MLM_PLL/main.py:117-161): BertForMaskedLM, CE over every real position
-    of each row (mean), AdamW.  Rows are ragged (no padding positions in the loss)."""
+    """MLM fine-tuning (MLM_PLL/main.py:73-161): BertForMaskedLM, CE over every position of the
+    (padded) rows, mean; AdamW.  ``key_len`` marks each row's padding (``pad_rows``); without
+    it the rows are ragged and every position is real."""
     HEAD = "mlm"
 
-    def step(self, ids, seq_off, labels, update: bool = True) -> float:
+    def step(self, ids, seq_off, labels, key_len=None, update=True) -> float:
         off = np.ascontiguousarray(seq_off, np.int32)
+        kl = None if key_len is None else np.ascontiguousarray(key_len, np.int32)
+        if kl is not None and len(kl) != len(off) - 1:
+            raise ValueError("key_len needs one entry per row")
         dev = self.device
         d_ids = torch.as_tensor(np.ascontiguousarray(ids, np.int32)).to(dev)
         d_lab = torch.as_tensor(np.ascontiguousarray(labels, np.int32)).to(dev)
         loss = torch.empty(1, dtype=torch.float32, device=dev)
-        self.opts.update = int(update)
+        self.opts.update = self._update_flag(update)
         _lib.check(self.lib.rs_train_step_mlm(self.handle, _lib.ptr(d_ids), off.ctypes.data, len(off) - 1,
-                                              _lib.ptr(d_lab), ctypes.byref(self.opts), _lib.ptr(loss),
-                                              _lib.stream_ptr(dev)))
+                                              None if kl is None else kl.ctypes.data, _lib.ptr(d_lab),
+                                              ctypes.byref(self.opts), _lib.ptr(loss), _lib.stream_ptr(dev)))
         return float(loss.item())
+
+
+def rescorebert_epoch(tr: RescoreBertTrainer, tokens, hyp_off, target, am, cer, batch_size: int, n_best: int,
+                      update=True) -> float:
+    """One pass of RescoreBert/main.py:82-163 run_one_epoch(train=True) over the hypotheses in
+    order: batches of ``batch_size * n_best`` rows (set_dataloader :71-79, shuffle False),
+    groups of ``n_best`` (``reference_groups``); ``update`` True = grad_update (the caller
+    resets AdamW first, as the reference builds it per call), "loss" = the dev pass.
+    Returns the epoch loss (mean of the batch losses)."""
+    hoff = np.asarray(hyp_off, np.int64)
+    n = len(hoff) - 1
+    rows = batch_size * n_best
+    tot, nb = 0.0, 0
+    for b0 in range(0, n, rows):
+        b1 = min(n, b0 + rows)
+        t0, t1 = int(hoff[b0]), int(hoff[b1])
+        loss, _ = tr.step(np.asarray(tokens[t0:t1]), (hoff[b0:b1 + 1] - t0).astype(np.int32),
+                          reference_groups(b1 - b0, n_best), target[b0:b1], am[b0:b1], cer[b0:b1], update=update)
+        tot += loss
+        nb += 1
+    return tot / max(nb, 1)
+
+
+def mlm_epoch(tr: MLMTrainer, seqs: Sequence[Sequence[int]], labels: Sequence[Sequence[int]], batch_size: int,
+              update=True, order=None) -> float:
+    """One pass of MLM_PLL/main.py:73-114 run_one_epoch (do_scoring False) over do_job rows:
+    batches of ``batch_size`` rows (in ``order``, default as given), padded as the reference's
+    collate pads them (``pad_rows``).  Returns the epoch loss (mean of the batch losses)."""
+    idx = np.arange(len(seqs)) if order is None else np.asarray(order)
+    tot, nb = 0.0, 0
+    for b0 in range(0, len(idx), batch_size):
+        sel = idx[b0:b0 + batch_size]
+        ids, off, lab, klen = pad_rows([seqs[i] for i in sel], [labels[i] for i in sel])
+        tot += tr.step(ids, off, lab, klen, update=update)
+        nb += 1
+    return tot / max(nb, 1)

@@ -39,9 +39,9 @@ extern "C" {
 #define RS_HEAD_CLS 2     /* RescoreBert head: linear.weight [1,H], linear.bias [1] */
 #define RS_HEAD_EMB 4     /* encoder only: token embeddings (BERTScore, bert_score.utils.bert_encode) */
 
-#define RS_LOSS_MD 0      /* RescoreBert training losses (RescoreBert/main.py:104-154) */
-#define RS_LOSS_MWER 1    /* MD + lambda * MWER */
-#define RS_LOSS_MWED 2    /* MD + lambda * MWED */
+#define RS_LOSS_MD 0      /* RescoreBert training methods (RescoreBert/main.py:104-147) */
+#define RS_LOSS_MWER 1    /* MD_MWER: MWER + md_loss_weight * MD */
+#define RS_LOSS_MWED 2    /* MD_MWED: MWED + md_loss_weight * MD */
 
 #define RS_BS_P 0         /* BERTScore component used as the MBR utility */
 #define RS_BS_R 1
@@ -168,19 +168,24 @@ int rs_bertscore_recall(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_
 int rs_mbr_scores_bs(const float* d_rmat, const int64_t* d_mat_off, const int32_t* d_utt_off, int32_t n_utt,
                      int32_t k, int32_t which, float* d_scores, int32_t* d_argmax, void* stream);
 
-/* ---- RescoreBert training (RescoreBert/main.py:104-229) --------------------------------
+/* ---- RescoreBert training (RescoreBert/main.py:82-229) ---------------------------------
  * A trainer holds fp32 parameters (HF keys as for rs_model; bert.pooler.* is accepted and
  * ignored — RescoreBert's loss never reaches it), their gradients and AdamW moments.
  * rs_train_step_cls runs forward (activations kept), the distillation loss, the full
- * backward and (opts->update) one torch.optim.AdamW step.  Losses (train.h):
- *   MD = mean_i (s_i - t_i)^2;  MWER / MWED per utterance over c_i = am_i + s_i;
- *   loss = MD + lambda * (MWER | MWED).  Dropout is not applied. */
+ * backward and (opts->update) one torch.optim.AdamW step.  Losses (RescoreBert/main.py:104-147;
+ * train.h), over utterance groups g given by h_utt_off (the reference's reshape(-1, n_best)):
+ *   MD      = sum_i (s_i - t_i)^2                            (MSELoss(reduction="sum"))
+ *   MD_MWER = sum_g sum_i softmax(c_g)_i (cer_i - mean_g cer) + md_loss_weight * MD
+ *   MD_MWED = sum_g KL(softmax(cer_g) || softmax(c_g / T_g)) + md_loss_weight * MD,
+ *             T_g = sum c_g / sum cer_g (differentiated through), c = s + am.
+ * Dropout is not applied (the reference's p = 0.1 mask is RNG-bound). */
 typedef struct rs_trainer rs_trainer;
 typedef struct rs_train_opts {
     int32_t loss;          /* RS_LOSS_MD / RS_LOSS_MWER / RS_LOSS_MWED */
-    float lambda_;         /* weight of the MWER / MWED term */
+    float md_loss_weight;  /* weight of MD in MD_MWER / MD_MWED (MD alone has weight 1) */
     float lr, beta1, beta2, eps, weight_decay;   /* torch.optim.AdamW arguments */
-    int32_t update;        /* 0: gradients only (no optimizer step) */
+    int32_t update;        /* 1: backward + AdamW step; 0: backward only (gradients kept);
+                              -1: forward + loss only (the reference's dev-loss pass) */
 } rs_train_opts;
 
 /* cfg->heads_mask: RS_HEAD_CLS (RescoreBert) or RS_HEAD_MLM (MLM fine-tuning); shapes as
@@ -190,19 +195,25 @@ int rs_trainer_set_tensor(rs_trainer* t, const char* hf_key, const void* host_pt
                           const int64_t* shape, int ndim);
 int rs_trainer_finalize(rs_trainer* t);
 /* d_tok/h_hyp_off as rs_cls_score; h_utt_off int32 [n_utt+1] groups hypotheses by utterance;
- * d_target (PLL), d_am, d_err (word errors) float32 [n_hyp] (am/err only for MWER/MWED);
+ * d_target (mlm_pll_score), d_am (hyps_am_score), d_err (hyps_cer) float32 [n_hyp] (am/err
+ * only for MWER/MWED);
  * d_scores (nullable) float32 [n_hyp] out; d_loss float32 [1] out.  Synchronises `stream`. */
 int rs_train_step_cls(rs_trainer* t, const int32_t* d_tok, const int32_t* h_hyp_off, int32_t n_hyp,
                       const int32_t* h_utt_off, int32_t n_utt, const float* d_target, const float* d_am,
                       const float* d_err, const rs_train_opts* opts, float* d_scores, float* d_loss,
                       void* stream);
-/* MLM fine-tuning step (MLM_PLL/main.py:117-161 mlm_finetune_bert; trainer created with
- * heads_mask RS_HEAD_MLM — cls.predictions.* with the decoder tied to the word embeddings):
- * d_ids / d_labels ragged int32 rows (h_seq_off host int32 [n_seq+1]), e.g. do_job rows of
- * the reference texts (one [MASK] per row, labels = the unmasked tokens); loss = mean over
- * all real positions of the CE of BertForMaskedLM's logits.  Synchronises `stream`. */
+/* MLM fine-tuning step (MLM_PLL/main.py:73-161 run_one_epoch / mlm_finetune_bert; trainer
+ * created with heads_mask RS_HEAD_MLM — cls.predictions.* with the decoder tied to the word
+ * embeddings): d_ids / d_labels int32 rows (h_seq_off host int32 [n_seq+1]).  h_key_len (host
+ * int32 [n_seq], nullable = whole rows): row s attends to its first h_key_len[s] tokens only —
+ * the reference's padded batch (collate MLM_PLL/main.py:28-54: ids / labels padded with 0,
+ * attention_mask 0) is rows of the batch's longest length whose pad positions are queries but
+ * not keys.  loss = mean over ALL positions of the rows (pads included, label 0) of the CE of
+ * BertForMaskedLM's logits (modeling_bert CrossEntropyLoss, MLM_PLL/main.py:89-97).
+ * Synchronises `stream`. */
 int rs_train_step_mlm(rs_trainer* t, const int32_t* d_ids, const int32_t* h_seq_off, int32_t n_seq,
-                      const int32_t* d_labels, const rs_train_opts* opts, float* d_loss, void* stream);
+                      const int32_t* h_key_len, const int32_t* d_labels, const rs_train_opts* opts,
+                      float* d_loss, void* stream);
 /* Synchronous copies of one parameter / its last gradient (numel must match). */
 int rs_trainer_get_tensor(rs_trainer* t, const char* hf_key, void* host_out, int64_t numel);
 int rs_trainer_get_grad(rs_trainer* t, const char* hf_key, void* host_out, int64_t numel);

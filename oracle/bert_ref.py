@@ -62,7 +62,9 @@ class TorchBert:
         B, T = input_ids.shape
         pos = torch.arange(T, device=self.device)
         e = "bert.embeddings."
-        x = (self.w[e + "word_embeddings.weight"][input_ids]
+        # nn.Embedding(padding_idx=pad_token_id) (modeling_bert BertEmbeddings): the lookup of
+        # the pad id passes no gradient to its row (the tied decoder still does)
+        x = (Fn.embedding(input_ids, self.w[e + "word_embeddings.weight"], padding_idx=s.pad_id)
              + self.w[e + "token_type_embeddings.weight"][0]
              + self.w[e + "position_embeddings.weight"][pos][None])
         x = self._ln(x, e + "LayerNorm")

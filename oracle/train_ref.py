@@ -1,11 +1,18 @@
-"""ORACLE (test infrastructure only) — torch autograd + torch.optim.AdamW restatement of a
-RescoreBert distillation training step, used to check the native trainer (train_api.hip).
+"""ORACLE (test infrastructure only) — torch autograd + torch.optim.AdamW restatement of the
+reference's training steps, used to check the native trainer (train_api.hip).
 
-Model: ``oracle.bert_ref.TorchBert`` (pinned against the reference's own RescoreBert via the
-golden fixtures) with every parameter a leaf tensor; a batch is padded to its longest
-hypothesis (``RescoreBert/main.py:31-79`` collate: pad 0, attention mask), scores are the CLS
-linear head.  Losses as ``asr_rescoring_amd/csrc/train.h`` (restated from the RescoreBERT
-paper — **parity unpinned** against the reference's loss code).  No dropout.
+Model: ``oracle.bert_ref.TorchBert`` (pinned against transformers via the golden fixtures)
+with every parameter a leaf tensor, no dropout.
+  * RescoreBert (RescoreBert/main.py:31-79 collate + :98-154 run_one_epoch): a batch is padded
+    to its longest hypothesis (pad 0, attention mask), scores are the CLS linear head, and the
+    losses are the reference's expressions (``rescorebert_loss``).
+  * MLM fine-tuning (MLM_PLL/main.py:28-54 collate + :73-114 run_one_epoch): rows padded with
+    id 0 and label 0, CE over every position of the padded batch (CrossEntropyLoss mean over
+    B*T, the [PAD]-labelled pads included), as BertForMaskedLM computes it there.
+  * ``train_rescorebert`` / ``train_mlm``: the reference's epoch loop (batches in order, a new
+    AdamW every epoch, epoch loss = mean of the batch losses, dev loss without updates).
+Pinned against the reference's own training runs by tests/test_oracle_golden.py (fixtures
+F6/F7 of tests/golden/make_golden_train.py).
 """
 from __future__ import annotations
 
@@ -15,6 +22,27 @@ import numpy as np
 import torch
 
 from .bert_ref import TorchBert
+
+
+def rescorebert_loss(sc: torch.Tensor, target, am, cer, n_best: int, method: str, md_loss_weight: float):
+    """RescoreBert/main.py:104-147 on one batch (float32 tensors of the batch's rows)."""
+    t = torch.as_tensor(np.asarray(target, np.float32))
+    md = torch.nn.MSELoss(reduction="sum")(sc, t)
+    if method == "MD":
+        return md
+    a = torch.as_tensor(np.asarray(am, np.float32))
+    c = torch.as_tensor(np.asarray(cer, np.float32)).reshape(-1, n_best)
+    mix = (sc + a).reshape(-1, n_best)
+    if method == "MD_MWER":
+        p = torch.softmax(mix, dim=-1)
+        avg = (torch.sum(c, dim=-1) / n_best).unsqueeze(dim=-1)
+        return torch.sum(torch.mul(p, c - avg)) + md_loss_weight * md
+    if method == "MD_MWED":
+        err = torch.softmax(c, dim=-1)
+        temp = (torch.sum(mix, dim=-1) / torch.sum(c, dim=-1)).unsqueeze(dim=-1)
+        q = torch.softmax(mix / temp, dim=-1)
+        return torch.nn.functional.kl_div(torch.log(q), err, reduction="sum") + md_loss_weight * md
+    raise ValueError(method)
 
 
 class TorchTrainer:
@@ -27,8 +55,11 @@ class TorchTrainer:
         self.model = TorchBert({k: np.array(v, np.float32, copy=True) for k, v in weights.items() if keep(k)}, shape)
         for t in self.model.w.values():
             t.requires_grad_(True)
-        self.opt = torch.optim.AdamW(list(self.model.w.values()), lr=lr, betas=betas, eps=eps,
-                                     weight_decay=weight_decay)
+        self.hp = dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay)
+        self.reset_optimizer()
+
+    def reset_optimizer(self):
+        self.opt = torch.optim.AdamW(list(self.model.w.values()), **self.hp)
 
     def scores(self, seqs: Sequence[Sequence[int]]) -> torch.Tensor:
         T = max(len(s) for s in seqs)
@@ -39,32 +70,15 @@ class TorchTrainer:
             am[i, :len(s)] = 1
         return self.model.cls_score(self.model.encoder(ids, am))
 
-    @staticmethod
-    def loss(sc, target, am, err, utt_off, kind: str, lam: float):
-        t = torch.as_tensor(np.asarray(target, np.float32))
-        md = ((sc - t) ** 2).mean()
-        if kind == "MD":
-            return md
-        a = torch.as_tensor(np.asarray(am, np.float32))
-        e = torch.as_tensor(np.asarray(err, np.float32))
-        terms = []
-        for u in range(len(utt_off) - 1):
-            i0, i1 = int(utt_off[u]), int(utt_off[u + 1])
-            c, eu = a[i0:i1] + sc[i0:i1], e[i0:i1]
-            if kind == "MD_MWER":
-                terms.append((torch.softmax(c, 0) * (eu - eu.mean())).sum())
-            else:
-                cs, es = float(c.detach().sum()), float(-eu.sum())
-                tau = cs / es if es != 0.0 and cs / es > 0.0 else 1.0
-                terms.append(-(torch.softmax(-eu, 0) * torch.log_softmax(c / tau, 0)).sum())
-        return md + lam * torch.stack(terms).mean()
-
-    def step(self, seqs, utt_off, target, am=None, err=None, kind="MD", lam=1.0, update=True):
+    def step(self, seqs, target, am=None, cer=None, n_best=1, method="MD", md_loss_weight=1.0, update=True):
+        """update: True (backward + AdamW), False (backward only), "loss" (no backward)."""
         self.opt.zero_grad(set_to_none=False)
-        sc = self.scores(seqs)
-        loss = self.loss(sc, target, am, err, utt_off, kind, lam)
-        loss.backward()
-        if update:
+        with torch.set_grad_enabled(update != "loss"):
+            sc = self.scores(seqs)
+            loss = rescorebert_loss(sc, target, am, cer, n_best, method, md_loss_weight)
+            if update != "loss":
+                loss.backward()
+        if update is True:
             self.opt.step()
         return float(loss.detach()), sc.detach().numpy()
 
@@ -74,22 +88,61 @@ class TorchTrainer:
     def tensor(self, key: str) -> np.ndarray:
         return self.model.w[key].detach().numpy()
 
-
-    def step_mlm(self, ids: np.ndarray, seq_off: np.ndarray, labels: np.ndarray, update=True) -> float:
-        """BertForMaskedLM CE over every real position (pads ignored), mean; AdamW."""
-        seqs = [ids[seq_off[i]:seq_off[i + 1]] for i in range(len(seq_off) - 1)]
-        T = max(len(x) for x in seqs)
+    def step_mlm(self, seqs: Sequence[Sequence[int]], labels: Sequence[Sequence[int]], update=True) -> float:
+        """One reference MLM batch: pad_sequence(ids / labels, 0), attention mask, CE mean over
+        all B*T positions (pads included), AdamW."""
+        T = max(len(s) for s in seqs)
         x = torch.zeros(len(seqs), T, dtype=torch.long)
         am = torch.zeros(len(seqs), T, dtype=torch.long)
-        lab = torch.full((len(seqs), T), -100, dtype=torch.long)
-        for i, sq in enumerate(seqs):
-            x[i, :len(sq)] = torch.as_tensor(sq.astype(np.int64))
+        lab = torch.zeros(len(seqs), T, dtype=torch.long)
+        for i, (sq, lb) in enumerate(zip(seqs, labels)):
+            x[i, :len(sq)] = torch.as_tensor(np.asarray(sq, np.int64))
             am[i, :len(sq)] = 1
-            lab[i, :len(sq)] = torch.as_tensor(labels[seq_off[i]:seq_off[i + 1]].astype(np.int64))
+            lab[i, :len(lb)] = torch.as_tensor(np.asarray(lb, np.int64))
         self.opt.zero_grad(set_to_none=False)
-        logits = self.model.mlm_logits(self.model.encoder(x, am))
-        loss = torch.nn.functional.cross_entropy(logits.view(-1, logits.shape[-1]), lab.view(-1), ignore_index=-100)
-        loss.backward()
-        if update:
+        with torch.set_grad_enabled(update != "loss"):
+            logits = self.model.mlm_logits(self.model.encoder(x, am))
+            loss = torch.nn.functional.cross_entropy(logits.view(-1, logits.shape[-1]), lab.view(-1))
+            if update != "loss":
+                loss.backward()
+        if update is True:
             self.opt.step()
         return float(loss.detach())
+
+
+def _split(tokens, hyp_off):
+    return [np.asarray(tokens[hyp_off[h]:hyp_off[h + 1]]).tolist() for h in range(len(hyp_off) - 1)]
+
+
+def train_rescorebert(tr: TorchTrainer, train: dict, dev: dict, epochs: int, batch_size: int, n_best: int,
+                      method: str, md_loss_weight: float):
+    """RescoreBert/main.py:166-229's loop: ``train`` / ``dev`` = dict(seqs, pll, am, cer).
+    Returns (train losses, dev losses) per epoch."""
+    tl, dl = [], []
+    rows = batch_size * n_best
+    for _ in range(epochs):
+        tr.reset_optimizer()
+        for split, out, upd in ((train, tl, True), (dev, dl, "loss")):
+            tot, nb = 0.0, 0
+            for b0 in range(0, len(split["seqs"]), rows):
+                sl = slice(b0, b0 + rows)
+                loss, _ = tr.step(split["seqs"][sl], split["pll"][sl], split["am"][sl], split["cer"][sl], n_best,
+                                  method, md_loss_weight, update=upd)
+                tot += loss
+                nb += 1
+            out.append(tot / nb)
+    return tl, dl
+
+
+def train_mlm(tr: TorchTrainer, train: dict, dev: dict, epochs: int, batch_size: int):
+    """MLM_PLL/main.py:117-161's loop over do_job rows ``dict(seqs, labels)``."""
+    tl, dl = [], []
+    for _ in range(epochs):
+        tr.reset_optimizer()
+        for split, out, upd in ((train, tl, True), (dev, dl, "loss")):
+            tot, nb = 0.0, 0
+            for b0 in range(0, len(split["seqs"]), batch_size):
+                tot += tr.step_mlm(split["seqs"][b0:b0 + batch_size], split["labels"][b0:b0 + batch_size], update=upd)
+                nb += 1
+            out.append(tot / nb)
+    return tl, dl

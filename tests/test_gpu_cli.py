@@ -97,24 +97,45 @@ def test_cli_rmbr_bertscore(c1):
 
 
 def test_cli_rescorebert_train_then_score(c1):
-    """rescorebert_train on the C1 texts (MLM_PLL teacher = the golden lm JSON), then the
-    written checkpoint feeds rescorebert scoring."""
+    """rescorebert_train with the reference's MD_MWER_train.yaml layout (method,
+    md_loss_weight, epoch, batch_size in utterances, hyps_token_ids / mlm_pll_score /
+    hyps_am_score / hyps_cer features) on the C1 texts (teacher = the golden lm JSON):
+    checkpoint_{n}.pth + loss.json per epoch; resuming at epoch 2 from checkpoint_1.pth
+    reproduces the straight run bitwise (AdamW is rebuilt every epoch, as in the reference);
+    the checkpoint then feeds rescorebert scoring."""
     import torch
     from asr_rescoring_amd import cli
     g, d = c1
     json.dump(g["lm"], open(d / "mlm_score.json", "w", encoding="utf-8"), ensure_ascii=False)
+    json.dump(g["hyps_cer"], open(d / "hyps_cer.json", "w", encoding="utf-8"), ensure_ascii=False)
+    feats = ["hyps_token_ids", "mlm_pll_score", "hyps_am_score", "hyps_cer"]
+    fpaths = [str(d / f) for f in ("hyps_text.json", "mlm_score.json", "hyps_score.json", "hyps_cer.json")]
+
+    def run(out, extra):
+        return cli.rescorebert_train(cli.ArgParser().parse(["--config", _cfg(d, "MD_MWER_train.yaml", {
+            "task": "training", "method": "MD_MWER", "seed": 10, "md_loss_weight": 0.0001, "lr": 1e-5, "epoch": 2,
+            "device": "cuda:0", "random_init_seed": 1234, "train_feature": feats, "train_feature_path": fpaths,
+            "dev_feature": feats, "dev_feature_path": fpaths, "output_path": str(out), "batch_size": 3,
+            "max_utt": 99999999, "n_best": 10, "dataloader": {"shuffle": False, "num_worker": 5},
+            "model": {"bert": "bert-base-chinese", "vocab": str(d / "vocab.txt")},
+            "resume": extra})]))
     out = d / "train_out"
-    res = cli.rescorebert_train(cli.ArgParser().parse(["--config", _cfg(d, "MD_MWER.yaml", {
-        "device": "cuda:0", "random_init_seed": 1234, "loss_type": "MD_MWER", "lambda": 0.5, "epochs": 2,
-        "batch_size": 3, "lr": 1e-5, "n_best": 10, "reset_optimizer": True,
-        "model": {"bert": "bert-base-chinese", "vocab": str(d / "vocab.txt")},
-        "train_feature": ["hyps_text", "ref_text", "hyps_score", "mlm_score"],
-        "train_feature_path": [str(d / f) for f in ("hyps_text.json", "ref_text.json", "hyps_score.json",
-                                                    "mlm_score.json")],
-        "output_path": str(out)})]))
-    assert len(res["losses"]) == 2 and all(np.isfinite(res["losses"]))
+    res = run(out, {"start_from": None, "checkpoint_path": None})
+    assert len(res["train_loss"]) == 2 and len(res["dev_loss"]) == 2
+    assert all(np.isfinite(res["train_loss"])) and all(np.isfinite(res["dev_loss"]))
+    assert [os.path.basename(p) for p in res["checkpoints"]] == ["checkpoint_1.pth", "checkpoint_2.pth"]
+    rec = json.load(open(out / "loss.json", encoding="utf-8"))
+    assert rec == {"train": res["train_loss"], "dev": res["dev_loss"]}
     sd = torch.load(res["checkpoints"][-1], map_location="cpu", weights_only=True)
     assert "linear.weight" in sd and "bert.pooler.dense.weight" in sd
+    # resume (RescoreBert/main.py:185-200): epoch 2 from checkpoint_1.pth and loss.json
+    out2 = d / "train_out_resume"
+    out2.mkdir()
+    json.dump({"train": res["train_loss"][:1], "dev": res["dev_loss"][:1]}, open(out2 / "loss.json", "w"))
+    res2 = run(out2, {"start_from": 2, "checkpoint_path": res["checkpoints"][0]})
+    assert res2["train_loss"] == res["train_loss"] and res2["dev_loss"] == res["dev_loss"]
+    sd2 = torch.load(res2["checkpoints"][-1], map_location="cpu", weights_only=True)
+    assert all(torch.equal(sd[k], sd2[k]) for k in sd)
     files = cli.rescorebert(cli.ArgParser().parse(["--config", _cfg(d, "MD_score.yaml", {
         "device": "cuda:0", "checkpoint_path": res["checkpoints"][-1], "n_best": 10,
         "model": {"bert": "bert-base-chinese", "vocab": str(d / "vocab.txt")},
@@ -125,17 +146,34 @@ def test_cli_rescorebert_train_then_score(c1):
 
 
 def test_cli_mlm_finetune_then_pll(c1):
-    """mlm_finetune on the C1 reference texts, then the checkpoint scores with mlm_pll."""
+    """mlm_finetune with the reference's train.yaml layout (do_job rows JSON as
+    train_data_path / dev_data_path, epoch, dataloader.batch_size / shuffle), then the
+    checkpoint scores with mlm_pll."""
     import torch
     from asr_rescoring_amd import cli
+    from asr_rescoring_amd.frontend import NativeTokenizer
+    from asr_rescoring_amd.train import do_job_rows
     g, d = c1
+    tok = NativeTokenizer(str(d / "vocab.txt"))
+    rows = []
+    for u, t in g["ref_text"].items():             # MLM_PLL/preprocess.py:9-30 "for_training" rows
+        ids, off, lab = do_job_rows([[101] + tok.encode(t) + [102]])
+        for i in range(len(off) - 1):
+            r = ids[off[i]:off[i + 1]].tolist()
+            rows.append({"utt_id": u, "hyp_id": None, "input_ids": r, "attention_masks": [1] * len(r),
+                         "mask_pos": i + 1, "labels": lab[off[i]:off[i + 1]].tolist()})
+    json.dump(rows, open(d / "train_rows.json", "w"))
     out = d / "mlm_out"
     res = cli.mlm_finetune(cli.ArgParser().parse(["--config", _cfg(d, "train.yaml", {
-        "device": "cuda:0", "random_init_seed": 1234, "epochs": 2, "batch_size": 32, "lr": 1e-5,
-        "model": {"bert": "bert-base-chinese", "vocab": str(d / "vocab.txt")},
-        "train_ref_text_path": str(d / "ref_text.json"), "output_path": str(out)})]))
-    assert len(res["losses"]) == 2 and all(np.isfinite(res["losses"]))
+        "task": "training", "seed": 10, "lr": 1e-5, "epoch": 2, "device": "cuda:0", "random_init_seed": 1234,
+        "train_data_path": str(d / "train_rows.json"), "dev_data_path": str(d / "train_rows.json"),
+        "output_path": str(out), "num_of_data": 99999999,
+        "dataloader": {"shuffle": False, "batch_size": 32, "num_worker": 5},
+        "model": {"bert": "bert-base-chinese", "vocab": str(d / "vocab.txt")}})]))
+    assert len(res["train_loss"]) == 2 and all(np.isfinite(res["train_loss"] + res["dev_loss"]))
+    assert json.load(open(out / "loss.json")) == {"train": res["train_loss"], "dev": res["dev_loss"]}
     sd = torch.load(res["checkpoints"][-1], map_location="cpu", weights_only=True)
+    assert os.path.basename(res["checkpoints"][-1]) == "checkpoint_2.pth"
     assert torch.equal(sd["cls.predictions.decoder.weight"], sd["bert.embeddings.word_embeddings.weight"])
     assert cli.main(["mlm_pll", "--config", _cfg(d, "score_ft.yaml", {
         "task": "scoring", "device": "cuda:0", "checkpoint_path": res["checkpoints"][-1],

@@ -149,3 +149,36 @@ def test_data_synthetic_and_json(tmp_path):
     assert raw == json.dumps(js, ensure_ascii=False, indent=4)      # util/saving.py:14-16
     assert list(js["utt_0"]) == ["hyp_1", "hyp_2", "hyp_3", "hyp_4"]
     assert B.forward_flops(34, BERT_BASE) == pytest.approx(5.459e9, rel=1e-3)
+
+
+# ---- training (F6 / F7: the reference's own training loops, tests/golden/make_golden_train.py)
+@pytest.mark.parametrize("method", ["MD", "MD_MWER", "MD_MWED"])
+def test_oracle_rescorebert_training_vs_reference(method):
+    """oracle.train_ref restates RescoreBert/main.py:82-229: two epochs (AdamW per epoch),
+    epoch / dev losses, dev scores and every parameter update equal the reference's run."""
+    from oracle.train_ref import TorchTrainer, train_rescorebert
+    from train_fixtures import check_updates, rb_fixture
+    w, tr_d, dv_d, hp, g = rb_fixture(method)
+    tr = TorchTrainer(w, BERT_TINY, lr=hp["lr"])
+    before = {k: tr.tensor(k).copy() for k in tr.model.w}
+    tl, dl = train_rescorebert(tr, tr_d, dv_d, 2, hp["batch_size"], hp["n_best"], method, hp["md_loss_weight"])
+    np.testing.assert_allclose(tl, g["train_loss"], rtol=1e-4)
+    np.testing.assert_allclose(dl, g["dev_loss"], rtol=1e-4)
+    with torch.no_grad():
+        sc = tr.scores(dv_d["seqs"]).numpy()
+    np.testing.assert_allclose(sc, g["dev_scores"], rtol=1e-4, atol=1e-5)
+    check_updates(g, before, {k: tr.tensor(k) for k in tr.model.w})
+
+
+def test_oracle_mlm_training_vs_reference():
+    """oracle.train_ref restates MLM_PLL/main.py:28-161: padded batches with [PAD] labels in
+    the CE mean, two epochs, dev loss, parameter updates."""
+    from oracle.train_ref import TorchTrainer, train_mlm
+    from train_fixtures import check_updates, mlm_fixture
+    w, tr_d, dv_d, hp, g = mlm_fixture()
+    tr = TorchTrainer(w, BERT_TINY, lr=hp["lr"], head="mlm")
+    before = {k: tr.tensor(k).copy() for k in tr.model.w}
+    tl, dl = train_mlm(tr, tr_d, dv_d, 2, hp["batch_size"])
+    np.testing.assert_allclose(tl, g["train_loss"], rtol=1e-4)
+    np.testing.assert_allclose(dl, g["dev_loss"], rtol=1e-4)
+    check_updates(g, before, {k: tr.tensor(k) for k in tr.model.w})

@@ -178,13 +178,13 @@ def c2train():
     (forward + backward ~ 3 x the forward's dense FLOPs)."""
     from asr_rescoring_amd.train import RescoreBertTrainer
     w = make_weights(BERT_BASE, seed=1234, with_cls_linear=True, with_pooler=True)
-    tr = RescoreBertTrainer(w, BERT_BASE, loss="MD_MWER", lam=1.0, lr=1e-5)
+    tr = RescoreBertTrainer(w, BERT_BASE, method="MD_MWER", md_loss_weight=1e-4, lr=1e-5)  # MD_MWER_train.yaml
     nb = D.synthetic_nbest(3, 50, seed=1)
     rng = np.random.default_rng(0)
     tgt = -np.abs(rng.normal(40, 8, nb.n_hyp)).astype(np.float32)
-    err = rng.integers(0, 6, nb.n_hyp).astype(np.float32)
+    cer = (rng.integers(0, 6, nb.n_hyp) / 30.0).astype(np.float32)
     am = nb.am.astype(np.float32)
-    step = lambda: tr.step(nb.tokens, nb.hyp_off, nb.utt_off, tgt, am, err)
+    step = lambda: tr.step(nb.tokens, nb.hyp_off, nb.utt_off, tgt, am, cer)
     dt = _timed(step, steps=5, warmup=2)
     tr.close()
     T = np.diff(nb.hyp_off).astype(np.float64)
@@ -196,22 +196,27 @@ def c2train():
 
 
 def mlmtrain():
-    """MLM fine-tuning on bert-base: do_job rows of 32 reference sentences (L ~ U{24..40}),
-    rows / s (one row = one masked copy) and fp32 TFLOP/s (3 x forward incl. the full-vocab head)."""
-    from asr_rescoring_amd.train import MLMTrainer, do_job_rows
+    """MLM fine-tuning on bert-base: the reference's batches (MLM_PLL/config/train.yaml: 32
+    do_job rows, padded to the batch's longest, CE over every position) of reference-length
+    sentences (L ~ U{24..40}); rows / s (one row = one masked copy) and fp32 TFLOP/s (3 x
+    forward incl. the full-vocab head, over the padded positions the step computes)."""
+    from asr_rescoring_amd.train import MLMTrainer, do_job_rows, pad_rows
     w = make_weights(BERT_BASE, seed=1234)
     tr = MLMTrainer(w, BERT_BASE, lr=1e-5)
     nb = D.synthetic_nbest(32, 1, seed=1)
     seqs = [nb.tokens[nb.hyp_off[h]:nb.hyp_off[h + 1]].tolist() for h in range(nb.n_hyp)]
     ids, off, lab = do_job_rows(seqs)
-    o = off[:161]
-    step = lambda: tr.step(ids[:o[-1]], o, lab[:o[-1]])
+    rows = [ids[off[i]:off[i + 1]].tolist() for i in range(32)]
+    labs = [lab[off[i]:off[i + 1]].tolist() for i in range(32)]
+    batch = pad_rows(rows, labs)
+    step = lambda: tr.step(*batch)
     dt = _timed(step, steps=5, warmup=2)
     tr.close()
+    o = batch[1]
     T = np.diff(o).astype(np.float64)
     H, F, L, V = BERT_BASE.hidden, BERT_BASE.intermediate, BERT_BASE.layers, BERT_BASE.vocab
     fl = 3.0 * (float(T.sum()) * (L * 2 * (4 * H * H + 2 * H * F) + 2 * (H * H + H * V)) + L * 4 * float((T * T).sum()) * H)
-    return [{"workload": "MLM fine-tuning, bert-base, 160 do_job rows per step (fp32)", "value": round(160 / dt, 1),
+    return [{"workload": "MLM fine-tuning, bert-base, 32 padded do_job rows per step (fp32)", "value": round(32 / dt, 1),
              "unit": "rows/s", "tokens_per_step": int(T.sum()), "ms_per_step": round(dt * 1e3, 1),
              "tflops_fp32": round(fl / dt / 1e12, 1)}]
 
