@@ -75,6 +75,7 @@ _SIGS = {
     "rs_trainer_reset_optimizer": (ctypes.c_int, [P]),
     "rs_trainer_destroy": (None, [P]),
     "rs_bertscore_recall": (ctypes.c_int, [P, P, P, P, I32, P, P]),
+    "rs_align": (ctypes.c_int, [P, P, P, P, I32, P, P, P, P, P, P, P, I32, P]),
     "rs_fuse_rerank": (ctypes.c_int, [P, P, P, P, I32, I32, P, I32, I32, P, P]),
     "rs_corpus_edits": (ctypes.c_int, [P, P, P, I32, I32, P, P]),
     "rs_ref_edit": (ctypes.c_int, [P, P, P, P, P, I32, P, P]),

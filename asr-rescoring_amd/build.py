@@ -1,12 +1,16 @@
 """Builds ``librescore.so`` in-tree with hipcc for gfx950 (no JIT cache, no pip install).
 
 Each ``csrc/*.hip`` (hipcc) and host-only ``csrc/*.cpp`` (g++) is compiled to an object in
-``csrc/build/`` (in parallel), then linked into ``asr-rescoring_amd/librescore.so``.  Rebuilds only what changed.
+``csrc/build/`` (in parallel), then linked into ``asr-rescoring_amd/librescore.so``.  Rebuilds
+only what changed, judged by CONTENT: every object and the library carry a ``.stamp`` with the
+sha256 of their inputs (source, headers, command line), so a copied-in or stale artefact whose
+stamp does not match its sources is rebuilt (mtimes are not trusted).
 """
 from __future__ import annotations
 
 import concurrent.futures as cf
 import glob
+import hashlib
 import os
 import subprocess
 import sys
@@ -23,11 +27,27 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-Wall", "-Wno-
          "-Wno-unused-variable", "-I", os.path.join(REPO, "include")]
 
 
-def _needs(target: str, deps) -> bool:
-    if not os.path.exists(target):
+def _digest(deps, cmd) -> str:
+    h = hashlib.sha256(" ".join(cmd).encode())
+    for d in sorted(deps):
+        h.update(d.encode())
+        with open(d, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()
+
+
+def _needs(target: str, deps, cmd) -> bool:
+    """True unless ``target`` exists with a stamp equal to the digest of deps + cmd."""
+    stamp = target + ".stamp"
+    if not (os.path.exists(target) and os.path.exists(stamp)):
         return True
-    t = os.path.getmtime(target)
-    return any(os.path.getmtime(d) > t for d in deps)
+    with open(stamp) as f:
+        return f.read().strip() != _digest(deps, cmd)
+
+
+def _stamp(target: str, deps, cmd) -> None:
+    with open(target + ".stamp", "w") as f:
+        f.write(_digest(deps, cmd))
 
 
 def _compile(src: str) -> str:
@@ -35,12 +55,13 @@ def _compile(src: str) -> str:
     obj = os.path.join(OBJ, os.path.basename(src).rsplit(".", 1)[0] + ".o")
     deps = [src] + glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.inc")) \
         + glob.glob(os.path.join(REPO, "include", "*.h"))
-    if _needs(obj, deps):
-        cmd = ([CXX, "-O2", "-std=c++17", "-fPIC", "-Wall", "-I", os.path.join(REPO, "include")] if host
-               else [HIPCC] + FLAGS) + ["-c", src, "-o", obj]
+    cmd = ([CXX, "-O2", "-std=c++17", "-fPIC", "-Wall", "-I", os.path.join(REPO, "include")] if host
+           else [HIPCC] + FLAGS) + ["-c", src, "-o", obj]
+    if _needs(obj, deps, cmd):
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed for {src}:\n{r.stderr[-6000:]}")
+        _stamp(obj, deps, cmd)
     return obj
 
 
@@ -49,12 +70,14 @@ def build_library(verbose: bool = False) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(_compile, srcs))
-    if _needs(LIB, objs):
-        cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs
-        # rocBLAS: fp32 GEMMs of the trainer (its soname matches the copy torch loads first)
-        r = subprocess.run(cmd + ["-L/opt/rocm/lib", "-lrocblas", "-lpthread"], capture_output=True, text=True)
+    # rocBLAS: fp32 GEMMs of the trainer (its soname matches the copy torch loads first)
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + \
+        ["-L/opt/rocm/lib", "-lrocblas", "-lpthread"]
+    if _needs(LIB, objs, cmd):
+        r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
+        _stamp(LIB, objs, cmd)
     if verbose:
         print("built", LIB, file=sys.stderr)
     return LIB

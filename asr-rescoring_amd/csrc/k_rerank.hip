@@ -11,14 +11,12 @@
 //                 same operation order), first-max argmax.
 //  corpus_edits   per-weight sum of the argmax hypotheses' edits (exact integer CER numerator).
 //
-// Edit distance: Myers/Hyyro bit-parallel (one 64-bit word) when the shorter string has
-// <= 64 symbols, else a two-row DP in private memory (strings up to RS_MAX_DP symbols).
+// Edit distance: Myers/Hyyro bit-parallel, one 64-bit word when the shorter string has <= 64
+// symbols, else the blocked form (words of 64 pattern rows, up to RS_MAX_EDIT symbols).
 #include "common.h"
 #include "../../include/rescore.h"
 
 namespace {
-
-constexpr int RS_MAX_DP = 1024;
 
 __device__ int myers64(const int* __restrict__ a, int m, const int* __restrict__ b, int n) {
     // a: pattern (m <= 64), b: text.  Global edit distance (first DP row = 0..n).
@@ -56,31 +54,55 @@ __device__ int myers64(const int* __restrict__ a, int m, const int* __restrict__
     return score;
 }
 
-__device__ int dp_edit(const int* __restrict__ a, int m, const int* __restrict__ b, int n) {
-    // two-row DP over the shorter string (m <= RS_MAX_DP)
-    int row[RS_MAX_DP + 1];
-    for (int j = 0; j <= m; ++j) row[j] = j;
-    for (int k = 1; k <= n; ++k) {
-        int diag = row[0];
-        row[0] = k;
-        const int c = b[k - 1];
-        for (int j = 1; j <= m; ++j) {
-            const int up = row[j];
-            const int v = min(min(up + 1, row[j - 1] + 1), diag + (a[j - 1] != c));
-            diag = up;
-            row[j] = v;
+// Blocked Myers / Hyyro (the pattern cut into 64-row words, horizontal deltas carried from
+// word to word): exact global edit distance for patterns of up to RS_MAX_EDIT symbols, in
+// O(ceil(m / 64) * n) word operations; the per-word Peq bits are formed on the fly.
+constexpr int RS_MAX_EDIT = 16384;
+constexpr int RS_MAX_WORDS = RS_MAX_EDIT / 64;
+
+__device__ int myers_blocked(const int* __restrict__ a, int m, const int* __restrict__ b, int n) {
+    unsigned long long Pv[RS_MAX_WORDS], Mv[RS_MAX_WORDS];
+    const int nw = (m + 63) >> 6;
+    for (int w = 0; w < nw; ++w) { Pv[w] = ~0ull; Mv[w] = 0ull; }
+    const unsigned long long top = 1ull << ((m - 1) & 63);   // last pattern row, in the last word
+    int score = m;
+    for (int k = 0; k < n; ++k) {
+        const int c = b[k];
+        int hin = 1;                                          // first DP row 0..n: delta +1
+        for (int w = 0; w < nw; ++w) {
+            const int base = w << 6, rows = min(64, m - base);
+            unsigned long long Eq = 0ull;
+            for (int i = 0; i < rows; ++i) Eq |= (unsigned long long)(a[base + i] == c) << i;
+            const unsigned long long pv = Pv[w], mv = Mv[w];
+            const unsigned long long Xv = Eq | mv;
+            if (hin < 0) Eq |= 1ull;
+            const unsigned long long Xh = (((Eq & pv) + pv) ^ pv) | Eq;
+            unsigned long long Ph = mv | ~(Xh | pv);
+            unsigned long long Mh = pv & Xh;
+            const unsigned long long hb = w == nw - 1 ? top : (1ull << 63);
+            const int hout = (Ph & hb) ? 1 : (Mh & hb) ? -1 : 0;
+            Ph <<= 1;
+            Mh <<= 1;
+            if (hin < 0) Mh |= 1ull;
+            else if (hin > 0) Ph |= 1ull;
+            Pv[w] = Mh | ~(Xv | Ph);
+            Mv[w] = Ph & Xv;
+            hin = hout;
         }
+        score += hin;
     }
-    return row[m];
+    return score;
 }
 
+// exact for strings of up to RS_MAX_EDIT symbols on the shorter side; -1 beyond (the host
+// wrappers reject such inputs before launching)
 __device__ int edit_distance(const int* a, int na, const int* b, int nb) {
     if (na > nb) {  // pattern = shorter string (ed is symmetric)
         const int* t = a; a = b; b = t;
         int tn = na; na = nb; nb = tn;
     }
     if (na <= 64) return myers64(a, na, b, nb);
-    if (na <= RS_MAX_DP) return dp_edit(a, na, b, nb);
+    if (na <= RS_MAX_EDIT) return myers_blocked(a, na, b, nb);
     return -1;
 }
 
@@ -109,10 +131,11 @@ __global__ void ref_edit_kernel(const int* __restrict__ chars, const int* __rest
                                 const int* __restrict__ utt_off, const int* __restrict__ ref_chars,
                                 const int* __restrict__ ref_off, int n_utt, int* __restrict__ out) {
     const int u = blockIdx.y;
-    const int s = utt_off[u] + blockIdx.x * blockDim.x + threadIdx.x;
-    if (u >= n_utt || s >= utt_off[u + 1]) return;
+    if (u >= n_utt) return;
     const int r0 = ref_off[u];
-    out[s] = edit_distance(ref_chars + r0, ref_off[u + 1] - r0, chars + str_off[s], str_off[s + 1] - str_off[s]);
+    // any number of hypotheses per utterance: strided over the blocks of grid.x
+    for (int s = utt_off[u] + blockIdx.x * blockDim.x + threadIdx.x; s < utt_off[u + 1]; s += gridDim.x * blockDim.x)
+        out[s] = edit_distance(ref_chars + r0, ref_off[u + 1] - r0, chars + str_off[s], str_off[s + 1] - str_off[s]);
 }
 
 // torch-CPU float32 Tensor.sum(-1) order for a contiguous row of n values (n < 512):
@@ -265,8 +288,7 @@ int rs_ref_edit(const int32_t* d_chars, const int32_t* d_str_off, const int32_t*
                 void* stream) {
     if (n_utt < 0) return RS_EARG;
     if (n_utt == 0) return RS_OK;
-    // max hypotheses per utterance bounded by grid.x * 64; the host passes n_utt only, so
-    // launch 16 x 64 threads per utterance (up to 1024 hypotheses each)
+    // 16 x 64 threads per utterance, hypotheses strided over them (any count)
     hipLaunchKernelGGL(ref_edit_kernel, dim3(16, n_utt), dim3(64), 0, (hipStream_t)stream, d_chars, d_str_off,
                        d_utt_off, d_ref_chars, d_ref_off, n_utt, d_ed_ref);
     return hipGetLastError() == hipSuccess ? RS_OK : RS_EHIP;

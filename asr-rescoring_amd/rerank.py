@@ -23,6 +23,9 @@ import torch
 from . import _lib
 from .data import NBest
 
+# Edit-distance kernels (csrc/k_rerank.hip): exact for strings of up to RS_MAX_EDIT symbols
+MAX_EDIT_LEN = 16384
+
 
 def _dev(a, dtype, device):
     return torch.as_tensor(np.ascontiguousarray(a), dtype=dtype).to(device)
@@ -56,8 +59,8 @@ def ref_edits(nb: NBest, device=0) -> torch.Tensor:
     rflat = np.concatenate(nb.refs).astype(np.int32)
     roff = np.zeros(nb.n_utt + 1, np.int32)
     roff[1:] = np.cumsum([len(r) for r in nb.refs])
-    if int(np.diff(nb.utt_off).max(initial=0)) > 1024:
-        raise ValueError("at most 1024 hypotheses per utterance")
+    if max(int(np.diff(soff).max(initial=0)), int(np.diff(roff).max(initial=0))) > MAX_EDIT_LEN:
+        raise ValueError(f"strings longer than {MAX_EDIT_LEN} symbols are not supported")
     d_c, d_so, d_uo = _dev(flat, torch.int32, dev), _dev(soff, torch.int32, dev), _dev(nb.utt_off, torch.int32, dev)
     d_rc, d_ro = _dev(rflat, torch.int32, dev), _dev(roff, torch.int32, dev)
     out = torch.empty(nb.n_hyp, dtype=torch.int32, device=dev)
@@ -121,8 +124,8 @@ def pairwise_edit(nb: NBest, device=0) -> Tuple[torch.Tensor, np.ndarray]:
     n_u = np.diff(nb.utt_off).astype(np.int64)
     moff = np.zeros(nb.n_utt + 1, np.int64)
     moff[1:] = np.cumsum(n_u * n_u)
-    if len(soff) > 1 and int(np.diff(soff).max()) > 1024:
-        raise ValueError("strings longer than 1024 symbols are not supported")
+    if len(soff) > 1 and int(np.diff(soff).max()) > MAX_EDIT_LEN:
+        raise ValueError(f"strings longer than {MAX_EDIT_LEN} symbols are not supported")
     d_c, d_so = _dev(flat, torch.int32, dev), _dev(soff, torch.int32, dev)
     d_uo, d_mo = _dev(nb.utt_off, torch.int32, dev), _dev(moff, torch.int64, dev)
     ed = torch.empty(int(moff[-1]), dtype=torch.int32, device=dev)

@@ -139,7 +139,9 @@ void rs_model_destroy(rs_model* m);
  *             (strings of utterance u = utt_off[u]..utt_off[u+1])
  *   d_mat_off int64 [n_utt+1] offsets of each n_u x n_u block in d_ed (row-major)
  *   d_ed      int32 out: d_ed[mat_off[u] + i*n_u + j] = ed(string_i, string_j)
- * Strings up to 64 symbols use a Myers/Hyyro bit-parallel kernel; longer ones a DP. */
+ * Myers/Hyyro bit-parallel: one 64-bit word when the shorter string of a pair has <= 64
+ * symbols, 64-row words with carried horizontal deltas beyond; exact when the shorter
+ * string has <= 16384 symbols, -1 otherwise (the Python wrappers reject such inputs). */
 int rs_pairwise_edit(const int32_t* d_chars, const int32_t* d_str_off, const int32_t* d_utt_off,
                      const int64_t* d_mat_off, int32_t n_utt, int32_t max_n, int32_t* d_ed,
                      void* stream);
@@ -167,6 +169,27 @@ int rs_bertscore_recall(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_
  * summation and argmax as rs_mbr_scores. */
 int rs_mbr_scores_bs(const float* d_rmat, const int64_t* d_mat_off, const int32_t* d_utt_off, int32_t n_utt,
                      int32_t k, int32_t which, float* d_scores, int32_t* d_argmax, void* stream);
+
+/* ---- Levenshtein alignment with backtrace (espnet_data/preprocess/align.py:5-97
+ * levenshtein_distance_alignment) -----------------------------------------
+ * Pair p aligns ref tokens d_ref[d_ref_off[p] .. d_ref_off[p+1]) with hyp tokens
+ * d_hyp[d_hyp_off[p] .. ) (int32 token ids, any values; 0 <= length <= 4096, max_len = the
+ * longest list of the call).  Reference rules: rows = hyp, columns = ref, both with a start
+ * sentinel; equal tokens take the diagonal cost as "U"; otherwise S = diag + 1, replaced only
+ * by a strictly smaller I = left + 1, then by a strictly smaller D = up + 1; first column D,
+ * first row I; traceback from the end: U / S consume both, D = hyp-only token (ref "*"),
+ * I = ref-only token (hyp "*"); output in forward order (the reference reverses its lists).
+ * Outputs at d_out_off[p] (int64, room for len(ref) + len(hyp) entries): d_ops int8
+ * (RS_AL_U / _S / _I / _D), d_ref_idx / d_hyp_idx int32 (index into the pair's ref / hyp
+ * tokens, -1 = "*"), d_n[p] = the alignment's length.  d_lab: uint8 scratch of
+ * (len(hyp) + 1) * (len(ref) + 1) bytes per pair at d_lab_off[p] (int64).  Async on `stream`. */
+#define RS_AL_U 0
+#define RS_AL_S 1
+#define RS_AL_I 2
+#define RS_AL_D 3
+int rs_align(const int32_t* d_ref, const int32_t* d_ref_off, const int32_t* d_hyp, const int32_t* d_hyp_off,
+             int32_t n_pairs, const int64_t* d_lab_off, uint8_t* d_lab, const int64_t* d_out_off, int8_t* d_ops,
+             int32_t* d_ref_idx, int32_t* d_hyp_idx, int32_t* d_n, int32_t max_len, void* stream);
 
 /* ---- RescoreBert training (RescoreBert/main.py:82-229) ---------------------------------
  * A trainer holds fp32 parameters (HF keys as for rs_model; bert.pooler.* is accepted and
@@ -245,7 +268,8 @@ int rs_corpus_edits(const int32_t* d_ed_ref, const int32_t* d_utt_off, const int
 
 /* Edit distance of every hypothesis to its utterance's reference (the per-hypothesis
  * table behind jiwer.cer's numerator): d_ref_chars/d_ref_off int32 [n_utt+1] are the
- * references, hypotheses as in rs_pairwise_edit.  d_ed_ref int32 [n_hyp]. */
+ * references, hypotheses as in rs_pairwise_edit (any number per utterance; the same length
+ * limit).  d_ed_ref int32 [n_hyp]. */
 int rs_ref_edit(const int32_t* d_chars, const int32_t* d_str_off, const int32_t* d_utt_off,
                 const int32_t* d_ref_chars, const int32_t* d_ref_off, int32_t n_utt,
                 int32_t* d_ed_ref, void* stream);

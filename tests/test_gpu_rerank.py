@@ -28,6 +28,39 @@ def test_ref_and_pairwise_edit_vs_oracle():
                 assert M[i, j] == R.levenshtein(nb.hyp_words(nb.utt_off[u] + i), nb.hyp_words(nb.utt_off[u] + j))
 
 
+def test_edit_long_strings_and_many_hypotheses():
+    """Strings past one 64-bit word and past the old 1024-symbol DP (blocked Myers, exact up
+    to 16384 symbols) and an utterance with 1500 hypotheses (ref_edit strides over them)."""
+    from asr_rescoring_amd import rerank
+    from oracle import rescore_ref as R
+    rng = np.random.default_rng(5)
+    base = rng.integers(106, 140, 1500)
+
+    def mutate(x, k):
+        x = list(x)
+        for _ in range(k):
+            p = int(rng.integers(0, len(x)))
+            x[p] = int(rng.integers(106, 140))
+        return x[:len(x) - int(rng.integers(0, 60))]
+    long_hyps = [[mutate(base, 300) for _ in range(4)], [mutate(base[:200], 40) for _ in range(3)]]
+    nb = D.from_lists(long_hyps, refs=[base[:1400].tolist(), base[:130].tolist()])
+    ed = rerank.ref_edits(nb).cpu().numpy()
+    for u in range(nb.n_utt):
+        for h in range(nb.utt_off[u], nb.utt_off[u + 1]):
+            assert ed[h] == R.levenshtein(nb.refs[u], nb.hyp_words(h)), (u, h)
+    mat, moff = rerank.pairwise_edit(nb)
+    mat = mat.cpu().numpy()
+    for u in range(nb.n_utt):
+        n = nb.utt_off[u + 1] - nb.utt_off[u]
+        M = mat[moff[u]:moff[u + 1]].reshape(n, n)
+        for i in range(n):
+            for j in range(n):
+                assert M[i, j] == R.levenshtein(nb.hyp_words(nb.utt_off[u] + i), nb.hyp_words(nb.utt_off[u] + j))
+    many = D.from_lists([[mutate(base[:20], 3) for _ in range(1500)]], refs=[base[:20].tolist()])
+    ed = rerank.ref_edits(many).cpu().numpy()
+    assert all(ed[h] == R.levenshtein(many.refs[0], many.hyp_words(h)) for h in range(many.n_hyp))
+
+
 def test_mbr_golden(golden_dir):
     from asr_rescoring_amd import rerank
     g = np.load(os.path.join(golden_dir, "rmbr.npz"), allow_pickle=False)

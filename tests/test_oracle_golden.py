@@ -182,3 +182,12 @@ def test_oracle_mlm_training_vs_reference():
     np.testing.assert_allclose(tl, g["train_loss"], rtol=1e-4)
     np.testing.assert_allclose(dl, g["dev_loss"], rtol=1e-4)
     check_updates(g, before, {k: tr.tensor(k) for k in tr.model.w})
+
+
+def test_alignment_oracle_known_answers():
+    """oracle.align_ref vs the reference's docstring examples (espnet_data/preprocess/align.py:12-18)."""
+    from oracle.align_ref import levenshtein_distance_alignment as al
+    assert al(["how", "are", "you"], ["how", "are", "you", "doing"]) == \
+        [["how", "are", "you", "*"], ["how", "are", "you", "doing"], ["U", "U", "U", "D"]]
+    assert al(list("你好嗎"), list("你好不好")) == [["你", "好", "*", "嗎"], ["你", "好", "不", "好"], ["U", "U", "D", "S"]]
+    assert al([], []) == [[], [], []]
