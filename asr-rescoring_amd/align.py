@@ -48,7 +48,9 @@ def align_ids(ref: List[List[int]], hyp: List[List[int]], device=0):
     lab_off = np.concatenate([[0], np.cumsum((lr + 1) * (lh + 1))]).astype(np.int64)
     out_off = np.concatenate([[0], np.cumsum(lr + lh)]).astype(np.int64)
     T = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)       # noqa: E731
-    d_ref, d_roff, d_hyp, d_hoff = T(np.append(cat(ref), 0)), T(off(lr)), T(np.append(cat(hyp), 0)), T(off(lh))
+    pad = lambda a: np.append(a, np.zeros(1, np.int32))                   # noqa: E731 (no empty buffers)
+    d_ref, d_roff, d_hyp, d_hoff = T(pad(cat(ref))), T(off(lr)), T(pad(cat(hyp))), T(off(lh))
+    assert d_ref.dtype == d_hyp.dtype == d_roff.dtype == torch.int32
     d_loff, d_ooff = T(lab_off), T(out_off)
     n_out = max(int(out_off[-1]), 1)
     d_lab = torch.empty(max(int(lab_off[-1]), 1), dtype=torch.uint8, device=dev)
