@@ -51,7 +51,10 @@ struct EpiArgs {
 
 // fp16 operand image of an fp32 activation row with logical width K:
 //   kx == 1: [hi]                          (RS_PREC_FP16)
-//   kx == 3: [hi | hi/64 | (x - hi)*64]    (RS_PREC_FP16X3)
+//   kx == 3: [hi | hi/64 | (x - hi)*64]    (RS_PREC_FP16X3, K-concatenated GEMM form)
+//   kx == 2: [hi | (x - hi)*64]            (RS_PREC_FP16X3, split-operand GEMM form: the
+//            x3s kernel forms hi/64 in registers; weights use the first two parts of their
+//            three-part image, [W_hi | W_lo*64])
 // paired with the weight image [W_hi | W_lo*64 | W_hi/64] the K-concatenated MFMA product is
 // A_hi.W_hi + A_hi.W_lo + A_lo.W_hi (the power-of-two factors cancel exactly): fp32-level
 // accuracy from fp16 MFMA in one accumulator.  The factors keep the lo parts out of the fp16
@@ -66,16 +69,20 @@ __device__ __forceinline__ void put_split(f16* row, int c, int K, int kx, float 
     if (kx == 3) {
         row[K + c] = x3_mid(hi);
         row[2 * K + c] = x3_lo(v, hi);
+    } else if (kx == 2) {
+        row[K + c] = x3_lo(v, hi);
     }
 }
 __device__ __forceinline__ void put_split4(f16* row, int c, int K, int kx, float4 v) {
     const half4 hi = {(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
     *(half4*)(row + c) = hi;
+    if (kx >= 2) {
+        const half4 lo = {x3_lo(v.x, hi[0]), x3_lo(v.y, hi[1]), x3_lo(v.z, hi[2]), x3_lo(v.w, hi[3])};
+        *(half4*)(row + (kx - 1) * K + c) = lo;
+    }
     if (kx == 3) {
         const half4 mid = {x3_mid(hi[0]), x3_mid(hi[1]), x3_mid(hi[2]), x3_mid(hi[3])};
         *(half4*)(row + K + c) = mid;
-        const half4 lo = {x3_lo(v.x, hi[0]), x3_lo(v.y, hi[1]), x3_lo(v.z, hi[2]), x3_lo(v.w, hi[3])};
-        *(half4*)(row + 2 * K + c) = lo;
     }
 }
 
@@ -110,6 +117,11 @@ __device__ __forceinline__ float wave_max(float v) {
 // launches of the same epilogue
 hipError_t launch_gemm(int epi, const f16* A, const f16* W, int M_pad, int N_pad, int K,
                        const EpiArgs& ep, hipStream_t st, int tag = 0);
+// split-operand fp16x3 GEMM (gemm_x3s_kernel): A two-part image [M_pad, 2K], W rows of ldw
+// halfs starting [W_hi | W_lo*64] (the three-part weight image, ldw = 3K); epi EPI_BIAS_F32 or
+// EPI_GELU_F16 (two-part image out, ep.nlog = N apart).  N_pad % 256 == 0, K % 32 == 0, K >= 64.
+hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_pad, int N_pad, int K,
+                           const EpiArgs& ep, hipStream_t st);
 int gemm_row_align();   // M padding granularity required by launch_gemm
 
 // kx: width factor of the fp16 operand images written (1 or 3, see put_split);
@@ -138,6 +150,12 @@ hipError_t launch_ln_res_rows(float* x32, const float2* stats, float2* stats_out
                              const f16* o16, int rows, const float* g, const float* b, float eps, int H,
                              f16* y16, bool write_x, hipStream_t st, const float2* stats1 = nullptr,
                              const float* g1 = nullptr, const float* b1 = nullptr, const f16* o16b = nullptr);
+// fp16x3 split-operand mode: x32 <- LN(x32; stats, pg, pb) + o32 (o32 = the projection's fp32
+// output, bias included), then its statistics (stats_out, may alias stats) and the operand image
+// of LN(x32; g, b) with width factor kx
+hipError_t launch_ln_res32(float* x32, const float2* stats, float2* stats_out, const float* pg, const float* pb,
+                           const float* o32, int rows, const float* g, const float* b, float eps, int H, f16* y16,
+                           int kx, hipStream_t st);
 // Unique layer-0 rows (dedup): for every hypothesis of the chunk its T rows, and every
 // sequence's [MASK] row, as the fp16 operand image of LN(embedding) (rows of SeqMeta.urow_*)
 hipError_t launch_embed_unique(const int* tok, SeqMeta sm, int s0, int s1, int mask_id, int vocab,

@@ -182,6 +182,36 @@ ln_res_rows_kernel(float* __restrict__ x32, const float2* stats, float2* stats_o
     ln_store<NV>(x, g, b, eps, lane, nullptr, stats_out + row, y16 + (size_t)row * H, 1);
 }
 
+// BertSelfOutput / BertOutput (modeling_bert.py:282-293, 340-351) in the fp16x3 split-operand
+// mode: the projection (x3s GEMM) wrote o32 = dense(h) + bias in fp32; here x = LN_prev(x32) +
+// o32 (the residual input rebuilt from the pre-LN stream and its statistics, the reference's
+// hidden_states + input_tensor order), x written back as the new pre-LN stream, its statistics,
+// and the kx-wide operand image of LN(x) for the next projection.
+template <int NV>
+__global__ void __launch_bounds__(256)
+ln_res32_kernel(float* __restrict__ x32, const float2* stats, float2* stats_out, const float* __restrict__ pg,
+                const float* __restrict__ pb, const float* __restrict__ o32, int rows, const float* __restrict__ g,
+                const float* __restrict__ b, float eps, f16* __restrict__ y16, int kx) {
+    constexpr int H = NV * 256;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    const float2 st0 = stats[row];
+    float4 x[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int c = v * 256 + lane * 4;
+        const float4 r = *(const float4*)(x32 + (size_t)row * H + c);
+        const float4 gg = *(const float4*)(pg + c);
+        const float4 bb = *(const float4*)(pb + c);
+        const float4 o = *(const float4*)(o32 + (size_t)row * H + c);
+        x[v] = make_float4(o.x + ln_apply(r.x, st0, gg.x, bb.x), o.y + ln_apply(r.y, st0, gg.y, bb.y),
+                           o.z + ln_apply(r.z, st0, gg.z, bb.z), o.w + ln_apply(r.w, st0, gg.w, bb.w));
+        *(float4*)(x32 + (size_t)row * H + c) = x[v];
+    }
+    ln_store<NV>(x, g, b, eps, lane, nullptr, stats_out + row, y16 + (size_t)row * kx * H, kx);
+}
+
 __device__ __forceinline__ void load8(const f16* p, float (&o)[8]) {
     const half8 v = *(const half8*)p;
 #pragma unroll
@@ -1045,6 +1075,24 @@ hipError_t launch_ln_rows(const float* x, int rows, const float* g, const float*
         default: return hipErrorInvalidValue;
     }
 #undef RS_LN
+    return hipGetLastError();
+}
+
+hipError_t launch_ln_res32(float* x32, const float2* stats, float2* stats_out, const float* pg, const float* pb,
+                           const float* o32, int rows, const float* g, const float* b, float eps, int H, f16* y16,
+                           int kx, hipStream_t st) {
+    if (rows <= 0) return hipSuccess;
+    const dim3 grid((rows + 3) / 4), block(256);
+#define RS_LN32(NV) hipLaunchKernelGGL(ln_res32_kernel<NV>, grid, block, 0, st, x32, stats, stats_out, pg, pb, o32, \
+                                       rows, g, b, eps, y16, kx)
+    switch (H) {
+        case 256: RS_LN32(1); break;
+        case 512: RS_LN32(2); break;
+        case 768: RS_LN32(3); break;
+        case 1024: RS_LN32(4); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef RS_LN32
     return hipGetLastError();
 }
 

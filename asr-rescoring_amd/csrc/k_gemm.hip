@@ -1072,6 +1072,332 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
 #undef RS_PERSIST_WAIT
 }
 
+// ---------------------------------------------------------------------------------------
+// fp16x3 with SPLIT operands ("x3s"): the fp32-accurate product A . W^T as three fp16 MFMA
+// products from two-part images, A = [A_hi | A_lo*64] ([M, 2K]) and W = [W_hi | W_lo*64]
+// ([N, 2K]) (common.h put_split2):
+//     acc += W_hi . A_hi  +  (W_hi/64) . (A_lo*64)  +  (W_lo*64) . (A_hi/64)
+// the /64 factors applied to the fragments in registers (v_pk_mul_f16; the power-of-two
+// factors cancel exactly, the MFMA's subnormal flush drops the same terms the three-part
+// images of the K-concatenated form drop).  Against that form (K x 3 over [hi | hi/64 | lo*64]
+// images) every LDS-DMA byte and every fragment read feeds 1.5x the MFMA work: a K-step of
+// BK = 32 stages A_hi, A_lo, W_hi, W_lo (4 x 16 KiB, the same 64 KiB stage) for 3 products.
+// Persistent: one workgroup per CU walks 256x256 tiles (8 waves, 128x64 each, 32x32x16 MFMA),
+// two LDS stages, one barrier per K-step, after which step kt+1's DMA goes into the buffer
+// step kt-1 used (one K-step of lead).  One fragment set per wave (the two-set software
+// pipeline does not fit 2 waves/SIMD: 128 accumulators + 2 x 48 fragment registers); the
+// partner wave of the SIMD covers a wave's read latency.  Tile transition: the next tile's
+// stage 0 goes into the free buffer before this tile's epilogue, so the next tile's first
+// wait leaves this tile's stores in flight.
+// Epilogues: EPI_BIAS_F32 (fp32 [M, ldc]), EPI_GELU_F16 (two-part GELU image, nlog apart),
+// EPI_BIAS_F16; bias added in the epilogue (its loads ride the last K-step).  Rows up to
+// M_pad are stored (the buffers are M_pad rows).
+template <int EPI, int VAR>
+__global__ void __launch_bounds__(512)
+gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int ldw, int n_tiles_n, int n_tiles,
+                EpiArgs ep) {
+    constexpr int BM = 256, BK = 32, NW = 8, WN = 4, WTM = 128, WTN = 64, MS = 32;
+    constexpr int TM = WTM / MS, TN = WTN / MS;
+    constexpr int RB = BK * 2;                   // 64-byte LDS rows
+    constexpr int REG = BM * RB;                 // one 256-row region: 16 KiB
+    constexpr int STAGE = 4 * REG;               // A_hi | A_lo | W_hi | W_lo
+    constexpr int NSTORE = EPI == EPI_BIAS_F16 ? 16 : 32;
+    static_assert(EPI == EPI_BIAS_F32 || EPI == EPI_GELU_F16 || EPI == EPI_BIAS_F16, "x3s epilogues");
+    extern __shared__ __attribute__((aligned(16))) char smem[];        // the LDS-DMA ring (2 stages)
+    // wave-private epilogue slabs: a separate LDS object, so the compiler can tell the slab
+    // reads do not alias the LDS-DMA writes in flight (no vmcnt wait before them)
+    __shared__ __attribute__((aligned(16))) char slabs[NW * 4096];
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN, wn = wave % WN;
+    const int frow = lane & 31, fh = lane >> 5;
+    const int nk = K / BK;
+    int t = blockIdx.x;
+    if (t >= n_tiles) return;
+    if constexpr ((VAR & 262144) != 0) {
+        if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
+    }
+    auto tile_of = [&](int tt, int& m0, int& n0) {
+        const int xcd = tt & 7, pos = tt >> 3, q = n_tiles >> 3, r = n_tiles & 7;
+        const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+        const int GM = ep.group_m, n_tiles_m = n_tiles / n_tiles_n, per_group = GM * n_tiles_n;
+        const int g = wgid / per_group, loc = wgid - g * per_group;
+        const int gm = min(GM, n_tiles_m - g * GM);
+        const int tn = loc / gm;
+        m0 = (g * GM + (loc - tn * gm)) * BM;
+        n0 = tn * BM;
+    };
+    // LDS-DMA: 1 KiB pieces of 16 rows x 64 B; wave w stages pieces p = 0..7 of region p >> 1,
+    // rows (p & 1) * 128 + w * 16 + lane / 4 (16-B chunk lane & 3, source-swizzled)
+    const int prow = wave * 16 + (lane >> 2);
+    const int pswz = swz<32>(prow, lane & 3) * 8;
+    const size_t ld2 = (size_t)2 * K;
+    const f16* srcA;
+    const f16* srcW;
+    auto set_src = [&](int m0, int n0) {
+        srcA = A + (size_t)(m0 + prow) * ld2 + pswz;
+        srcW = W + (size_t)(n0 + prow) * ldw + pswz;
+    };
+    // VAR 16: the pieces as buffer_load_dwordx4 ... lds (32-bit lane offsets into a per-tile
+    // panel descriptor, k0 in the scalar offset) instead of global_load_lds (64-bit lane
+    // addresses): half the address data per DMA instruction
+    __amdgpu_buffer_rsrc_t rsA, rsW;
+    int voffA[4], voffW[4];                       // lane byte offsets: (p & 1) row half x (r & 1) hi / lo
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int l = 0; l < 2; ++l) {
+            voffA[2 * h + l] = ((prow + 128 * h) * (int)ld2 + l * K + pswz) * 2;
+            voffW[2 * h + l] = ((prow + 128 * h) * ldw + l * K + pswz) * 2;
+        }
+    auto set_rsrc = [&](int m0, int n0) {
+        rsA = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * ld2), (short)0, (int)(256 * ld2 * 2), 0x00020000);
+        rsW = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (size_t)n0 * ldw), (short)0, 256 * ldw * 2, 0x00020000);
+    };
+    auto piece = [&](int buf, int k0, int p) {
+        if constexpr ((VAR & 1) != 0) return;     // diagnostic: no K-loop staging (stale tiles)
+        const int r = p >> 1;
+        if constexpr ((VAR & 16) != 0) {
+            __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW,
+                                                     (__attribute__((address_space(3))) void*)(smem + buf * STAGE + r * REG +
+                                                                                                ((p & 1) * 8 + wave) * 1024),
+                                                     16, (r < 2 ? voffA : voffW)[2 * (p & 1) + (r & 1)], k0 * 2, 0, 0);
+            return;
+        }
+        const f16* g = r < 2 ? srcA + (size_t)(p & 1) * 128 * ld2 + (r & 1) * K + k0
+                             : srcW + (size_t)(p & 1) * 128 * ldw + (r & 1) * K + k0;
+        __builtin_amdgcn_global_load_lds((const void*)g,
+                                         (__attribute__((address_space(3))) void*)(smem + buf * STAGE + r * REG +
+                                                                                    ((p & 1) * 8 + wave) * 1024),
+                                         16, 0, 0);
+    };
+    auto stage = [&](int buf, int k0) {
+#pragma unroll
+        for (int p = 0; p < 8; ++p) piece(buf, k0, p);
+    };
+    // fragment addresses: row R, logical chunk 2s + fh -> position (fh ^ ((R >> 2) & 3)) ^ 2s;
+    // rows 32 apart share the swizzle, so fragment / region offsets are immediates
+    const int offA = (wm * WTM + frow) * RB + ((fh ^ (((wm * WTM + frow) >> 2) & 3)) << 4);
+    const int offW = 2 * REG + (wn * WTN + frow) * RB + ((fh ^ (((wn * WTN + frow) >> 2) & 3)) << 4);
+    struct Frags { half8 ah[TM], al[TM], wh[TN], wl[TN]; };
+    auto load_frags = [&](int buf, int s, Frags& f) {
+        const char* sb = smem + buf * STAGE;
+        const int xa = offA ^ (s << 5), xw = offW ^ (s << 5);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            f.wh[j] = *(const half8*)(sb + xw + j * MS * RB);
+            f.wl[j] = *(const half8*)(sb + xw + REG + j * MS * RB);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+            f.ah[i] = *(const half8*)(sb + xa + i * MS * RB);
+            f.al[i] = *(const half8*)(sb + xa + REG + i * MS * RB);
+        }
+    };
+    f32x16 acc[TM][TN];
+    const half8 down = (half8)(f16)X3_DOWN;
+    auto mfma3 = [&](Frags& f) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.wh[j], f.ah[i], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < TN; ++j) f.wh[j] *= down;                  // W_hi / 64
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.wh[j], f.al[i], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) f.ah[i] *= down;                  // A_hi / 64
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(f.wl[j], f.ah[i], acc[i][j], 0, 0, 0);
+    };
+
+    int m0, n0;
+    tile_of(t, m0, n0);
+    set_src(m0, n0);
+    set_rsrc(m0, n0);
+    stage(0, 0);
+    int par = 0;                                                  // buffer of K-step 0
+    bool first = true;
+    Frags F;
+    for (;;) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16)(0.f);
+        for (int kt = 0; kt < nk; ++kt) {
+            const int cur = (par + kt) & 1;
+            // step kt landed for this wave (at a tile's first step the previous tile's stores
+            // are younger and stay in flight); the barrier: landed for every wave, and every
+            // wave is done reading step kt-1's buffer, which now receives step kt+1
+            if constexpr ((VAR & 8) != 0) {
+                // diagnostic: the DMA is never waited for (isolates its latency from its presence)
+            } else if (kt == 0 && !first) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("s_barrier" ::: "memory");
+            if constexpr ((VAR & 4) != 0) {
+                // VAR 4: step kt+1's eight DMA pieces spread over substep 0's MFMAs (one or
+                // two per group of four), so neither wave of a SIMD spends the start of the
+                // step issuing DMA while its partner does the same and the MFMA pipe idles
+                const bool st_ok = kt + 1 < nk;
+                load_frags(cur, 0, F);
+                __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                for (int q = 0; q < 6; ++q) {
+                    // MFMAs 4q .. 4q+3 of the substep: product q / 2, row pair (q & 1)
+                    const int pr = q >> 1;
+                    if (q == 2) {
+#pragma unroll
+                        for (int j = 0; j < TN; ++j) F.wh[j] *= down;
+                    }
+                    if (q == 4) {
+#pragma unroll
+                        for (int i = 0; i < TM; ++i) F.ah[i] *= down;
+                    }
+#pragma unroll
+                    for (int ii = 0; ii < 2; ++ii)
+#pragma unroll
+                        for (int j = 0; j < TN; ++j) {
+                            const int i = 2 * (q & 1) + ii;
+                            const half8 a = pr == 0 ? F.ah[i] : pr == 1 ? F.al[i] : F.ah[i];
+                            const half8 b = pr == 2 ? F.wl[j] : F.wh[j];
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(b, a, acc[i][j], 0, 0, 0);
+                        }
+                    __builtin_amdgcn_sched_barrier(0);
+                    if (st_ok) {
+                        piece(cur ^ 1, (kt + 1) * BK, q < 2 ? 2 * q : q + 2);
+                        if (q < 2) piece(cur ^ 1, (kt + 1) * BK, 2 * q + 1);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                load_frags(cur, 1, F);
+                mfma3(F);
+                __builtin_amdgcn_sched_barrier(0);
+                continue;
+            }
+            if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                load_frags(cur, s, F);
+                mfma3(F);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        }
+        // ---- transition
+        const int last = (par + nk - 1) & 1;                      // buffer of the last K-step
+        const int cm0 = m0, cn0 = n0;
+        // bias of this tile (16-B quads of the lane's 4 consecutive columns): only the bias
+        // loads are outstanding here (the last K-step issued no DMA), so one vmcnt(0) waits
+        // for exactly them; inline asm keeps the compiler from placing its own wait
+        f32x4 bq[TN * 4];
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                const float* bp = ep.bias + cn0 + wn * WTN + MS * j + 8 * g + 4 * fh;
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bq[4 * j + g]) : "v"(bp) : "memory");
+            }
+        asm volatile("s_waitcnt vmcnt(0)"
+                     : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]), "+v"(bq[4]), "+v"(bq[5]), "+v"(bq[6]),
+                       "+v"(bq[7])
+                     :
+                     : "memory");
+        // the next tile's stage 0 (into the buffer step nk-2 used) lands while this epilogue runs
+        t += gridDim.x;
+        const bool more = t < n_tiles;
+        if (more) {
+            tile_of(t, m0, n0);
+            set_src(m0, n0);
+            set_rsrc(m0, n0);
+            stage(last ^ 1, 0);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+#pragma unroll
+                for (int g = 0; g < 4; ++g)
+#pragma unroll
+                    for (int e = 0; e < 4; e += 2) {
+                        f32x2 v = {acc[i][j][4 * g + e] + bq[4 * j + g][e], acc[i][j][4 * g + e + 1] + bq[4 * j + g][e + 1]};
+                        if constexpr (EPI == EPI_GELU_F16) v = gelu2(v);
+                        acc[i][j][4 * g + e] = v.x;
+                        acc[i][j][4 * g + e + 1] = v.y;
+                    }
+        if constexpr ((VAR & 2) != 0) {          // diagnostic: no epilogue stores (acc kept alive)
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
+            if (!more) break;
+            par = last ^ 1;
+            first = false;
+            continue;
+        }
+        // stores: each 32 x 32 (fp32) / 32 x 64 (fp16) block through the wave's private slab
+        char* slb = slabs + wave * 4096;
+        const int rr0 = lane >> 3, c16 = lane & 7;
+        if constexpr (EPI == EPI_BIAS_F32) {
+#pragma unroll
+            for (int i = 0; i < TM; ++i)
+#pragma unroll
+                for (int j = 0; j < TN; ++j) {
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                        *(f32x4*)(slb + frow * 128 + (((2 * g + fh) ^ (frow & 7)) << 4)) =
+                            (f32x4){acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
+                    float* ob = (float*)ep.out + (size_t)(cm0 + wm * WTM + MS * i) * ep.ldc + cn0 + wn * WTN + MS * j + 4 * c16;
+#pragma unroll
+                    for (int it = 0; it < 4; ++it) {
+                        const int rr = it * 8 + rr0;
+                        const uint4 v = *(const uint4*)(slb + rr * 128 + ((c16 ^ (rr & 7)) << 4));
+                        st16<64>((uint4*)(ob + (size_t)rr * ep.ldc), v);
+                    }
+                }
+        } else {
+            // fp16 image(s) of the 32 x 64 block i: image 0 = hi, image 1 (GELU, two-part) = lo*64
+            constexpr int NIMG = EPI == EPI_GELU_F16 ? 2 : 1;
+#pragma unroll
+            for (int img = 0; img < NIMG; ++img)
+#pragma unroll
+                for (int i = 0; i < TM; ++i) {
+#pragma unroll
+                    for (int j = 0; j < TN; ++j)
+#pragma unroll
+                        for (int gp = 0; gp < 2; ++gp) {
+                            half8 h;
+#pragma unroll
+                            for (int e = 0; e < 8; ++e) {
+                                const float x = acc[i][j][8 * gp + e];
+                                const f16 hi = (f16)x;
+                                h[e] = img == 0 ? hi : x3_lo(x, hi);
+                            }
+                            const uint4 hv = __builtin_bit_cast(uint4, h);
+                            const auto s0 = __builtin_amdgcn_permlane32_swap(hv.x, hv.z, false, false);
+                            const auto s1 = __builtin_amdgcn_permlane32_swap(hv.y, hv.w, false, false);
+                            const int c = 4 * j + 2 * gp + fh;
+                            *(uint4*)(slb + frow * 128 + ((c ^ (frow & 7)) << 4)) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+                        }
+                    f16* ob = (f16*)ep.out + (size_t)(cm0 + wm * WTM + MS * i) * ep.ldc + img * ep.nlog + cn0 + wn * WTN + 8 * c16;
+#pragma unroll
+                    for (int it = 0; it < 4; ++it) {
+                        const int rr = it * 8 + rr0;
+                        const uint4 v = *(const uint4*)(slb + rr * 128 + ((c16 ^ (rr & 7)) << 4));
+                        st16<64>((uint4*)(ob + (size_t)rr * ep.ldc), v);
+                    }
+                }
+        }
+        if (!more) break;
+        par = last ^ 1;
+        first = false;
+    }
+}
+
 int n_cus() {
     static int n = [] {
         int dev = 0, v = 0;
@@ -1080,6 +1406,29 @@ int n_cus() {
         return v > 0 ? v : 256;
     }();
     return n;
+}
+
+template <int EPI, int VAR = 262144>
+hipError_t launch_x3s(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep, hipStream_t st,
+                      int ldw = 0) {
+    constexpr int smem = 2 * 65536;                  // ring (2 x 64 KiB); + 32 KiB static wave slabs
+    if (K % 32 || K < 64 || M_pad % 256 || N_pad % 256) return hipErrorInvalidValue;
+    static bool attr_set = false;
+    if (!attr_set) {
+        hipError_t e = hipFuncSetAttribute((const void*)gemm_x3s_kernel<EPI, VAR>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+        if (e != hipSuccess) return e;
+        attr_set = true;
+    }
+    const int ntn = N_pad / 256, n_tiles = (M_pad / 256) * ntn;
+    const int cus = n_cus() / 8 * 8;
+    const int grid = n_tiles <= cus ? n_tiles : cus;
+    static const int gm_env = getenv("RS_GEMM_GROUP_M_X3S") ? atoi(getenv("RS_GEMM_GROUP_M_X3S")) : 0;
+    EpiArgs e2 = ep;
+    e2.group_m = gm_env > 0 ? gm_env : 8;
+    hipLaunchKernelGGL((gemm_x3s_kernel<EPI, VAR>), dim3(grid), dim3(512), smem, st, A, W, K, ldw > 0 ? ldw : 2 * K,
+                       ntn, n_tiles, e2);
+    return hipGetLastError();
 }
 
 template <int EPI, int VAR = 0>
@@ -1248,6 +1597,22 @@ hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
 
 int gemm_row_align() { return 256; }
 
+// Production split-operand fp16x3 GEMM: LDS-DMA by buffer_load ... lds (VAR 16) spread over the
+// MFMAs (VAR 4), younger wave half at s_setprio 1 (VAR 262144); tools/x3s_bench.py.
+hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_pad, int N_pad, int K,
+                           const EpiArgs& ep, hipStream_t st) {
+    if (M_pad % 256 || N_pad % 256 || K % 32 || K < 64 || ldw < 2 * K || M_pad <= 0) return hipErrorInvalidValue;
+    // the buffer descriptors address one 256-row panel: 32-bit byte offsets
+    if ((long long)256 * ldw * 2 >= (1ll << 31) || (long long)256 * 2 * K * 2 >= (1ll << 31)) return hipErrorInvalidValue;
+    constexpr int V = 262144 | 16 | 4;
+    switch (epi) {
+        case EPI_BIAS_F32: return launch_x3s<EPI_BIAS_F32, V>(A, W, M_pad, N_pad, K, ep, st, ldw);
+        case EPI_GELU_F16: return launch_x3s<EPI_GELU_F16, V>(A, W, M_pad, N_pad, K, ep, st, ldw);
+        case EPI_BIAS_F16: return launch_x3s<EPI_BIAS_F16, V>(A, W, M_pad, N_pad, K, ep, st, ldw);
+    }
+    return hipErrorInvalidValue;
+}
+
 hipError_t launch_gemm(int epi, const f16* A, const f16* W, int M_pad, int N_pad, int K,
                        const EpiArgs& ep, hipStream_t st, int tag) {
     if (M_pad % 256 || N_pad % 128 || K % 64 || M_pad <= 0) return hipErrorInvalidValue;
@@ -1292,6 +1657,37 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         default: return -1;                                                                           \
     }
     if (M % 256 || N % 256 || K % 64) return -1;
+    if (cfg == 33 || cfg == 34) {  // production x3s with W rows of 3K halfs (three-part weight image): 33 fp32, 34 GELU
+        ep.nlog = N;
+        if (cfg == 34) ep.ldc = 2 * N;
+        if (dbg == 1) e = launch_x3s<EPI_BIAS_F32, 262144>(a, w, M, N, K, ep, st, 3 * K);
+        else if (dbg == 2) e = launch_x3s<EPI_BIAS_F32, 262144 | 16>(a, w, M, N, K, ep, st, 3 * K);
+        else if (dbg == 3) e = launch_x3s<EPI_BIAS_F32, 262144 | 4>(a, w, M, N, K, ep, st, 3 * K);
+        else e = launch_gemm_x3s(cfg == 33 ? EPI_BIAS_F32 : EPI_GELU_F16, a, w, 3 * K, M, N, K, ep, st);
+        return e == hipSuccess ? 0 : -2;
+    }
+    if (cfg >= 30 && cfg <= 32) {  // split-operand fp16x3 (A [M, 2K], W [N, 2K] images): 30 fp16, 31 GELU image, 32 fp32
+        ep.nlog = N;
+        if (cfg == 31) ep.ldc = 2 * N;
+        if (cfg == 32 && dbg == 1) e = launch_x3s<EPI_BIAS_F32, 262144 | 1>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 2) e = launch_x3s<EPI_BIAS_F32, 262144 | 2>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 3) e = launch_x3s<EPI_BIAS_F32, 262144 | 3>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 4) e = launch_x3s<EPI_BIAS_F32, 0>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 5) e = launch_x3s<EPI_BIAS_F32, 262144 | 4>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 6) e = launch_x3s<EPI_BIAS_F32, 262144 | 4 | 2>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 7) e = launch_x3s<EPI_BIAS_F32, 262144 | 4 | 2 | 8>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 8) e = launch_x3s<EPI_BIAS_F32, 262144 | 2 | 8>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 9) e = launch_x3s<EPI_BIAS_F32, 262144 | 16>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 10) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 11) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 2>(a, w, M, N, K, ep, st);
+
+        else if (cfg == 32 && dbg == 15) e = launch_x3s<EPI_BIAS_F32, 262144>(a, w, M, N, K, ep, st);
+        else {   // dbg 0: the production variant (launch_gemm_x3s)
+            const int epi = cfg == 30 ? EPI_BIAS_F16 : cfg == 31 ? EPI_GELU_F16 : EPI_BIAS_F32;
+            e = launch_gemm_x3s(epi, a, w, 2 * K, M, N, K, ep, st);
+        }
+        return e == hipSuccess ? 0 : -2;
+    }
     if (cfg == 23 || cfg == 24) {  // + next tile's DMA issued before the epilogue math: 23 bias, 24 GELU
         e = cfg == 23 ? launch_persist<EPI_BIAS_F16, 786432 | 1048576 | 2097152>(a, w, M, N, K, ep, st)
                       : launch_persist<EPI_GELU_F16, 786432 | 1048576 | 2097152>(a, w, M, N, K, ep, st);

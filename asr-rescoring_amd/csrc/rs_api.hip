@@ -266,6 +266,15 @@ bool ffn2_f16() {
     return e && !strcmp(e, "f16");
 }
 
+// RS_X3S (fp16x3 mode, default 1): the encoder projections run as split-operand GEMMs
+// (gemm_x3s_kernel: two-part activation images, three fp16 products formed in registers, fp32
+// outputs + ln_res32 rows for the residual blocks); 0 = the K-concatenated three-part form.
+// Read per call (tests flip it in-process).
+bool x3s_on(const rs_bert_cfg& cf) {
+    const char* e = getenv("RS_X3S");
+    return !(e && !strcmp(e, "0")) && cf.hidden % 256 == 0 && cf.intermediate % 256 == 0;
+}
+
 // Runs the encoder + head over sequences [c.s0, c.s1) (one chunk).
 int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, const Chunk& c,
               int mode, float* d_out_rows /* indexed by sequence */) {
@@ -275,6 +284,8 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
     const int qkv_epi = q32 ? EPI_BIAS_F32 : EPI_BIAS_F16;
     const int rows = c.rows, ns = c.s1 - c.s0;
     const bool dedup = c.urows > 0;           // layer-0 Q/K/V over unique rows (MLM, fp16, kx == 1)
+    const bool x3s = kx == 3 && x3s_on(cf);   // split-operand GEMMs: full-row images are two-part
+    const int kxf = x3s ? 2 : kx;             // width factor of the full-row operand images
     float2* xst = m->xst.as<float2>();
     f16* h16 = m->h16.as<f16>();
     float* t32 = m->t32.as<float>();     // residual stream, pre-LN fp32 (LN rebuilt from xst)
@@ -286,12 +297,22 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
         // dedup: the per-copy pass keeps only the fp32 residual + LN statistics; the layer-0
         // GEMM operand is built over the chunk's unique rows (plan_unique_rows)
         HIPTRY(launch_embed_ln(d_tok, sm, c.s0, c.s1, 0, cf.mask_id, cf.vocab, m->word32, m->pos32,
-                               m->type32, m->eg, m->eb, cf.ln_eps, H, t32, xst, dedup ? nullptr : h16, kx, st));
+                               m->type32, m->eg, m->eb, cf.ln_eps, H, t32, xst, dedup ? nullptr : h16, kxf, st));
         if (dedup)
             HIPTRY(launch_embed_unique(d_tok, sm, c.s0, c.s1, cf.mask_id, cf.vocab, m->word32, m->pos32,
                                        m->type32, m->eg, m->eb, cf.ln_eps, H, h16, kx, st));
     }
     EpiArgs ep{};
+    // split-operand GEMM over m_valid rows: A two-part image, W rows of ldw halfs; profiled as
+    // MFMA work (three products of logical K)
+    auto gx = [&](int kind, int epi, const f16* A, const f16* W, int ldw, int m_valid, int N, int K, EpiArgs e,
+                  int n_flop_cols) -> int {
+        const int al = gemm_row_align();
+        e.m_valid = m_valid;
+        ProfScope ps(m, st, kind, 2.0 * m_valid * (double)n_flop_cols * 3.0 * K);
+        HIPTRY(launch_gemm_x3s(epi, A, W, ldw, (m_valid + al - 1) / al * al, N, K, e, st));
+        return RS_OK;
+    };
     auto gelu_ep = [&](const float* bias, f16* out) {
         EpiArgs e{};
         e.bias = bias; e.out = out; e.ldc = kx * F; e.kx = kx; e.nlog = F;
@@ -322,20 +343,49 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
             const size_t esz = q32 ? 4 : 2;
             ep.bias = L.bqkv + H;
             ep.out = (char*)qkv + H * esz;
-            if (int r = gemm(m, st, RS_K_QKV, qkv_epi, h16, L.wqkv + (size_t)H * kx * H, rows, 2 * H, kx * H, ep,
-                             2 * H)) return r;
+            if (x3s) {
+                if (int r = gx(RS_K_QKV, EPI_BIAS_F32, h16, L.wqkv + (size_t)H * 3 * H, 3 * H, rows, 2 * H, H, ep, 2 * H))
+                    return r;
+            } else if (int r = gemm(m, st, RS_K_QKV, qkv_epi, h16, L.wqkv + (size_t)H * kx * H, rows, 2 * H, kx * H, ep,
+                                    2 * H)) return r;
             f16* hq16g = m->hq16.as<f16>();
             {
                 ProfScope ps(m, st, RS_K_OTHER, 0);
-                HIPTRY(launch_gather_query_rows(h16, kx * H, sm, c.s0, c.s1, 0, hq16g, st));
+                HIPTRY(launch_gather_query_rows(h16, kxf * H, sm, c.s0, c.s1, 0, hq16g, st));
             }
             EpiArgs eq{};
             eq.bias = L.bqkv; eq.out = m->tq32.p; eq.ldc = H;
-            if (int r = gemm(m, st, RS_K_QKV, qkv_epi, hq16g, L.wqkv, ns, H, kx * H, eq, H)) return r;
+            if (x3s) {
+                if (int r = gx(RS_K_QKV, EPI_BIAS_F32, hq16g, L.wqkv, 3 * H, ns, H, H, eq, H)) return r;
+            } else if (int r = gemm(m, st, RS_K_QKV, qkv_epi, hq16g, L.wqkv, ns, H, kx * H, eq, H)) return r;
             qdense = m->tq32.p;
+        } else if (x3s) {
+            if (int r = gx(RS_K_QKV, EPI_BIAS_F32, h16, L.wqkv, 3 * H, rows, 3 * H, H, ep, last ? 2 * H : 3 * H)) return r;
         } else if (int r = gemm(m, st, RS_K_QKV, qkv_epi, h16, L.wqkv, uq ? c.urows : rows, 3 * H, kx * H, ep,
                                 last ? 2 * H : 3 * H)) return r;
-        if (!last) {
+        if (!last && x3s) {
+            // fp16x3 split-operand layer: projections write fp32 (o32 in the dead QKV buffer),
+            // the residual blocks close in ln_res32 (x32 <- LN(x32) + o32, next two-part image)
+            {
+                ProfScope ps(m, st, RS_K_ATTN, 0);
+                HIPTRY(launch_attention_full(qkv, true, sm, c.s0, c.s1, 0, H, nh, ctx, 2, st, false, c.max_len));
+            }
+            float* o32 = (float*)qkv;
+            ep = EpiArgs{}; ep.bias = L.bo; ep.out = o32; ep.ldc = H;
+            if (int r = gx(RS_K_OPROJ, EPI_BIAS_F32, ctx, L.wo, 3 * H, rows, H, H, ep, H)) return r;
+            {
+                ProfScope ps(m, st, RS_K_OTHER, 0);
+                HIPTRY(launch_ln_res32(t32, xst, xst, pg, pb, o32, rows, L.g1, L.be1, cf.ln_eps, H, h16, 2, st));
+            }
+            ep = EpiArgs{}; ep.bias = L.b1; ep.out = inter; ep.ldc = 2 * F; ep.kx = 2; ep.nlog = F;
+            if (int r = gx(RS_K_FFN1, EPI_GELU_F16, h16, L.w1, 3 * H, rows, F, H, ep, F)) return r;
+            ep = EpiArgs{}; ep.bias = L.b2; ep.out = o32; ep.ldc = H;
+            if (int r = gx(RS_K_FFN2, EPI_BIAS_F32, inter, L.w2, 3 * F, rows, H, F, ep, H)) return r;
+            {
+                ProfScope ps(m, st, RS_K_OTHER, 0);
+                HIPTRY(launch_ln_res32(t32, xst, xst, L.g1, L.be1, o32, rows, L.g2, L.be2, cf.ln_eps, H, h16, 2, st));
+            }
+        } else if (!last) {
             {
                 ProfScope ps(m, st, RS_K_ATTN, 0);
                 HIPTRY(launch_attention_full(qkv, q32, sm, c.s0, c.s1, 0, H, nh, ctx, kx, st, uq, c.max_len));

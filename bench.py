@@ -169,13 +169,17 @@ def main():
                 tsrc = f"profiles/{pmc_files[-1]}"
         alg_bytes = None
         if nk:
-            # operand images in (kx fp16 parts of A and W), output out (fp16 image / fp32)
-            out_b = {"qkv": 4 if kx == 3 else 2, "ffn1": 2 * kx}.get(dom, 4 if kx == 3 else 2)
-            alg_bytes = rows_per_launch * (kx * nk[1] * 2 + nk[0] * out_b) + kx * nk[0] * nk[1] * 2
+            # operand images in, output out.  fp16: [hi] operands, fp16 out.  fp16x3 (split-operand
+            # GEMMs, RS_X3S default): two-part [hi | lo*64] A and W read, fp32 out (QKV / O-proj /
+            # FFN2) or the two-part GELU image (FFN1); RS_X3S=0: three-part images, K x 3
+            x3s = kx == 3 and os.environ.get("RS_X3S", "1") != "0"
+            parts = 2 if x3s else kx
+            out_b = (4 if dom != "ffn1" else 2 * parts) if kx == 3 else 2
+            alg_bytes = rows_per_launch * (parts * nk[1] * 2 + nk[0] * out_b) + parts * nk[0] * nk[1] * 2
         roof = {"kernel": f"gemm_{args.precision}_{dom}", "bound": "mfma", "achieved": round(achieved, 2),
                 "peak": PEAK_FP16_TFLOPS, "unit": "TFLOP/s", "frac": round(achieved / PEAK_FP16_TFLOPS, 4),
-                "achieved_basis": ("MFMA work: 2*M*N*K over the kx-wide fp16 operand images "
-                                   f"(kx={kx}) / HIP-event launch time, vs the dense fp16 MFMA peak"),
+                "achieved_basis": (f"MFMA work: {kx} fp16 products of 2*M*N*K each (fp16x3: hi.hi + hi.lo + lo.hi) / "
+                                   "HIP-event launch time, vs the dense fp16 MFMA peak"),
                 "achieved_algorithmic": round(achieved_alg, 2),
                 "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes": alg_bytes,
                 "launches": n, "avg_launch_ms": round(ms / max(n, 1), 4),

@@ -99,9 +99,13 @@ def test_pll_tiny_golden(pll_tiny, golden_dir):
     assert rel_err(rows.cpu().numpy(), g["row_lp"]).max() < REL
 
 
-def test_pll_fp16x3_golden(w_base, golden_dir):
-    """Split-fp16 (x3) precision mode: fp32-level accuracy from fp16 MFMA."""
+@pytest.mark.parametrize("x3s", ["1", "0"])
+def test_pll_fp16x3_golden(w_base, golden_dir, monkeypatch, x3s):
+    """Split-fp16 (x3) precision mode: fp32-level accuracy from fp16 MFMA, with the split-operand
+    GEMMs (RS_X3S=1, default: two-part images, three products in registers) and with the
+    K-concatenated three-part form (RS_X3S=0)."""
     from asr_rescoring_amd.scorer import PLLScorer
+    monkeypatch.setenv("RS_X3S", x3s)
     g = _load(golden_dir, "pll_base.npz")
     s = PLLScorer(w_base, BERT_BASE, device=0, max_rows=4096, precision="fp16x3")
     pll, rows = s.score_nbest(g["tokens"], g["hyp_off"], return_rows=True)

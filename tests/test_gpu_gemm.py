@@ -70,3 +70,33 @@ def test_persistent_schedule_bitwise(gemm, name, N, K, gelu):
         o1 = gemm(prod, 0, A, W, b, torch.full((M, N), float("nan"), device="cuda", dtype=torch.float16))
         o2 = gemm(base, 0, A, W, b, torch.full((M, N), float("nan"), device="cuda", dtype=torch.float16))
         assert torch.equal(o1.view(torch.int16), o2.view(torch.int16)), (name, rep)
+
+
+def _split2(x):
+    hi = x.half()
+    return torch.cat([hi, ((x - hi.float()) * 64.0).half()], dim=1).contiguous()
+
+
+@pytest.mark.parametrize("name,N,K,gelu", SHAPES)
+def test_x3s_vs_torch_fp32(gemm, name, N, K, gelu):
+    """Split-operand fp16x3 GEMM (gemm_x3s_kernel, production variant through cfg 30-32 of
+    rs_debug_gemm): fp32 output and the two-part GELU image vs an fp32 torch matmul, at
+    fp32-level accuracy (3 fp16 products; measured ~2e-6 of max |C|)."""
+    M = 1024
+    g = torch.Generator(device="cuda").manual_seed(11)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    W = torch.randn(N, K, device="cuda", generator=g) * 0.05
+    b = torch.randn(N, device="cuda", generator=g) * 0.1
+    A2, W2 = _split2(A), _split2(W)
+    ref = A @ W.t() + b
+    lib = _lib.load()          # direct call: the logical K (the fixture passes A's width)
+    st = torch.cuda.current_stream().cuda_stream
+    for cfg, o in ((32, torch.empty(M, N, device="cuda")), (31, torch.empty(M, 2 * N, device="cuda", dtype=torch.float16))):
+        assert lib.rs_debug_gemm(cfg, 0, A2.data_ptr(), W2.data_ptr(), b.data_ptr(), o.data_ptr(), M, N, K, st) == 0
+        torch.cuda.synchronize()
+        if cfg == 32:
+            err = (o - ref).abs().max() / ref.abs().max()
+        else:
+            gl = torch.nn.functional.gelu(ref)
+            err = (o[:, :N].float() + o[:, N:].float() / 64.0 - gl).abs().max() / gl.abs().max()
+        assert err < 1e-5, (cfg, float(err))

@@ -8,6 +8,9 @@ import sys
 
 
 def short(n):
+    m = re.search(r"gemm_x3s_kernelILi(\d+)ELi(\d+)E", n)
+    if m:
+        return f"x3s<{m.group(1)},{m.group(2)}>"
     m = re.search(r"gemm_persist_kernelILi(\d+)ELi(\d+)E", n)
     if m:
         return f"persist<{m.group(1)},{m.group(2)}>"
