@@ -77,12 +77,14 @@ def _split2(x):
     return torch.cat([hi, ((x - hi.float()) * 64.0).half()], dim=1).contiguous()
 
 
+@pytest.mark.parametrize("dbg,M", [(0, 1024), (0, 40960), (19, 40960)])
 @pytest.mark.parametrize("name,N,K,gelu", SHAPES)
-def test_x3s_vs_torch_fp32(gemm, name, N, K, gelu):
-    """Split-operand fp16x3 GEMM (gemm_x3s_kernel, production variant through cfg 30-32 of
-    rs_debug_gemm): fp32 output and the two-part GELU image vs an fp32 torch matmul, at
-    fp32-level accuracy (3 fp16 products; measured ~2e-6 of max |C|)."""
-    M = 1024
+def test_x3s_vs_torch_fp32(gemm, name, N, K, gelu, dbg, M):
+    """Split-operand fp16x3 GEMM (gemm_x3s_kernel through cfg 31/32 of rs_debug_gemm; dbg 0 =
+    the production 16x16x32 form, 19 = the 32x32x16 form): fp32 output and the two-part GELU
+    image vs an fp32 torch matmul, at fp32-level accuracy (3 fp16 products; measured ~2e-6 of
+    max |C|).  M = 40960 gives every persistent workgroup several tiles (tile transitions,
+    the last tile of each workgroup)."""
     g = torch.Generator(device="cuda").manual_seed(11)
     A = torch.randn(M, K, device="cuda", generator=g)
     W = torch.randn(N, K, device="cuda", generator=g) * 0.05
@@ -92,7 +94,7 @@ def test_x3s_vs_torch_fp32(gemm, name, N, K, gelu):
     lib = _lib.load()          # direct call: the logical K (the fixture passes A's width)
     st = torch.cuda.current_stream().cuda_stream
     for cfg, o in ((32, torch.empty(M, N, device="cuda")), (31, torch.empty(M, 2 * N, device="cuda", dtype=torch.float16))):
-        assert lib.rs_debug_gemm(cfg, 0, A2.data_ptr(), W2.data_ptr(), b.data_ptr(), o.data_ptr(), M, N, K, st) == 0
+        assert lib.rs_debug_gemm(cfg, dbg, A2.data_ptr(), W2.data_ptr(), b.data_ptr(), o.data_ptr(), M, N, K, st) == 0
         torch.cuda.synchronize()
         if cfg == 32:
             err = (o - ref).abs().max() / ref.abs().max()
