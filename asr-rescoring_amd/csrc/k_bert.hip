@@ -725,16 +725,6 @@ attn16_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
 // (hi, scaled lo) with the same 80-half rows.  T <= 64 (one key block; the host routes longer
 // sequences to attn_full_kernel<float>).
 constexpr float LO_SCALE = 4096.f, LO_UNSCALE = 1.f / 4096.f;
-__device__ __forceinline__ void split8(const float* p, half8& hi, half8& lo) {
-    const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
-    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-        hi[e] = (f16)v[e];
-        lo[e] = (f16)((v[e] - (float)hi[e]) * LO_SCALE);
-    }
-}
-
 __global__ void __launch_bounds__(64, 2)
 attn16x3_kernel(const float* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
                 f16* __restrict__ ctx, int kx) {
@@ -753,11 +743,48 @@ attn16x3_kernel(const float* __restrict__ qkv, SeqMeta sm, int s0, int row0, int
         const fp16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) fp16x4*)p);
         return __builtin_bit_cast(half4, v);
     };
-    // V rows (fp32) -> hi / lo fp16 images: 16 float4 per row, 4 rows per pass of the wave
-#pragma unroll 4
+    // every V and K load of the (sequence, head) issued before any is used: 32 float4 per lane
+    // in flight (latency-bound kernel, 2 waves per SIMD), then V -> hi / lo LDS images and K
+    // -> hi / lo fragments
+    float4 vraw[16], kraw[4][2][2];
+#pragma unroll
     for (int it = 0; it < 16; ++it) {
         const int kr = it * 4 + (lane >> 4), c4 = (lane & 15) * 4;
-        const float4 v = kr < T ? *(const float4*)(base + (size_t)kr * ld + 2 * H + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        vraw[it] = kr < T ? *(const float4*)(base + (size_t)kr * ld + 2 * H + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int kt = 0; kt < 4; ++kt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int key = kt * 16 + r16;
+            const float* kp = base + (size_t)key * ld + H + ks * 32 + g * 8;
+            kraw[kt][ks][0] = key < T ? *(const float4*)kp : make_float4(0.f, 0.f, 0.f, 0.f);
+            kraw[kt][ks][1] = key < T ? *(const float4*)(kp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    // the first query tile's rows, prefetched the same way
+    float4 qraw[2][2];
+    auto load_q = [&](int q0) {
+        const int t = q0 + r16;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const float* qp = base + (size_t)t * ld + ks * 32 + g * 8;
+            qraw[ks][0] = t < T ? *(const float4*)qp : make_float4(0.f, 0.f, 0.f, 0.f);
+            qraw[ks][1] = t < T ? *(const float4*)(qp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    load_q(0);
+    auto split_raw = [](const float4 (&r)[2], half8& hi, half8& lo) {
+        const float v[8] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            hi[e] = (f16)v[e];
+            lo[e] = (f16)((v[e] - (float)hi[e]) * LO_SCALE);
+        }
+    };
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+        const int kr = it * 4 + (lane >> 4), c4 = (lane & 15) * 4;
+        const float4 v = vraw[it];
         const half4 h = {(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
         const half4 l = {(f16)((v.x - (float)h[0]) * LO_SCALE), (f16)((v.y - (float)h[1]) * LO_SCALE),
                          (f16)((v.z - (float)h[2]) * LO_SCALE), (f16)((v.w - (float)h[3]) * LO_SCALE)};
@@ -768,11 +795,7 @@ attn16x3_kernel(const float* __restrict__ qkv, SeqMeta sm, int s0, int row0, int
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            const int key = kt * 16 + r16;
-            if (key < T) split8(base + (size_t)key * ld + H + ks * 32 + g * 8, kfh[kt][ks], kfl[kt][ks]);
-            else kfh[kt][ks] = kfl[kt][ks] = (half8){};
-        }
+        for (int ks = 0; ks < 2; ++ks) split_raw(kraw[kt][ks], kfh[kt][ks], kfl[kt][ks]);
     __syncthreads();
     half8 vfh[4][2], vfl[4][2];
 #pragma unroll
@@ -791,10 +814,8 @@ attn16x3_kernel(const float* __restrict__ qkv, SeqMeta sm, int s0, int row0, int
         const int t = q0 + r16;
         half8 qh[2], ql[2];
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            if (t < T) split8(base + (size_t)t * ld + ks * 32 + g * 8, qh[ks], ql[ks]);
-            else qh[ks] = ql[ks] = (half8){};
-        }
+        for (int ks = 0; ks < 2; ++ks) split_raw(qraw[ks], qh[ks], ql[ks]);
+        if (q0 + 16 < T) load_q(q0 + 16);             // next tile's rows under this tile's math
         f32x4 x[4];
         float bm = -INFINITY;
 #pragma unroll

@@ -1467,7 +1467,17 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             }
             char* slb = slabs + wave * 4096;
             const int rr0 = lane >> 3, c16 = lane & 7;
-            if constexpr (EPI == EPI_BIAS_F32) {
+            if constexpr (EPI == EPI_BIAS_F32 && (VAR & 256) != 0) {
+                // VAR 256: direct 16-B stores from the accumulator layout (4 lanes cover 64
+                // contiguous bytes of a row), no slab pass
+#pragma unroll
+                for (int i = 0; i < 8; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        float* ob = (float*)ep.out + (size_t)(cm0 + wm * WTM + 16 * i + r16) * ep.ldc + cn0 + wn * WTN + 16 * j + 4 * q4;
+                        st16<64>((uint4*)ob, __builtin_bit_cast(uint4, acc16[i][j]));
+                    }
+            } else if constexpr (EPI == EPI_BIAS_F32) {
                 // 32 x 32 fp32 slab blocks: row blocks 2 i2 + a, column blocks 2 j2 + b
 #pragma unroll
                 for (int i2 = 0; i2 < 4; ++i2)
@@ -1490,10 +1500,11 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 // fp16 image(s) in 32 x 64 slab blocks (row blocks 2 i2 + a, all four column
                 // blocks): image 0 = hi, image 1 (GELU, two-part) = lo*64
                 constexpr int NIMG = EPI == EPI_GELU_F16 ? 2 : 1;
+                // row-block pair outermost: its accumulators die after both images are out
 #pragma unroll
-                for (int img = 0; img < NIMG; ++img)
+                for (int i2 = 0; i2 < 4; ++i2)
 #pragma unroll
-                    for (int i2 = 0; i2 < 4; ++i2) {
+                    for (int img = 0; img < NIMG; ++img) {
 #pragma unroll
                         for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -1897,6 +1908,8 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         else if (cfg == 32 && dbg == 17) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 128>(a, w, M, N, K, ep, st);
         else if (cfg == 32 && dbg == 18) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 3>(a, w, M, N, K, ep, st);
         else if (cfg == 31 && dbg == 16) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 20) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 2>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 21) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 256>(a, w, M, N, K, ep, st);
         else if (cfg == 32 && dbg == 19) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4>(a, w, M, N, K, ep, st);
         else if (cfg == 31 && dbg == 19) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4>(a, w, M, N, K, ep, st);
         else if (cfg == 30 && dbg == 19) e = launch_x3s<EPI_BIAS_F16, 262144 | 16 | 4>(a, w, M, N, K, ep, st);
