@@ -74,7 +74,7 @@ _SIGS = {
     "rs_trainer_get_grad": (ctypes.c_int, [P, ctypes.c_char_p, P, I64]),
     "rs_trainer_reset_optimizer": (ctypes.c_int, [P]),
     "rs_trainer_destroy": (None, [P]),
-    "rs_bertscore_recall": (ctypes.c_int, [P, P, P, P, I32, P, P]),
+    "rs_bertscore_recall": (ctypes.c_int, [P, P, P, P, I32, P, P, P]),
     "rs_align": (ctypes.c_int, [P, P, P, P, I32, P, P, P, P, P, P, P, I32, P]),
     "rs_fuse_rerank": (ctypes.c_int, [P, P, P, P, I32, I32, P, I32, I32, P, P]),
     "rs_corpus_edits": (ctypes.c_int, [P, P, P, I32, I32, P, P]),

@@ -385,6 +385,7 @@ def rmbr(cfg) -> Dict[str, float]:
                                device=_dev(cfg), max_rows=get(cfg, "max_rows", 65536),
                                precision=get(cfg, "precision", "fp16x3"))
         which = str(get(cfg, "bertscore_component", "R")).upper()
+        bs_batch = int(get(cfg, "batch_size", 128))     # RMBR/config/RMBR.yaml: bert_score batch_size
 
     def split_nb(prefix):
         nonlocal tok
@@ -401,14 +402,15 @@ def rmbr(cfg) -> Dict[str, float]:
     def decode(nb, nb_tok, k):
         if scorer is None:
             return rerank.mbr_decode(nb, k, device=_dev(cfg))
-        return BS.mbr_decode(scorer, nb_tok, k, which)
+        return BS.mbr_decode(scorer, nb_tok, k, which, batch_size=bs_batch)
 
     dev, dev_tok = split_nb("dev")
     log.info("Running MBR on dev set to find best length ...")
     if scorer is None:
         best_cer, best_len, best_sc = rerank.find_best_length(dev, n_best, device=_dev(cfg))
     else:
-        best_cer, best_len, best_sc = BS.find_best_length(scorer, dev_tok, n_best, which, nb_chars=dev)
+        best_cer, best_len, best_sc = BS.find_best_length(scorer, dev_tok, n_best, which, nb_chars=dev,
+                                                          batch_size=bs_batch)
     log.info(f"best_cer: {best_cer}")
     log.info(f"best_length: {best_len}")
     print("best_cer: ", best_cer)

@@ -163,7 +163,7 @@ hipError_t launch_embed_unique(const int* tok, SeqMeta sm, int s0, int s1, int m
                                const float* b, float eps, int H, f16* h16u, int kx, hipStream_t st);
 // BERTScore recall matrix (k_bertscore.hip); items = (utterance, j0, j1, -) ref-column runs
 hipError_t launch_bertscore_recall(const f16* emb, int H, const int* hyp_off, const int* utt_off,
-                                   const long long* mat_off, const int4* items, int n_items, float* rmat,
+                                   const long long* mat_off, const int4* items, int n_items, float* rmat, float* rmat0,
                                    hipStream_t st);
 // Last hidden state, L2-normalised per token, fp16 at out[(tok_off + t) * H] (BERTScore)
 hipError_t launch_embed_out(const float* x32, const float2* stats, const float* g, const float* b,

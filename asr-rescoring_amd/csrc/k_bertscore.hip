@@ -13,7 +13,10 @@
 // MFMA tile, v_mfma_f32_32x32x16_f16, fp32 accumulation) straight from global memory, fold
 // each tile's 32x64 cosines into per-(cand hypothesis, column) maxima with LDS ordered-int
 // atomic max (exact, order-independent), then reduce the maxima of each ref hypothesis'
-// interior columns in column order.
+// interior columns in column order.  A second matrix (rmat0, optional) takes each maximum as
+// max(m, 0): bert_score multiplies the cosines by the pair batch's pad masks, so when the cand
+// is shorter than the longest cand of its batch a padded position offers a cosine of 0 to the
+// max (bertscore.py picks R or R0 per pair from the caller's batch layout).
 #include "common.h"
 
 namespace {
@@ -38,7 +41,7 @@ template <int NV>
 __global__ void __launch_bounds__(512)
 bs_recall_kernel(const f16* __restrict__ emb, const int* __restrict__ hyp_off,
                  const int* __restrict__ utt_off, const long long* __restrict__ mat_off,
-                 const int4* __restrict__ items, float* __restrict__ rmat) {
+                 const int4* __restrict__ items, float* __restrict__ rmat, float* __restrict__ rmat0) {
     using C = BsCfg<NV>;
     constexpr int H = C::H, LDB = C::LDB, NG = C::NG, NKB = H / 64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -125,15 +128,22 @@ bs_recall_kernel(const f16* __restrict__ emb, const int* __restrict__ hyp_off,
                 const int tb = ho[j], te = ho[j + 1];
                 const int Tj = te - tb, Ti = ho[i + 1] - ho[i];
                 float* dst = rmat + mo + (long long)i * n + j;
+                float* dst0 = rmat0 ? rmat0 + mo + (long long)i * n + j : nullptr;
                 float acc = cs == cbeg ? 0.f : *dst;
+                float acc0 = cs == cbeg || !dst0 ? 0.f : *dst0;
                 if (Tj > 2 && Ti > 2) {
                     const float w = 1.0f / (float)(Tj - 2);
                     const int lo = max(tb + 1, cs), hi = min(te - 1, cs + 64);
-                    for (int t = lo; t < hi; ++t) acc += key2f(cm[(i - g0) * 64 + (t - cs)]) * w;
+                    for (int t = lo; t < hi; ++t) {
+                        const float v = key2f(cm[(i - g0) * 64 + (t - cs)]);
+                        acc += v * w;
+                        acc0 += fmaxf(v, 0.f) * w;
+                    }
                 } else {
-                    acc = 0.f;                    // bert_score: empty cand or ref -> P = R = 0
+                    acc = acc0 = 0.f;             // bert_score: empty cand or ref -> P = R = 0
                 }
                 *dst = acc;
+                if (dst0) *dst0 = acc0;
             }
             __syncthreads();                      // cm is cleared by the next group
         }
@@ -142,7 +152,7 @@ bs_recall_kernel(const f16* __restrict__ emb, const int* __restrict__ hyp_off,
 
 template <int NV>
 hipError_t launch_bs(const f16* emb, const int* hyp_off, const int* utt_off, const long long* mat_off,
-                     const int4* items, int n_items, float* rmat, hipStream_t st) {
+                     const int4* items, int n_items, float* rmat, float* rmat0, hipStream_t st) {
     static bool attr = false;
     if (!attr) {
         hipError_t e = hipFuncSetAttribute((const void*)bs_recall_kernel<NV>,
@@ -151,7 +161,7 @@ hipError_t launch_bs(const f16* emb, const int* hyp_off, const int* utt_off, con
         attr = true;
     }
     hipLaunchKernelGGL(bs_recall_kernel<NV>, dim3(n_items), dim3(512), BsCfg<NV>::smem, st, emb, hyp_off,
-                       utt_off, mat_off, items, rmat);
+                       utt_off, mat_off, items, rmat, rmat0);
     return hipGetLastError();
 }
 
@@ -159,13 +169,13 @@ hipError_t launch_bs(const f16* emb, const int* hyp_off, const int* utt_off, con
 
 hipError_t launch_bertscore_recall(const f16* emb, int H, const int* hyp_off, const int* utt_off,
                                    const long long* mat_off, const int4* items, int n_items, float* rmat,
-                                   hipStream_t st) {
+                                   float* rmat0, hipStream_t st) {
     if (n_items <= 0) return hipSuccess;
     switch (H) {
-        case 256: return launch_bs<1>(emb, hyp_off, utt_off, mat_off, items, n_items, rmat, st);
-        case 512: return launch_bs<2>(emb, hyp_off, utt_off, mat_off, items, n_items, rmat, st);
-        case 768: return launch_bs<3>(emb, hyp_off, utt_off, mat_off, items, n_items, rmat, st);
-        case 1024: return launch_bs<4>(emb, hyp_off, utt_off, mat_off, items, n_items, rmat, st);
+        case 256: return launch_bs<1>(emb, hyp_off, utt_off, mat_off, items, n_items, rmat, rmat0, st);
+        case 512: return launch_bs<2>(emb, hyp_off, utt_off, mat_off, items, n_items, rmat, rmat0, st);
+        case 768: return launch_bs<3>(emb, hyp_off, utt_off, mat_off, items, n_items, rmat, rmat0, st);
+        case 1024: return launch_bs<4>(emb, hyp_off, utt_off, mat_off, items, n_items, rmat, rmat0, st);
         default: return hipErrorInvalidValue;
     }
 }

@@ -818,7 +818,7 @@ int rs_token_embed(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, 
 }
 
 int rs_bertscore_recall(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off,
-                        const int32_t* h_utt_off, int32_t n_utt, float* d_rmat, void* stream) {
+                        const int32_t* h_utt_off, int32_t n_utt, float* d_rmat, float* d_rmat0, void* stream) {
     if (!m || !h_hyp_off || !h_utt_off || n_utt < 0 || (n_utt > 0 && (!d_tok || !d_rmat)))
         return fail(RS_EARG, "null argument");
     if (n_utt == 0) return RS_OK;
@@ -876,7 +876,7 @@ int rs_bertscore_recall(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_
     int* d = m->plan.as<int>();
     ProfScope ps(m, st, RS_K_OTHER, 0);
     HIPTRY(launch_bertscore_recall(m->emb.as<f16>(), H, d + w_items + w_moff, d + w_items + w_moff + n_hyp + 1,
-                                   (const long long*)(d + w_items), (const int4*)d, n_items, d_rmat, st));
+                                   (const long long*)(d + w_items), (const int4*)d, n_items, d_rmat, d_rmat0, st));
     return RS_OK;
 }
 

@@ -160,9 +160,13 @@ int rs_token_embed(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, 
  *   mat_off(u) = sum_{v<u} n_v^2 (n_u = h_utt_off[u+1] - h_utt_off[u]);
  * P(i|j) = R(j|i), F = 2PR/(P+R).  R = mean over ref j's tokens except [CLS]/[SEP] of the max
  * cosine over all of cand i's tokens; 0 when either hypothesis is empty (T == 2).
+ * d_rmat0 (optional, same layout): each maximum taken as max(m, 0) — bert_score's value when
+ * the cand is shorter than the longest cand of its pair batch (the padded positions' masked
+ * cosine 0 joins the max, bert_score/utils.py greedy_cos_idf); the caller picks R or R0 per
+ * pair from its batch layout (bertscore.py).
  * h_hyp_off[0] == 0, h_utt_off[0] == 0 (host arrays); every hypothesis has T >= 2. */
 int rs_bertscore_recall(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off,
-                        const int32_t* h_utt_off, int32_t n_utt, float* d_rmat, void* stream);
+                        const int32_t* h_utt_off, int32_t n_utt, float* d_rmat, float* d_rmat0, void* stream);
 
 /* RMBR mbr_decode (RMBR/mbr.py:5-28) with the BERTScore utility component `which`
  * (RS_BS_P/R/F) of cand hyp_i against ref hyp_j, from the rs_bertscore_recall matrix;

@@ -9,8 +9,9 @@ reference (no requirements file); its published algorithm (bert_score 0.3.x,
   ``bert_encode`` returns that truncated model's last hidden state.
 * ``score(idf=False)``: idf weight 1 for every token except [CLS] and [SEP] (0).
 * ``bert_cos_score_idf``: unique sentences embedded once; pairs processed in batches of
-  ``batch_size`` (64), each side padded with ``pad_batch_stats`` (embedding pad value 2.0,
-  idf pad 0, mask = real length).
+  ``batch_size`` (library default 64; the reference's RMBR config passes 128), each side padded
+  with ``pad_batch_stats`` (embedding pad value 2.0, idf pad 0, mask = real length) — so a
+  padded position's masked cosine 0 joins the other side's max.
 * ``greedy_cos_idf``: embeddings divided by their L2 norm; ``sim = bmm(hyp, ref^T) * masks``;
   P = sum(max over ref of sim * hyp_idf / sum hyp_idf), R = same over ref; F = 2PR/(P+R);
   P and R set to 0 when a side has only [CLS][SEP]; NaN F set to 0.
@@ -130,6 +131,48 @@ def utility_matrices(model: TorchBert, utts: List[List[Sequence[int]]], which: s
     for (u, i, j), v in zip(where, val):
         mats[u][i, j] = v
     return mats
+
+
+def pair_recall(model: TorchBert, utts: List[List[Sequence[int]]]) -> List[Tuple[np.ndarray, np.ndarray]]:
+    """Per utterance, for every ordered pair (cand i, ref j) of its hypotheses without any batch
+    padding: R[i, j] = mean over ref j's tokens except [CLS]/[SEP] of the max cosine over all of
+    cand i's tokens, and R0[i, j] with each max clamped at 0 (the value a padded cand gets in
+    bert_score's masked max); 0 when either side is empty ([CLS][SEP])."""
+    out = []
+    for hyps in utts:
+        embs = embed_sentences(model, [list(h) for h in hyps])
+        embs = [e / torch.norm(e, dim=-1, keepdim=True) for e in embs]
+        n = len(hyps)
+        R, R0 = np.zeros((n, n), np.float32), np.zeros((n, n), np.float32)
+        for i in range(n):
+            for j in range(n):
+                if len(hyps[i]) <= 2 or len(hyps[j]) <= 2:
+                    continue
+                m = (embs[i] @ embs[j].t()).max(dim=0)[0][1:-1]
+                R[i, j] = float(m.mean())
+                R0[i, j] = float(m.clamp_min(0.0).mean())
+        out.append((R, R0))
+    return out
+
+
+def rmbr_mbr_decode(model: TorchBert, utts: List[List[Sequence[int]]], k: int, which: str = "R",
+                    batch_size: int = 128) -> Tuple[np.ndarray, np.ndarray]:
+    """RMBR/mbr.py:5-28 with BertScoreFunction (RMBR/utility_functions.py:9-22): the pair list
+    (cand = hyp i repeated k-1 times, refs = the other hyps of the top k), one bert_score call
+    over it in batches of ``batch_size`` (RMBR config: 128), scores reshaped to [U, k, k-1],
+    float32 torch-CPU sum, first max."""
+    cands, refs = [], []
+    for hyps in utts:
+        for i in range(k):
+            cands += [list(hyps[i])] * (k - 1)
+            refs += [list(h) for h in hyps[:i] + hyps[i + 1:k]]
+    P, R, F = bert_score(model, cands, refs, batch_size=batch_size)
+    val = {"P": P, "R": R, "F": F}[which].reshape(len(utts), k, k - 1)
+    scores = np.zeros((len(utts), k), np.float32)
+    for u in range(len(utts)):
+        for i in range(k):
+            scores[u, i] = torch_cpu_sum_f32(val[u, i])
+    return np.argmax(scores, axis=-1), scores
 
 
 def mbr_decode(k: int, mats: List[np.ndarray]) -> Tuple[np.ndarray, np.ndarray]:
