@@ -156,6 +156,8 @@ hipError_t launch_ln_res_rows(float* x32, const float2* stats, float2* stats_out
 hipError_t launch_ln_res32(float* x32, const float2* stats, float2* stats_out, const float* pg, const float* pb,
                            const float* o32, int rows, const float* g, const float* b, float eps, int H, f16* y16,
                            int kx, hipStream_t st);
+hipError_t launch_ln_res_img(f16* h16, const float* o32, int rows, const float* g, const float* b, float eps, int H,
+                             hipStream_t st);
 // Unique layer-0 rows (dedup): for every hypothesis of the chunk its T rows, and every
 // sequence's [MASK] row, as the fp16 operand image of LN(embedding) (rows of SeqMeta.urow_*)
 hipError_t launch_embed_unique(const int* tok, SeqMeta sm, int s0, int s1, int mask_id, int vocab,
@@ -167,7 +169,8 @@ hipError_t launch_bertscore_recall(const f16* emb, int H, const int* hyp_off, co
                                    hipStream_t st);
 // Last hidden state, L2-normalised per token, fp16 at out[(tok_off + t) * H] (BERTScore)
 hipError_t launch_embed_out(const float* x32, const float2* stats, const float* g, const float* b,
-                            SeqMeta sm, int s0, int s1, int row0, int H, f16* out, hipStream_t st);
+                            SeqMeta sm, int s0, int s1, int row0, int H, f16* out, hipStream_t st,
+                            const f16* himg = nullptr);
 // max_len: longest sequence of the launch (0 = unknown): the 16x16x32 kernel serves chunks whose
 // sequences all fit one 64-key block, the 32x32x16 kernel the others (fewer K/V reloads).
 // dedup: qkv holds unique rows; sequence s, position t reads row (t == mask_pos ? urow_m : urow_h + t)
@@ -178,7 +181,7 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
 hipError_t launch_attention_query(const void* qkv, bool qkv32, const float* x32, const float2* stats,
                                   const float* g, const float* b, SeqMeta sm, int s0, int s1,
                                   int row0, int H, int heads, f16* ctxq, float* resq, int kx,
-                                  hipStream_t st, const void* qd = nullptr);
+                                  hipStream_t st, const void* qd = nullptr, const f16* himg = nullptr);
 // dst[s - s0] = src[row of sequence s's query position], ld halfs per row
 hipError_t launch_gather_query_rows(const f16* src, int ld, SeqMeta sm, int s0, int s1, int row0, f16* dst,
                                    hipStream_t st);

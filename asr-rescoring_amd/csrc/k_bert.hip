@@ -118,8 +118,8 @@ embed_ln_kernel(const int* __restrict__ tok, SeqMeta sm, int s0, int row0, int m
         embed_row<NV>(tok, toff, t, mp, mask_id, vocab, word, pos, type0, lane, x);
         const size_t r = (size_t)(rs + t);
 #pragma unroll
-        for (int v = 0; v < NV; ++v) *(float4*)(x32 + r * H + v * 256 + lane * 4) = x[v];
-        ln_store<NV>(x, g, b, eps, lane, nullptr, stats + r, h16 ? h16 + r * kx * H : nullptr, kx);
+        for (int v = 0; v < NV; ++v) if (x32) *(float4*)(x32 + r * H + v * 256 + lane * 4) = x[v];
+        ln_store<NV>(x, g, b, eps, lane, nullptr, stats ? stats + r : nullptr, h16 ? h16 + r * kx * H : nullptr, kx);
     }
 }
 
@@ -210,6 +210,32 @@ ln_res32_kernel(float* __restrict__ x32, const float2* stats, float2* stats_out,
         *(float4*)(x32 + (size_t)row * H + c) = x[v];
     }
     ln_store<NV>(x, g, b, eps, lane, nullptr, stats_out + row, y16 + (size_t)row * kx * H, kx);
+}
+
+// Residual + LayerNorm of a split-operand layer with the residual stream held ONLY as the
+// two-part operand image of the normalised hidden state (h = hi + lo/64, ~22 bits):
+//   h16 <- image(LN(o32 + h)), in place (one wave per row reads the whole row first).
+// 12 B per element (o32, the image in, the image out) instead of ln_res32's 16 (no fp32
+// pre-LN stream, no statistics): the next block's residual is the image itself.
+template <int NV>
+__global__ void __launch_bounds__(256)
+ln_res_img_kernel(f16* __restrict__ h16, const float* __restrict__ o32, int rows, const float* __restrict__ g,
+                  const float* __restrict__ b, float eps) {
+    constexpr int H = NV * 256;
+    const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (row >= rows) return;
+    f16* hr = h16 + (size_t)row * 2 * H;
+    float4 x[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+        const int c = v * 256 + lane * 4;
+        const half4 hi = *(const half4*)(hr + c), lo = *(const half4*)(hr + H + c);
+        const float4 o = *(const float4*)(o32 + (size_t)row * H + c);
+        x[v] = make_float4(o.x + ((float)hi[0] + (float)lo[0] * X3_DOWN), o.y + ((float)hi[1] + (float)lo[1] * X3_DOWN),
+                           o.z + ((float)hi[2] + (float)lo[2] * X3_DOWN), o.w + ((float)hi[3] + (float)lo[3] * X3_DOWN));
+    }
+    ln_store<NV>(x, g, b, eps, lane, nullptr, nullptr, hr, 2);
 }
 
 __device__ __forceinline__ void load8(const f16* p, float (&o)[8]) {
@@ -885,7 +911,7 @@ __global__ void __launch_bounds__(64)
 attn_query_kernel(const QT* __restrict__ qkv, const QT* __restrict__ qd, const float* __restrict__ x32,
                   const float2* __restrict__ stats, const float* __restrict__ lg,
                   const float* __restrict__ lb, SeqMeta sm, int s0, int row0, int H,
-                  f16* __restrict__ ctxq, float* __restrict__ resq, int kx) {
+                  f16* __restrict__ ctxq, float* __restrict__ resq, int kx, const f16* __restrict__ himg) {
     __shared__ float sq[64];
     __shared__ float sp[64];
     const int s = s0 + blockIdx.x, h = blockIdx.y;
@@ -927,10 +953,11 @@ attn_query_kernel(const QT* __restrict__ qkv, const QT* __restrict__ qd, const f
     }
     const int s_loc = s - s0;
     put_split(ctxq + (size_t)s_loc * kx * H, h * 64 + lane, H, kx, acc / l);
-    {   // residual of the scored row: LN of its pre-LN sum
+    {   // residual of the scored row: LN of its pre-LN sum, or the normalised state's image
         const int c = h * 64 + lane;
         const size_t r = (size_t)(rs + qi);
-        resq[(size_t)s_loc * H + c] = ln_apply(x32[r * H + c], stats[r], lg[c], lb[c]);
+        resq[(size_t)s_loc * H + c] = himg ? (float)himg[r * 2 * H + c] + (float)himg[r * 2 * H + H + c] * X3_DOWN
+                                           : ln_apply(x32[r * H + c], stats[r], lg[c], lb[c]);
     }
 }
 
@@ -1037,23 +1064,29 @@ template <int NV>
 __global__ void __launch_bounds__(256)
 embed_out_kernel(const float* __restrict__ x32, const float2* __restrict__ stats,
                  const float* __restrict__ g, const float* __restrict__ b, SeqMeta sm, int s0,
-                 int row0, f16* __restrict__ out) {
+                 int row0, f16* __restrict__ out, const f16* __restrict__ himg) {
     constexpr int H = NV * 256;
     const int s = s0 + blockIdx.x;
     const int T = sm.len[s], rs = sm.row[s] - row0, toff = sm.tok_off[s];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     for (int t = wave; t < T; t += 4) {
         const size_t r = (size_t)(rs + t);
-        const float2 st = stats[r];
         float4 y[NV];
         float q = 0.f;
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             const int c = v * 256 + lane * 4;
-            const float4 x = *(const float4*)(x32 + r * H + c);
-            const float4 gg = *(const float4*)(g + c), bb = *(const float4*)(b + c);
-            y[v] = make_float4(ln_apply(x.x, st, gg.x, bb.x), ln_apply(x.y, st, gg.y, bb.y),
-                               ln_apply(x.z, st, gg.z, bb.z), ln_apply(x.w, st, gg.w, bb.w));
+            if (himg) {                       // the normalised state's two-part image
+                const half4 hi = *(const half4*)(himg + r * 2 * H + c), lo = *(const half4*)(himg + r * 2 * H + H + c);
+                y[v] = make_float4((float)hi[0] + (float)lo[0] * X3_DOWN, (float)hi[1] + (float)lo[1] * X3_DOWN,
+                                   (float)hi[2] + (float)lo[2] * X3_DOWN, (float)hi[3] + (float)lo[3] * X3_DOWN);
+            } else {
+                const float2 st = stats[r];
+                const float4 x = *(const float4*)(x32 + r * H + c);
+                const float4 gg = *(const float4*)(g + c), bb = *(const float4*)(b + c);
+                y[v] = make_float4(ln_apply(x.x, st, gg.x, bb.x), ln_apply(x.y, st, gg.y, bb.y),
+                                   ln_apply(x.z, st, gg.z, bb.z), ln_apply(x.w, st, gg.w, bb.w));
+            }
             q += y[v].x * y[v].x + y[v].y * y[v].y + y[v].z * y[v].z + y[v].w * y[v].w;
         }
         const float nrm = sqrtf(wave_sum(q));
@@ -1068,10 +1101,10 @@ embed_out_kernel(const float* __restrict__ x32, const float2* __restrict__ stats
 }
 
 hipError_t launch_embed_out(const float* x32, const float2* stats, const float* g, const float* b,
-                            SeqMeta sm, int s0, int s1, int row0, int H, f16* out, hipStream_t st) {
+                            SeqMeta sm, int s0, int s1, int row0, int H, f16* out, hipStream_t st, const f16* himg) {
     const int n = s1 - s0;
     if (n <= 0) return hipSuccess;
-#define RS_EO(NV) hipLaunchKernelGGL(embed_out_kernel<NV>, dim3(n), dim3(256), 0, st, x32, stats, g, b, sm, s0, row0, out)
+#define RS_EO(NV) hipLaunchKernelGGL(embed_out_kernel<NV>, dim3(n), dim3(256), 0, st, x32, stats, g, b, sm, s0, row0, out, himg)
     switch (H) {
         case 256: RS_EO(1); break;
         case 512: RS_EO(2); break;
@@ -1114,6 +1147,22 @@ hipError_t launch_ln_res32(float* x32, const float2* stats, float2* stats_out, c
         default: return hipErrorInvalidValue;
     }
 #undef RS_LN32
+    return hipGetLastError();
+}
+
+hipError_t launch_ln_res_img(f16* h16, const float* o32, int rows, const float* g, const float* b, float eps, int H,
+                             hipStream_t st) {
+    if (rows <= 0) return hipSuccess;
+    const dim3 grid((rows + 3) / 4), block(256);
+#define RS_LNI(NV) hipLaunchKernelGGL(ln_res_img_kernel<NV>, grid, block, 0, st, h16, o32, rows, g, b, eps)
+    switch (H) {
+        case 256: RS_LNI(1); break;
+        case 512: RS_LNI(2); break;
+        case 768: RS_LNI(3); break;
+        case 1024: RS_LNI(4); break;
+        default: return hipErrorInvalidValue;
+    }
+#undef RS_LNI
     return hipGetLastError();
 }
 
@@ -1201,13 +1250,13 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
 hipError_t launch_attention_query(const void* qkv, bool qkv32, const float* x32, const float2* stats,
                                   const float* g, const float* b, SeqMeta sm, int s0, int s1,
                                   int row0, int H, int heads, f16* ctxq, float* resq, int kx,
-                                  hipStream_t st, const void* qd) {
+                                  hipStream_t st, const void* qd, const f16* himg) {
     if (s1 <= s0) return hipSuccess;
     const dim3 grid(s1 - s0, heads);
     if (qkv32)
-        hipLaunchKernelGGL(attn_query_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, (const float*)qd, x32, stats, g, b, sm, s0, row0, H, ctxq, resq, kx);
+        hipLaunchKernelGGL(attn_query_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, (const float*)qd, x32, stats, g, b, sm, s0, row0, H, ctxq, resq, kx, himg);
     else
-        hipLaunchKernelGGL(attn_query_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, (const f16*)qd, x32, stats, g, b, sm, s0, row0, H, ctxq, resq, kx);
+        hipLaunchKernelGGL(attn_query_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, (const f16*)qd, x32, stats, g, b, sm, s0, row0, H, ctxq, resq, kx, himg);
     return hipGetLastError();
 }
 

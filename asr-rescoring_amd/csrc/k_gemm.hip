@@ -1444,17 +1444,24 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             stage(last ^ 1, 0);
         }
         if constexpr (M16) {
+            // bias (+ GELU) of row blocks [i0, i1)
+            auto finish = [&](int i0, int i1) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
+                for (int i = i0; i < i1; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j)
+                    for (int j = 0; j < 4; ++j)
 #pragma unroll
-                    for (int e = 0; e < 4; e += 2) {
-                        f32x2 v = {acc16[i][j][e] + bq[j][e], acc16[i][j][e + 1] + bq[j][e + 1]};
-                        if constexpr (EPI == EPI_GELU_F16) v = gelu2(v);
-                        acc16[i][j][e] = v.x;
-                        acc16[i][j][e + 1] = v.y;
-                    }
+                        for (int e = 0; e < 4; e += 2) {
+                            f32x2 v = {acc16[i][j][e] + bq[j][e], acc16[i][j][e + 1] + bq[j][e + 1]};
+                            if constexpr (EPI == EPI_GELU_F16) v = gelu2(v);
+                            acc16[i][j][e] = v.x;
+                            acc16[i][j][e + 1] = v.y;
+                        }
+            };
+            // VAR 512 (fp16-image epilogues): each row-block pair's bias + GELU right before its
+            // slab pass, so that VALU work overlaps the previous pair's LDS and global stores
+            constexpr bool LATE = (VAR & 512) != 0 && EPI != EPI_BIAS_F32 && (VAR & 2) == 0;
+            if constexpr (!LATE) finish(0, 8);
             if constexpr ((VAR & 2) != 0) {      // diagnostic: no epilogue stores (acc kept alive)
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
@@ -1502,7 +1509,8 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 constexpr int NIMG = EPI == EPI_GELU_F16 ? 2 : 1;
                 // row-block pair outermost: its accumulators die after both images are out
 #pragma unroll
-                for (int i2 = 0; i2 < 4; ++i2)
+                for (int i2 = 0; i2 < 4; ++i2) {
+                    if constexpr (LATE) finish(2 * i2, 2 * i2 + 2);
 #pragma unroll
                     for (int img = 0; img < NIMG; ++img) {
 #pragma unroll
@@ -1525,6 +1533,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
 #pragma unroll
                         for (int it = 0; it < 4; ++it) st16<64>((uint4*)(ob + (size_t)(it * 8 + rr0) * ep.ldc), v[it]);
                     }
+                }
             }
             if (!more) break;
             par = last ^ 1;
@@ -1818,7 +1827,7 @@ hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_p
     // 16x16x32 MFMA (default; +4-7 % per shape over 32x32x16, tools/x3s_bench.py);
     // RS_X3S_MFMA=32 keeps the 32x32x16 form for A/B runs
     static const bool mf32 = getenv("RS_X3S_MFMA") && !strcmp(getenv("RS_X3S_MFMA"), "32");
-    constexpr int V = 262144 | 16 | 4 | 128, V32 = 262144 | 16 | 4;
+    constexpr int V = 262144 | 16 | 4 | 128 | 512, V32 = 262144 | 16 | 4;
     switch (epi) {
         case EPI_BIAS_F32:
             return mf32 ? launch_x3s<EPI_BIAS_F32, V32>(A, W, M_pad, N_pad, K, ep, st, ldw)
@@ -1911,6 +1920,7 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         else if (cfg == 32 && dbg == 20) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 2>(a, w, M, N, K, ep, st);
         else if (cfg == 32 && dbg == 21) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 256>(a, w, M, N, K, ep, st);
         else if (cfg == 32 && dbg == 19) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4>(a, w, M, N, K, ep, st);
+        else if (cfg == 31 && dbg == 22) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512>(a, w, M, N, K, ep, st);
         else if (cfg == 31 && dbg == 19) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4>(a, w, M, N, K, ep, st);
         else if (cfg == 30 && dbg == 19) e = launch_x3s<EPI_BIAS_F16, 262144 | 16 | 4>(a, w, M, N, K, ep, st);
         else if (cfg == 30 && dbg == 16) e = launch_x3s<EPI_BIAS_F16, 262144 | 16 | 4 | 128>(a, w, M, N, K, ep, st);

@@ -274,6 +274,13 @@ bool x3s_on(const rs_bert_cfg& cf) {
     const char* e = getenv("RS_X3S");
     return !(e && !strcmp(e, "0")) && cf.hidden % 256 == 0 && cf.intermediate % 256 == 0;
 }
+// RS_X3S_IMGRES (split-operand layers, default 1): the residual stream is held only as the
+// two-part image of the normalised hidden state (ln_res_img: 12 B per element per residual
+// block, no fp32 pre-LN stream or statistics); 0 = ln_res32 over the fp32 pre-LN stream.
+bool x3s_imgres_on() {
+    const char* e = getenv("RS_X3S_IMGRES");
+    return !(e && !strcmp(e, "0"));
+}
 
 // Runs the encoder + head over sequences [c.s0, c.s1) (one chunk).
 int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, const Chunk& c,
@@ -286,6 +293,7 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
     const bool dedup = c.urows > 0;           // layer-0 Q/K/V over unique rows (MLM, fp16, kx == 1)
     const bool x3s = kx == 3 && x3s_on(cf);   // split-operand GEMMs: full-row images are two-part
     const int kxf = x3s ? 2 : kx;             // width factor of the full-row operand images
+    const bool imgres = x3s && x3s_imgres_on();  // residual stream = the two-part image in h16
     float2* xst = m->xst.as<float2>();
     f16* h16 = m->h16.as<f16>();
     float* t32 = m->t32.as<float>();     // residual stream, pre-LN fp32 (LN rebuilt from xst)
@@ -297,7 +305,8 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
         // dedup: the per-copy pass keeps only the fp32 residual + LN statistics; the layer-0
         // GEMM operand is built over the chunk's unique rows (plan_unique_rows)
         HIPTRY(launch_embed_ln(d_tok, sm, c.s0, c.s1, 0, cf.mask_id, cf.vocab, m->word32, m->pos32,
-                               m->type32, m->eg, m->eb, cf.ln_eps, H, t32, xst, dedup ? nullptr : h16, kxf, st));
+                               m->type32, m->eg, m->eb, cf.ln_eps, H, imgres ? nullptr : t32, imgres ? nullptr : xst,
+                               dedup ? nullptr : h16, kxf, st));
         if (dedup)
             HIPTRY(launch_embed_unique(d_tok, sm, c.s0, c.s1, cf.mask_id, cf.vocab, m->word32, m->pos32,
                                        m->type32, m->eg, m->eb, cf.ln_eps, H, h16, kx, st));
@@ -375,7 +384,8 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
             if (int r = gx(RS_K_OPROJ, EPI_BIAS_F32, ctx, L.wo, 3 * H, rows, H, H, ep, H)) return r;
             {
                 ProfScope ps(m, st, RS_K_OTHER, 0);
-                HIPTRY(launch_ln_res32(t32, xst, xst, pg, pb, o32, rows, L.g1, L.be1, cf.ln_eps, H, h16, 2, st));
+                if (imgres) HIPTRY(launch_ln_res_img(h16, o32, rows, L.g1, L.be1, cf.ln_eps, H, st));
+                else HIPTRY(launch_ln_res32(t32, xst, xst, pg, pb, o32, rows, L.g1, L.be1, cf.ln_eps, H, h16, 2, st));
             }
             ep = EpiArgs{}; ep.bias = L.b1; ep.out = inter; ep.ldc = 2 * F; ep.kx = 2; ep.nlog = F;
             if (int r = gx(RS_K_FFN1, EPI_GELU_F16, h16, L.w1, 3 * H, rows, F, H, ep, F)) return r;
@@ -383,7 +393,8 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
             if (int r = gx(RS_K_FFN2, EPI_BIAS_F32, inter, L.w2, 3 * F, rows, H, F, ep, H)) return r;
             {
                 ProfScope ps(m, st, RS_K_OTHER, 0);
-                HIPTRY(launch_ln_res32(t32, xst, xst, L.g1, L.be1, o32, rows, L.g2, L.be2, cf.ln_eps, H, h16, 2, st));
+                if (imgres) HIPTRY(launch_ln_res_img(h16, o32, rows, L.g2, L.be2, cf.ln_eps, H, st));
+                else HIPTRY(launch_ln_res32(t32, xst, xst, L.g1, L.be1, o32, rows, L.g2, L.be2, cf.ln_eps, H, h16, 2, st));
             }
         } else if (!last) {
             {
@@ -447,7 +458,7 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
             {
                 ProfScope ps(m, st, RS_K_ATTN, 0);
                 HIPTRY(launch_attention_query(qkv, q32, t32, xst, pg, pb, sm, c.s0, c.s1, 0, H, nh, ctxq, resq, kx, st,
-                                              qdense));
+                                              qdense, imgres ? h16 : nullptr));
             }
             ep = EpiArgs{}; ep.bias = L.bo; ep.res = resq; ep.out = tq; ep.ldc = H;
             if (int r = gemm(m, st, RS_K_OPROJ, EPI_RES_F32, ctxq, L.wo, ns, H, kx * H, ep, H)) return r;
@@ -462,7 +473,7 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
     if (mode == MODE_EMB) {
         const Layer& L = m->layers[cf.layers - 1];
         ProfScope ps(m, st, RS_K_OTHER, 0);
-        HIPTRY(launch_embed_out(t32, xst, L.g2, L.be2, sm, c.s0, c.s1, 0, H, m->emb_dst, st));
+        HIPTRY(launch_embed_out(t32, xst, L.g2, L.be2, sm, c.s0, c.s1, 0, H, m->emb_dst, st, imgres ? h16 : nullptr));
         return RS_OK;
     }
     float* hq32 = m->hq32.as<float>();

@@ -69,7 +69,7 @@ def main():
             err32 = max(err32, ((out32[:2048] - ref).abs().max() / ref.abs().max()).item())
         gl = torch.nn.functional.gelu(ref)
         errg = 0.0
-        for d in (0, 16):
+        for d in (0, 16, 22):
             out_img.zero_()
             assert call(31, A2, W2, out_img, K, d) == 0
             torch.cuda.synchronize()
@@ -109,7 +109,7 @@ def main():
                     ("x3s-f32-mf16diag", 32, A2, W2, out32, K, 12), ("x3s-f32-mf16diag-neither", 32, A2, W2, out32, K, 13),
                     ("x3s-f32-prod-neither", 32, A2, W2, out32, K, 14),
                     ("x3s16-f32", 32, A2, W2, out32, K, 16), ("x3s16-f32-noilv", 32, A2, W2, out32, K, 17),
-                    ("x3s16-f32-neither", 32, A2, W2, out32, K, 18), ("x3s16-gelu2", 31, A2, W2, out_img, K, 16),
+                    ("x3s16-f32-neither", 32, A2, W2, out32, K, 18), ("x3s16-gelu2", 31, A2, W2, out_img, K, 16), ("x3s16-gelu2-late", 31, A2, W2, out_img, K, 22),
                     ("x3s16-f32-noepi", 32, A2, W2, out32, K, 20), ("x3s16-f32-direct", 32, A2, W2, out32, K, 21),
                     ("x3s-gelu2", 31, A2, W2, out_img, K, 0), ("kcat-persist-f16", 9, A3, W3, out16, 3 * K, 0)]
         if os.environ.get("VARIANTS"):
