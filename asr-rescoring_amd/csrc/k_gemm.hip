@@ -1191,6 +1191,12 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     };
     auto piece = [&](int buf, int k0, int p) {
         if constexpr ((VAR & 1) != 0) return;     // diagnostic: no K-loop staging (stale tiles)
+        if constexpr ((VAR & 1024) != 0) {        // diagnostic: the W half of the staging only
+            if (p < 4) return;
+        }
+        if constexpr ((VAR & 2048) != 0) {        // diagnostic: the A half of the staging only
+            if (p >= 4) return;
+        }
         const int r = p >> 1;
         if constexpr ((VAR & 16) != 0) {
             __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW,
@@ -1919,6 +1925,8 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         else if (cfg == 31 && dbg == 16) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128>(a, w, M, N, K, ep, st);
         else if (cfg == 32 && dbg == 20) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 2>(a, w, M, N, K, ep, st);
         else if (cfg == 32 && dbg == 21) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 256>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 23) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 2 | 1024>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 24) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 2 | 2048>(a, w, M, N, K, ep, st);
         else if (cfg == 32 && dbg == 19) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4>(a, w, M, N, K, ep, st);
         else if (cfg == 31 && dbg == 22) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512>(a, w, M, N, K, ep, st);
         else if (cfg == 31 && dbg == 19) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4>(a, w, M, N, K, ep, st);

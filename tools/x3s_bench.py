@@ -110,7 +110,8 @@ def main():
                     ("x3s-f32-prod-neither", 32, A2, W2, out32, K, 14),
                     ("x3s16-f32", 32, A2, W2, out32, K, 16), ("x3s16-f32-noilv", 32, A2, W2, out32, K, 17),
                     ("x3s16-f32-neither", 32, A2, W2, out32, K, 18), ("x3s16-gelu2", 31, A2, W2, out_img, K, 16), ("x3s16-gelu2-late", 31, A2, W2, out_img, K, 22),
-                    ("x3s16-f32-noepi", 32, A2, W2, out32, K, 20), ("x3s16-f32-direct", 32, A2, W2, out32, K, 21),
+                    ("x3s16-f32-noepi", 32, A2, W2, out32, K, 20), ("x3s16-f32-noepi-Wonly", 32, A2, W2, out32, K, 23),
+                    ("x3s16-f32-noepi-Aonly", 32, A2, W2, out32, K, 24), ("x3s16-f32-direct", 32, A2, W2, out32, K, 21),
                     ("x3s-gelu2", 31, A2, W2, out_img, K, 0), ("kcat-persist-f16", 9, A3, W3, out16, 3 * K, 0)]
         if os.environ.get("VARIANTS"):
             keep = os.environ["VARIANTS"].split(",")
