@@ -1199,12 +1199,15 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         }
         const int r = p >> 1;
         if constexpr ((VAR & 16) != 0) {
-            __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW,
-                                                     (__attribute__((address_space(3))) void*)(smem + buf * STAGE + r * REG +
-                                                                                                ((p & 1) * 8 + wave) * 1024),
-                                                     16, (r < 2 ? voffA : voffW)[2 * (p & 1) + (r & 1)], k0 * 2, 0, 0);
+            // VAR 4096 (diagnostic): 4-byte pieces — the same instruction count, a quarter of
+            // the bytes (separates the DMA's issue cost from its bandwidth)
+            auto* dst = (__attribute__((address_space(3))) void*)(smem + buf * STAGE + r * REG + ((p & 1) * 8 + wave) * 1024);
+            const int vo = (r < 2 ? voffA : voffW)[2 * (p & 1) + (r & 1)];
+            if constexpr ((VAR & 4096) != 0) __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 4, vo, k0 * 2, 0, 0);
+            else __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 16, vo, k0 * 2, 0, 0);
             return;
         }
+        if (k0 >= K) return;                      // (flat-address form: no past-the-panel dummy step)
         const f16* g = r < 2 ? srcA + (size_t)(p & 1) * 128 * ld2 + (r & 1) * K + k0
                              : srcW + (size_t)(p & 1) * 128 * ldw + (r & 1) * K + k0;
         __builtin_amdgcn_global_load_lds((const void*)g,
@@ -1281,7 +1284,13 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     const int offA16 = (wm * WTM + r16) * RB + ((q4 ^ g16(r16 >> 2)) << 4);
     const int offW16 = 2 * REG + (wn * WTN + r16) * RB + ((q4 ^ g16(r16 >> 2)) << 4);
     f32x4 acc16[8][4];
-    auto kstep16 = [&](int buf, int k0n /* next step's k0, < 0: no DMA here */) {
+    // VAR 4: the next step's eight DMA pieces ride this step's first MFMA groups; the last step
+    // of a tile passes k0n = 2^29 and issues none (a runtime test per piece).  VAR 8192 drops
+    // the test and stages that k0n anyway — past the panel descriptors' extent, which the
+    // buffer loads return as zeros without touching memory, into the buffer the next tile's
+    // stage 0 then overwrites (same wave, same rows, in order): one basic block per step, but
+    // measured 0-2 % slower (more live registers, spills outside the loop)
+    auto kstep16 = [&](int buf, int k0n) {
         const char* sb = smem + buf * STAGE;
         half8 wh[4], wl[4], wd[4];
 #pragma unroll
@@ -1314,10 +1323,12 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         acc16[4 * h + ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b, a, acc16[4 * h + ii][j], 0, 0, 0);
                     }
                     // the next step's eight DMA pieces, one per group of four MFMAs of half 0
-                    if (k0n >= 0 && h == 0 && 4 * pr + ii < 8) {
-                        __builtin_amdgcn_sched_barrier(0);
-                        piece(buf ^ 1, k0n, 4 * pr + ii);
-                        __builtin_amdgcn_sched_barrier(0);
+                    if constexpr ((VAR & 4) != 0) {
+                        if (h == 0 && 4 * pr + ii < 8 && ((VAR & 8192) != 0 || k0n < (1 << 29))) {
+                            __builtin_amdgcn_sched_barrier(0);
+                            piece(buf ^ 1, k0n, 4 * pr + ii);
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
                     }
                 }
             }
@@ -1358,7 +1369,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 const bool st_ok = kt + 1 < nk;
                 if ((VAR & 4) == 0 && st_ok) stage(cur ^ 1, (kt + 1) * BK);
                 __builtin_amdgcn_sched_barrier(0);
-                kstep16(cur, (VAR & 4) != 0 && st_ok ? (kt + 1) * BK : -1);
+                kstep16(cur, st_ok ? (kt + 1) * BK : (1 << 29));
                 __builtin_amdgcn_sched_barrier(0);
                 continue;
             }
@@ -1927,6 +1938,9 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         else if (cfg == 32 && dbg == 21) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 256>(a, w, M, N, K, ep, st);
         else if (cfg == 32 && dbg == 23) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 2 | 1024>(a, w, M, N, K, ep, st);
         else if (cfg == 32 && dbg == 24) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 2 | 2048>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 25) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 2 | 4096>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 26) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 8192>(a, w, M, N, K, ep, st);
+        else if (cfg == 31 && dbg == 26) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 8192>(a, w, M, N, K, ep, st);
         else if (cfg == 32 && dbg == 19) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4>(a, w, M, N, K, ep, st);
         else if (cfg == 31 && dbg == 22) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512>(a, w, M, N, K, ep, st);
         else if (cfg == 31 && dbg == 19) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4>(a, w, M, N, K, ep, st);

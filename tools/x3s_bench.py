@@ -62,7 +62,7 @@ def main():
         assert call(32, A2, W2, out32, K) == 0
         torch.cuda.synchronize()
         err32 = ((out32[:2048] - ref).abs().max() / ref.abs().max()).item()
-        for d in (5, 9, 10, 16, 17, 21):
+        for d in (0, 5, 9, 10, 16, 17, 21, 26):
             out32.zero_()
             assert call(32, A2, W2, out32, K, d) == 0
             torch.cuda.synchronize()
@@ -111,7 +111,10 @@ def main():
                     ("x3s16-f32", 32, A2, W2, out32, K, 16), ("x3s16-f32-noilv", 32, A2, W2, out32, K, 17),
                     ("x3s16-f32-neither", 32, A2, W2, out32, K, 18), ("x3s16-gelu2", 31, A2, W2, out_img, K, 16), ("x3s16-gelu2-late", 31, A2, W2, out_img, K, 22),
                     ("x3s16-f32-noepi", 32, A2, W2, out32, K, 20), ("x3s16-f32-noepi-Wonly", 32, A2, W2, out32, K, 23),
-                    ("x3s16-f32-noepi-Aonly", 32, A2, W2, out32, K, 24), ("x3s16-f32-direct", 32, A2, W2, out32, K, 21),
+                    ("x3s16-f32-noepi-Aonly", 32, A2, W2, out32, K, 24),
+                    ("x3s16-f32-noepi-dma4B", 32, A2, W2, out32, K, 25),
+                    ("x3s16-f32-branchfree", 32, A2, W2, out32, K, 26), ("x3s16-gelu2-branchfree", 31, A2, W2, out_img, K, 26),
+                    ("x3s-gelu2-prod", 31, A2, W2, out_img, K, 0), ("x3s16-f32-direct", 32, A2, W2, out32, K, 21),
                     ("x3s-gelu2", 31, A2, W2, out_img, K, 0), ("kcat-persist-f16", 9, A3, W3, out16, 3 * K, 0)]
         if os.environ.get("VARIANTS"):
             keep = os.environ["VARIANTS"].split(",")
