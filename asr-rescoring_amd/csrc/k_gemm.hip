@@ -1324,9 +1324,13 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                     }
                     // the next step's eight DMA pieces, one per group of four MFMAs of half 0
                     if constexpr ((VAR & 4) != 0) {
-                        if (h == 0 && 4 * pr + ii < 8 && ((VAR & 8192) != 0 || k0n < (1 << 29))) {
+                        // VAR 16384: the pieces spread over the whole step (every third group)
+                        constexpr bool SPREAD = (VAR & 16384) != 0;
+                        const int grp = 12 * h + 4 * pr + ii;
+                        const bool at = SPREAD ? grp % 3 == 0 : grp < 8;
+                        if (at && ((VAR & 8192) != 0 || k0n < (1 << 29))) {
                             __builtin_amdgcn_sched_barrier(0);
-                            piece(buf ^ 1, k0n, 4 * pr + ii);
+                            piece(buf ^ 1, k0n, SPREAD ? grp / 3 : grp);
                             __builtin_amdgcn_sched_barrier(0);
                         }
                     }
@@ -1941,6 +1945,10 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         else if (cfg == 32 && dbg == 25) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 2 | 4096>(a, w, M, N, K, ep, st);
         else if (cfg == 32 && dbg == 26) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 8192>(a, w, M, N, K, ep, st);
         else if (cfg == 31 && dbg == 26) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 8192>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 27) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 16384>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 28) e = launch_x3s<EPI_BIAS_F32, 16 | 4 | 128 | 512>(a, w, M, N, K, ep, st);
+        else if (cfg == 31 && dbg == 27) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 16384>(a, w, M, N, K, ep, st);
+        else if (cfg == 31 && dbg == 28) e = launch_x3s<EPI_GELU_F16, 16 | 4 | 128 | 512>(a, w, M, N, K, ep, st);
         else if (cfg == 32 && dbg == 19) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4>(a, w, M, N, K, ep, st);
         else if (cfg == 31 && dbg == 22) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512>(a, w, M, N, K, ep, st);
         else if (cfg == 31 && dbg == 19) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4>(a, w, M, N, K, ep, st);
