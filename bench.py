@@ -94,7 +94,9 @@ def main():
     # runs the 101-weight fusion sweep over the whole set.  The global set grows with the
     # rank count (weak scaling: per-rank work ~ utts utterances).
     from asr_rescoring_amd import shard
-    nb_all = D.synthetic_nbest(args.utts * world, args.nbest, seed=1)
+    # hard: hypotheses permuted and AM scores unsorted, so the fused argmax moves with the weight
+    # and the rerank check below is not the trivial AM-only case (same token counts)
+    nb_all = D.synthetic_nbest(args.utts * world, args.nbest, seed=1, hard=True)
     parts = shard.plan_shards(shard.utterance_costs(nb_all), world)
     u0, u1 = parts[rank]
     nb = nb_all.slice_utts(u0, u1)
@@ -208,7 +210,7 @@ def main():
     # Also a scoring-parity spot check at bench scale: the PLL of every sampled hypothesis
     # (reference work pattern, fp32 CPU) against the HIP lm of the timed steps.
     cpu = None
-    if rank == 0 and args.cpu_seconds > 0:
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:       # the contract: rank 0 at N = 1 only
         from oracle.bert_ref import TorchBert, set_cpu_threads
         import oracle.bert_ref as OB
         threads = set_cpu_threads()
@@ -233,7 +235,7 @@ def main():
 
     # ---- secondary leg: the reduced-precision fp16 mode on the same input (labelled) ------
     fp16 = None
-    if rank == 0 and args.precision != "fp16" and args.fp16_steps > 0:
+    if rank == 0 and world == 1 and args.precision != "fp16" and args.fp16_steps > 0:
         s16 = PLLScorer(weights, BERT_BASE, device=local, max_rows=args.max_rows, precision="fp16")
         lm16 = s16.score_nbest(d_tok, nb.hyp_off)
         torch.cuda.synchronize()
@@ -254,7 +256,7 @@ def main():
         rec = {"metric": "masked-token BERT forwards/sec (MLM_PLL, N=50, L~32)", "value": round(value, 2),
                "unit": "masked fwd/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": None, "dtype": DTYPE[args.precision], "data": "synthetic (PCG64 seed 1; random-init bert-base weights seed 1234)",
+               "vs_baseline": None, "dtype": DTYPE[args.precision], "data": "synthetic (PCG64 seed 1, permuted N-best with unsorted AM scores; random-init bert-base weights seed 1234)",
                "config": {"workload": "C3 MLM_PLL full PLL", "model": "bert-base-chinese shape (12L/768/12H/3072/V21128)",
                           "utts_per_rank": args.utts, "n_best": args.nbest, "utts_total": nb_all.n_utt,
                           "forwards_per_step": n_fwd_all, "forwards_rank0_step": n_fwd,
