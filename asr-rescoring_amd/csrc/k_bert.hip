@@ -751,6 +751,9 @@ attn16_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
 // (hi, scaled lo) with the same 80-half rows.  T <= 64 (one key block; the host routes longer
 // sequences to attn_full_kernel<float>).
 constexpr float LO_SCALE = 4096.f, LO_UNSCALE = 1.f / 4096.f;
+// DEDUP (MLM layer 0): Q, K, V rows come from the chunk's unique rows (row t of copy s is
+// unique row urow_m[s] at its masked position, urow_h[s] + t elsewhere), as attn16_kernel.
+template <bool DEDUP>
 __global__ void __launch_bounds__(64, 2)
 attn16x3_kernel(const float* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
                 f16* __restrict__ ctx, int kx) {
@@ -762,7 +765,14 @@ attn16x3_kernel(const float* __restrict__ qkv, SeqMeta sm, int s0, int row0, int
     const int T = sm.len[s], rs = sm.row[s] - row0;
     const int lane = threadIdx.x, r16 = lane & 15, g = lane >> 4;
     const int ld = 3 * H;
-    const float* base = qkv + (size_t)rs * ld + hd * 64;
+    const int ub = DEDUP ? sm.urow_h[s] : rs;
+    const int mp = DEDUP ? sm.mask_pos[s] : -1, um = DEDUP ? sm.urow_m[s] : 0;
+    const float* base = qkv + (size_t)ub * ld + hd * 64;
+    const float* mbase = qkv + (size_t)um * ld + hd * 64;
+    auto rowp = [&](int t) -> const float* {
+        if constexpr (DEDUP) return t == mp ? mbase : base + (size_t)t * ld;
+        else return base + (size_t)t * ld;
+    };
     const float scale = 0.125f;
     const int tr_off = (4 * g + ((lane & 15) >> 2)) * VR + 4 * (lane & 3);
     auto tr_read = [&](const f16* p) {
@@ -776,14 +786,14 @@ attn16x3_kernel(const float* __restrict__ qkv, SeqMeta sm, int s0, int row0, int
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
         const int kr = it * 4 + (lane >> 4), c4 = (lane & 15) * 4;
-        vraw[it] = kr < T ? *(const float4*)(base + (size_t)kr * ld + 2 * H + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        vraw[it] = kr < T ? *(const float4*)(rowp(kr) + 2 * H + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int kt = 0; kt < 4; ++kt)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
             const int key = kt * 16 + r16;
-            const float* kp = base + (size_t)key * ld + H + ks * 32 + g * 8;
+            const float* kp = rowp(key) + H + ks * 32 + g * 8;
             kraw[kt][ks][0] = key < T ? *(const float4*)kp : make_float4(0.f, 0.f, 0.f, 0.f);
             kraw[kt][ks][1] = key < T ? *(const float4*)(kp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
@@ -793,7 +803,7 @@ attn16x3_kernel(const float* __restrict__ qkv, SeqMeta sm, int s0, int row0, int
         const int t = q0 + r16;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-            const float* qp = base + (size_t)t * ld + ks * 32 + g * 8;
+            const float* qp = rowp(t) + ks * 32 + g * 8;
             qraw[ks][0] = t < T ? *(const float4*)qp : make_float4(0.f, 0.f, 0.f, 0.f);
             qraw[ks][1] = t < T ? *(const float4*)(qp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
@@ -1213,8 +1223,13 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
     const char* a16 = getenv("RS_ATTN16");
     // (T > 64 re-stages K/V per 16-query tile: slower than the 32-query tiles there)
     const bool use16 = !(a16 && !strcmp(a16, "0")) && !head_order && max_len > 0 && max_len <= 64;
-    if (dedup) {                                  // fp16 QKV, kx == 1 only (host gates it)
-        if (qkv32 || kx != 1 || H % 64) return hipErrorInvalidValue;
+    if (dedup && qkv32) {                         // fp16x3 split-operand layer 0 (T <= 64)
+        if (kx != 2 || H % 64 || max_len <= 0 || max_len > 64) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(attn16x3_kernel<true>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
+        return hipGetLastError();
+    }
+    if (dedup) {                                  // fp16 QKV, kx == 1 (host gates it)
+        if (kx != 1 || H % 64) return hipErrorInvalidValue;
         if (use16) {
             hipLaunchKernelGGL(attn16_kernel<true>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
             return hipGetLastError();
@@ -1233,7 +1248,7 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
     const char* a16x3 = getenv("RS_ATTN16X3");
     const bool use16x3 = !(a16x3 && !strcmp(a16x3, "0")) && max_len > 0 && max_len <= 64 && H % 64 == 0;
     if (qkv32 && use16x3)
-        hipLaunchKernelGGL(attn16x3_kernel, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
+        hipLaunchKernelGGL(attn16x3_kernel<false>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
     else if (qkv32)
         hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
     else if (kind == 0 && use16)
@@ -1329,7 +1344,7 @@ extern "C" int rs_debug_attention(int kind, const void* qkv, const int* len, con
     if (kind == 0)      // (sequence, head) grid
         hipLaunchKernelGGL(attn_tr_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1, 0);
     else if (kind == 8) // split-precision 16x16x32 attention over fp32 qkv [rows, 3H], ctx fp16 image [rows, 3H]
-        hipLaunchKernelGGL(attn16x3_kernel, grid, dim3(64), 0, st, (const float*)qkv, sm, 0, 0, H, (f16*)ctx, 3);
+        hipLaunchKernelGGL(attn16x3_kernel<false>, grid, dim3(64), 0, st, (const float*)qkv, sm, 0, 0, H, (f16*)ctx, 3);
     else if (kind == 9) // fp32 VALU attention (same I/O as kind 8)
         hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, 0, 0, H, (f16*)ctx, 3);
     else if (kind == 6) // 16x16x32 attention

@@ -290,7 +290,7 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
     const bool q32 = kx == 3;                 // fp16x3: QKV kept in fp32 for attention
     const int qkv_epi = q32 ? EPI_BIAS_F32 : EPI_BIAS_F16;
     const int rows = c.rows, ns = c.s1 - c.s0;
-    const bool dedup = c.urows > 0;           // layer-0 Q/K/V over unique rows (MLM, fp16, kx == 1)
+    const bool dedup = c.urows > 0;           // layer-0 Q/K/V over unique rows (MLM; fp16, or fp16x3 split)
     const bool x3s = kx == 3 && x3s_on(cf);   // split-operand GEMMs: full-row images are two-part
     const int kxf = x3s ? 2 : kx;             // width factor of the full-row operand images
     const bool imgres = x3s && x3s_imgres_on();  // residual stream = the two-part image in h16
@@ -304,12 +304,14 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
         ProfScope ps(m, st, RS_K_OTHER, 0);
         // dedup: the per-copy pass keeps only the fp32 residual + LN statistics; the layer-0
         // GEMM operand is built over the chunk's unique rows (plan_unique_rows)
+        // (split-operand dedup: every copy row's image stays in h16 — it is the layer-0
+        // residual — and the unique rows' image goes to the idle FFN buffer)
         HIPTRY(launch_embed_ln(d_tok, sm, c.s0, c.s1, 0, cf.mask_id, cf.vocab, m->word32, m->pos32,
                                m->type32, m->eg, m->eb, cf.ln_eps, H, imgres ? nullptr : t32, imgres ? nullptr : xst,
-                               dedup ? nullptr : h16, kxf, st));
+                               dedup && !x3s ? nullptr : h16, kxf, st));
         if (dedup)
             HIPTRY(launch_embed_unique(d_tok, sm, c.s0, c.s1, cf.mask_id, cf.vocab, m->word32, m->pos32,
-                                       m->type32, m->eg, m->eb, cf.ln_eps, H, h16, kx, st));
+                                       m->type32, m->eg, m->eb, cf.ln_eps, H, x3s ? inter : h16, kxf, st));
     }
     EpiArgs ep{};
     // split-operand GEMM over m_valid rows: A two-part image, W rows of ldw halfs; profiled as
@@ -369,7 +371,8 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
             } else if (int r = gemm(m, st, RS_K_QKV, qkv_epi, hq16g, L.wqkv, ns, H, kx * H, eq, H)) return r;
             qdense = m->tq32.p;
         } else if (x3s) {
-            if (int r = gx(RS_K_QKV, EPI_BIAS_F32, h16, L.wqkv, 3 * H, rows, 3 * H, H, ep, last ? 2 * H : 3 * H)) return r;
+            if (int r = gx(RS_K_QKV, EPI_BIAS_F32, uq ? inter : h16, L.wqkv, 3 * H, uq ? c.urows : rows, 3 * H, H, ep,
+                           last ? 2 * H : 3 * H)) return r;
         } else if (int r = gemm(m, st, RS_K_QKV, qkv_epi, h16, L.wqkv, uq ? c.urows : rows, 3 * H, kx * H, ep,
                                 last ? 2 * H : 3 * H)) return r;
         if (!last && x3s) {
@@ -377,7 +380,7 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
             // the residual blocks close in ln_res32 (x32 <- LN(x32) + o32, next two-part image)
             {
                 ProfScope ps(m, st, RS_K_ATTN, 0);
-                HIPTRY(launch_attention_full(qkv, true, sm, c.s0, c.s1, 0, H, nh, ctx, 2, st, false, c.max_len));
+                HIPTRY(launch_attention_full(qkv, true, sm, c.s0, c.s1, 0, H, nh, ctx, 2, st, uq, c.max_len));
             }
             float* o32 = (float*)qkv;
             ep = EpiArgs{}; ep.bias = L.bo; ep.out = o32; ep.ldc = H;
@@ -559,8 +562,12 @@ int run_all(rs_model* m, hipStream_t st, const int* d_tok, SeqList& sl, int mode
     // layer-0 dedup: MLM mode, fp16 operands, >= 2 layers (layer 0 is not the query-only layer)
     const char* dedup_s = getenv("RS_DEDUP");      // read per call (tests flip it)
     const int dedup_env = dedup_s ? atoi(dedup_s) : 1;
-    if (dedup_env && mode == MODE_MLM && m->kx == 1 && m->cfg.layers >= 2)
-        for (Chunk& c : chunks) c.urows = plan_unique_rows(sl, c.s0, c.s1);
+    // fp16x3: the split-operand layer with the image-held residual (its attention kernel reads
+    // the unique rows for chunks with T <= 64)
+    const bool x3_dedup = m->kx == 3 && x3s_on(m->cfg) && x3s_imgres_on();
+    if (dedup_env && mode == MODE_MLM && (m->kx == 1 || x3_dedup) && m->cfg.layers >= 2)
+        for (Chunk& c : chunks)
+            if (m->kx == 1 || c.max_len <= 64) c.urows = plan_unique_rows(sl, c.s0, c.s1);
 
     // one upload of all metadata through a pinned staging buffer
     const size_t n_extra = extra ? extra->size() : 0;
