@@ -129,8 +129,11 @@ int gemm_row_align();   // M padding granularity required by launch_gemm
 // LayerNorm output of one element from its row statistics: the single expression every
 // kernel uses, so an LN rebuilt downstream (EPI_RESLN_F32, attention_query) is bit-identical
 // to the one the LN kernel writes.
+// Every multiply-add of the LayerNorm is spelled out (fmaf / __fmul_rn): left to -ffp-contract,
+// the same source contracted differently in different kernels (embed_ln vs embed_unique), and
+// the rows two kernels must produce bit-identically (layer-0 dedup) differed in the last bit.
 __device__ __forceinline__ float ln_apply(float x, float2 st, float g, float b) {
-    return (x - st.x) * st.y * g + b;
+    return __builtin_fmaf(__fmul_rn(x - st.x, st.y), g, b);
 }
 
 // embed_ln writes the pre-LN embedding sum (x32), its row statistics and the fp16 operand

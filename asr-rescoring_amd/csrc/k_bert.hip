@@ -33,14 +33,14 @@ __device__ __forceinline__ void ln_store(const float4 (&x)[NV], const float* g, 
     float s = 0.f;
 #pragma unroll
     for (int v = 0; v < NV; ++v) s += (x[v].x + x[v].y) + (x[v].z + x[v].w);
-    const float mean = wave_sum(s) * (1.0f / H);
+    const float mean = __fmul_rn(wave_sum(s), 1.0f / H);
     float q = 0.f;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         const float4 d = make_float4(x[v].x - mean, x[v].y - mean, x[v].z - mean, x[v].w - mean);
-        q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+        q += __builtin_fmaf(d.x, d.x, __fmul_rn(d.y, d.y)) + __builtin_fmaf(d.z, d.z, __fmul_rn(d.w, d.w));
     }
-    const float2 st = make_float2(mean, 1.0f / sqrtf(wave_sum(q) * (1.0f / H) + eps));
+    const float2 st = make_float2(mean, 1.0f / sqrtf(__builtin_fmaf(wave_sum(q), 1.0f / H, eps)));
     if (stats && lane == 0) *stats = st;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
