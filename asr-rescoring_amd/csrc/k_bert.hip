@@ -17,6 +17,7 @@
 // [hi | hi/64 | lo*64]).  The residual stream stays PRE-LayerNorm in fp32 (x32) with per-row
 // (mean, rstd): its consumers (the next residual GEMM's accumulator init, attention_query)
 // rebuild LN(x) with ln_apply, so no LN kernel writes an fp32 copy of its output.
+#include <type_traits>
 #include "common.h"
 #include <stdlib.h>
 #include <string.h>
@@ -914,6 +915,173 @@ attn16x3_kernel(const float* __restrict__ qkv, SeqMeta sm, int s0, int row0, int
     }
 }
 
+// attn16x3_kernel re-laid for occupancy: V staged for R = 48 or 64 key rows only (R = 48 when
+// every sequence of the chunk has T <= 48: the 16 rows past it are zeros the second 32-key
+// block reads from registers), 128-B LDS rows without padding — the 16-B chunks XOR-swizzled
+// by (row & 6), which keeps the ds_read_b64_tr_b16 lane groups on distinct banks — and the
+// Vt fragments read from LDS per query tile instead of held in registers.  R = 48: 12 KiB of
+// LDS and <= 168 VGPRs, so 3 waves per SIMD instead of 2.
+template <bool DEDUP, int R>
+__global__ void __launch_bounds__(64, R == 48 ? 3 : 2)
+attn16x3v2_kernel(const float* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
+                  f16* __restrict__ ctx, int kx) {
+    typedef __fp16 fp16x4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
+    constexpr int KT = R / 16;                    // 16-key tiles staged
+    __shared__ __attribute__((aligned(16))) f16 sVh[R * 64];
+    __shared__ __attribute__((aligned(16))) f16 sVl[R * 64];
+    const int s = s0 + blockIdx.x, hd = blockIdx.y;
+    const int T = sm.len[s], rs = sm.row[s] - row0;
+    const int lane = threadIdx.x, r16 = lane & 15, g = lane >> 4;
+    const int ld = 3 * H;
+    const int ub = DEDUP ? sm.urow_h[s] : rs;
+    const int mp = DEDUP ? sm.mask_pos[s] : -1, um = DEDUP ? sm.urow_m[s] : 0;
+    const float* base = qkv + (size_t)ub * ld + hd * 64;
+    const float* mbase = qkv + (size_t)um * ld + hd * 64;
+    auto rowp = [&](int t) -> const float* {
+        if constexpr (DEDUP) return t == mp ? mbase : base + (size_t)t * ld;
+        else return base + (size_t)t * ld;
+    };
+    // V image address (halfs) of (row, col): 16-B chunk col / 8 swizzled by (row & 6)
+    auto vaddr = [](int row, int col) { return row * 64 + ((((col >> 3) ^ (row & 6))) << 3) + (col & 7); };
+    const float scale = 0.125f;
+    auto tr_read = [&](const f16* p) {
+        const fp16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) fp16x4*)p);
+        return __builtin_bit_cast(half4, v);
+    };
+    float4 vraw[R / 4], kraw[KT][2][2];
+#pragma unroll
+    for (int it = 0; it < R / 4; ++it) {
+        const int kr = it * 4 + (lane >> 4), c4 = (lane & 15) * 4;
+        vraw[it] = kr < T ? *(const float4*)(rowp(kr) + 2 * H + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const int key = kt * 16 + r16;
+            const float* kp = rowp(key) + H + ks * 32 + g * 8;
+            kraw[kt][ks][0] = key < T ? *(const float4*)kp : make_float4(0.f, 0.f, 0.f, 0.f);
+            kraw[kt][ks][1] = key < T ? *(const float4*)(kp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    float4 qraw[2][2];
+    auto load_q = [&](int q0) {
+        const int t = q0 + r16;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+            const float* qp = rowp(t) + ks * 32 + g * 8;
+            qraw[ks][0] = t < T ? *(const float4*)qp : make_float4(0.f, 0.f, 0.f, 0.f);
+            qraw[ks][1] = t < T ? *(const float4*)(qp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    load_q(0);
+    auto split_raw = [](const float4 (&r)[2], half8& hi, half8& lo) {
+        const float v[8] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+            hi[e] = (f16)v[e];
+            lo[e] = (f16)((v[e] - (float)hi[e]) * LO_SCALE);
+        }
+    };
+#pragma unroll
+    for (int it = 0; it < R / 4; ++it) {
+        const int kr = it * 4 + (lane >> 4), c4 = (lane & 15) * 4;
+        const float4 v = vraw[it];
+        const half4 h = {(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
+        const half4 l = {(f16)((v.x - (float)h[0]) * LO_SCALE), (f16)((v.y - (float)h[1]) * LO_SCALE),
+                         (f16)((v.z - (float)h[2]) * LO_SCALE), (f16)((v.w - (float)h[3]) * LO_SCALE)};
+        const int a = vaddr(kr, c4);
+        *(half4*)(sVh + a) = h;
+        *(half4*)(sVl + a) = l;
+    }
+    half8 kfh[KT][2], kfl[KT][2];
+#pragma unroll
+    for (int kt = 0; kt < KT; ++kt)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) split_raw(kraw[kt][ks], kfh[kt][ks], kfl[kt][ks]);
+    __syncthreads();
+    // transposed-read role: lane supplies row 4g + (l & 15) / 4 of a 16-row group, columns
+    // 16 dt + 4 (l & 3); rows 16 and 32 further keep the same swizzle (row & 6)
+    const int trow = 4 * g + ((lane & 15) >> 2);
+    int tro[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) tro[dt] = vaddr(trow, 16 * dt + 4 * (lane & 3));
+    const int nkt = min(KT, (T + 15) >> 4), nm = (nkt + 1) >> 1;
+    for (int q0 = 0; q0 < T; q0 += 16) {
+        const int t = q0 + r16;
+        half8 qh[2], ql[2];
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) split_raw(qraw[ks], qh[ks], ql[ks]);
+        if (q0 + 16 < T) load_q(q0 + 16);
+        f32x4 x[4];
+        float bm = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < 4; ++kt) {
+            x[kt] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+            if (kt < KT && kt < nkt) {
+                f32x4 a = {}, al = {};
+#pragma unroll
+                for (int ks = 0; ks < 2; ++ks) {
+                    al = __builtin_amdgcn_mfma_f32_16x16x32_f16(kfl[kt < KT ? kt : 0][ks], qh[ks], al, 0, 0, 0);
+                    al = __builtin_amdgcn_mfma_f32_16x16x32_f16(kfh[kt < KT ? kt : 0][ks], ql[ks], al, 0, 0, 0);
+                    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kfh[kt < KT ? kt : 0][ks], qh[ks], a, 0, 0, 0);
+                }
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const int key = kt * 16 + 4 * g + e;
+                    const float v = key < T ? __builtin_fmaf(al[e], LO_UNSCALE, a[e]) * scale : -INFINITY;
+                    x[kt][e] = v;
+                    bm = fmaxf(bm, v);
+                }
+            }
+        }
+        bm = fmaxf(bm, __shfl_xor(bm, 16));
+        bm = fmaxf(bm, __shfl_xor(bm, 32));
+        half8 ph[2], pl[2];
+        float ls = 0.f;
+#pragma unroll
+        for (int m2 = 0; m2 < 2; ++m2)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const float p = __expf(x[2 * m2 + (j >> 2)][j & 3] - bm);
+                ph[m2][j] = (f16)p;
+                pl[m2][j] = (f16)((p - (float)ph[m2][j]) * LO_SCALE);
+                ls += p;
+            }
+        ls += __shfl_xor(ls, 16);
+        ls += __shfl_xor(ls, 32);
+        f32x4 o[4];
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+            f32x4 oh = {}, ol = {};
+#pragma unroll
+            for (int m2 = 0; m2 < 2; ++m2)
+                if (m2 < nm) {
+                    const int ob = 32 * m2 * 64 + tro[dt];
+                    half4 lo = tr_read(sVh + ob), hi = (half4){};
+                    if (R == 64 || m2 == 0) hi = tr_read(sVh + ob + 16 * 64);
+                    const half8 vh = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    lo = tr_read(sVl + ob);
+                    hi = (half4){};
+                    if (R == 64 || m2 == 0) hi = tr_read(sVl + ob + 16 * 64);
+                    const half8 vl = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+                    ol = __builtin_amdgcn_mfma_f32_16x16x32_f16(vl, ph[m2], ol, 0, 0, 0);
+                    ol = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, pl[m2], ol, 0, 0, 0);
+                    oh = __builtin_amdgcn_mfma_f32_16x16x32_f16(vh, ph[m2], oh, 0, 0, 0);
+                }
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[dt][e] = __builtin_fmaf(ol[e], LO_UNSCALE, oh[e]);
+        }
+        if (t < T) {
+            const float il = 1.0f / ls;
+            f16* orow = ctx + (size_t)(rs + t) * kx * H;
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt)
+                put_split4(orow, hd * 64 + dt * 16 + 4 * g, H, kx,
+                           make_float4(o[dt][0] * il, o[dt][1] * il, o[dt][2] * il, o[dt][3] * il));
+        }
+    }
+}
+
 // Last layer: one wave per (sequence, head), only the scored query row.  Lanes over keys
 // for QK^T, lanes over the 64 head dims for P.V.
 template <class QT>
@@ -1223,9 +1391,20 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
     const char* a16 = getenv("RS_ATTN16");
     // (T > 64 re-stages K/V per 16-query tile: slower than the 32-query tiles there)
     const bool use16 = !(a16 && !strcmp(a16, "0")) && !head_order && max_len > 0 && max_len <= 64;
+    // RS_ATTN_V2 (default 1): attn16x3v2_kernel (R = 48 rows when max_len <= 48); 0 = attn16x3_kernel
+    const char* av2 = getenv("RS_ATTN_V2");
+    const bool v2 = !(av2 && !strcmp(av2, "0"));
+    auto x3v2 = [&](auto dd) {
+        constexpr bool D = decltype(dd)::value;
+        if (max_len <= 48)
+            hipLaunchKernelGGL((attn16x3v2_kernel<D, 48>), grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
+        else
+            hipLaunchKernelGGL((attn16x3v2_kernel<D, 64>), grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
+    };
     if (dedup && qkv32) {                         // fp16x3 split-operand layer 0 (T <= 64)
         if (kx != 2 || H % 64 || max_len <= 0 || max_len > 64) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(attn16x3_kernel<true>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
+        if (v2) x3v2(std::true_type{});
+        else hipLaunchKernelGGL(attn16x3_kernel<true>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
         return hipGetLastError();
     }
     if (dedup) {                                  // fp16 QKV, kx == 1 (host gates it)
@@ -1247,7 +1426,9 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
     // RS_ATTN16X3=0: fp32 VALU attention in the fp16x3 mode instead of the split-MFMA kernel
     const char* a16x3 = getenv("RS_ATTN16X3");
     const bool use16x3 = !(a16x3 && !strcmp(a16x3, "0")) && max_len > 0 && max_len <= 64 && H % 64 == 0;
-    if (qkv32 && use16x3)
+    if (qkv32 && use16x3 && v2)
+        x3v2(std::false_type{});
+    else if (qkv32 && use16x3)
         hipLaunchKernelGGL(attn16x3_kernel<false>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
     else if (qkv32)
         hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
@@ -1345,6 +1526,10 @@ extern "C" int rs_debug_attention(int kind, const void* qkv, const int* len, con
         hipLaunchKernelGGL(attn_tr_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1, 0);
     else if (kind == 8) // split-precision 16x16x32 attention over fp32 qkv [rows, 3H], ctx fp16 image [rows, 3H]
         hipLaunchKernelGGL(attn16x3_kernel<false>, grid, dim3(64), 0, st, (const float*)qkv, sm, 0, 0, H, (f16*)ctx, 3);
+    else if (kind == 10) // attn16x3v2_kernel, R = 48 (every T <= 48)
+        hipLaunchKernelGGL((attn16x3v2_kernel<false, 48>), grid, dim3(64), 0, st, (const float*)qkv, sm, 0, 0, H, (f16*)ctx, 3);
+    else if (kind == 11) // attn16x3v2_kernel, R = 64 (every T <= 64)
+        hipLaunchKernelGGL((attn16x3v2_kernel<false, 64>), grid, dim3(64), 0, st, (const float*)qkv, sm, 0, 0, H, (f16*)ctx, 3);
     else if (kind == 9) // fp32 VALU attention (same I/O as kind 8)
         hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, 0, 0, H, (f16*)ctx, 3);
     else if (kind == 6) // 16x16x32 attention

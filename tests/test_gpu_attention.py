@@ -73,14 +73,16 @@ def test_attention_kernels_agree():
     assert (a - b).abs().max().item() < 2e-3
 
 
-@pytest.mark.parametrize("kind", [8, 9])
-def test_split_precision_attention_vs_torch(kind):
+@pytest.mark.parametrize("kind,tmax", [(8, 64), (9, 64), (10, 48), (11, 64)])
+def test_split_precision_attention_vs_torch(kind, tmax):
     """fp16x3 mode: fp32 Q/K/V, ctx written as the [hi | hi/64 | lo*64] operand image.  kind 8 =
-    attn16x3_kernel (three fp16 MFMAs per product), kind 9 = fp32 VALU kernel; both at
-    fp32-level accuracy: |hi + lo - ref| <= 2e-6 on O(1) outputs.  T <= 64 (kind 8's range)."""
+    attn16x3_kernel (three fp16 MFMAs per product), 10 / 11 = attn16x3v2_kernel with 48 / 64
+    staged key rows (swizzled unpadded V image, Vt fragments read per query tile), 9 = fp32
+    VALU kernel; all at fp32-level accuracy: |hi + lo - ref| <= 2e-6 on O(1) outputs.
+    T <= tmax (the kernel's range)."""
     H, heads = 768, 12
     rng = np.random.default_rng(4)
-    T = np.array([t for t in LENGTHS if t <= 64] * 2, np.int32)
+    T = np.array([t for t in LENGTHS if t <= tmax] * 2, np.int32)
     rng.shuffle(T)
     row = np.concatenate([[0], np.cumsum(T)[:-1]]).astype(np.int32)
     dev = torch.device("cuda", 0)
