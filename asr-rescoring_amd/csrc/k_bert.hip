@@ -254,11 +254,12 @@ __device__ __forceinline__ void load8(const float* p, float (&o)[8]) {
 template <class QT>
 __global__ void __launch_bounds__(64)
 attn_full_kernel(const QT* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
-                 f16* __restrict__ ctx, int kx) {
+                 f16* __restrict__ ctx, int kx, int skip_le) {
     __shared__ __attribute__((aligned(16))) float sK[64][64];
     __shared__ __attribute__((aligned(16))) float sV[64][64];
     const int s = s0 + blockIdx.x, h = blockIdx.y;
     const int T = sm.len[s], rs = sm.row[s] - row0;
+    if (T <= skip_le) return;                     // (mixed chunks: the short ones run on MFMA)
     const int lane = threadIdx.x;
     const int ld = 3 * H;
     const QT* base = qkv + (size_t)rs * ld + h * 64;
@@ -931,6 +932,7 @@ attn16x3v2_kernel(const float* __restrict__ qkv, SeqMeta sm, int s0, int row0, i
     __shared__ __attribute__((aligned(16))) f16 sVl[R * 64];
     const int s = s0 + blockIdx.x, hd = blockIdx.y;
     const int T = sm.len[s], rs = sm.row[s] - row0;
+    if (T > R) return;                            // (mixed chunks: the long ones run on attn_full)
     const int lane = threadIdx.x, r16 = lane & 15, g = lane >> 4;
     const int ld = 3 * H;
     const int ub = DEDUP ? sm.urow_h[s] : rs;
@@ -1430,12 +1432,17 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
         x3v2(std::false_type{});
     else if (qkv32 && use16x3)
         hipLaunchKernelGGL(attn16x3_kernel<false>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
-    else if (qkv32)
-        hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
+    else if (qkv32 && v2 && !(a16x3 && !strcmp(a16x3, "0")) && H % 64 == 0) {
+        // a chunk with some T > 64: its T <= 64 sequences on the split-MFMA kernel, the longer
+        // ones (online softmax over 64-key blocks) on the fp32 VALU kernel; each skips the other's
+        hipLaunchKernelGGL((attn16x3v2_kernel<false, 64>), grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
+        hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx, 64);
+    } else if (qkv32)
+        hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx, 0);
     else if (kind == 0 && use16)
         hipLaunchKernelGGL(attn16_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
     else if (kind == 2)
-        hipLaunchKernelGGL(attn_full_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
+        hipLaunchKernelGGL(attn_full_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx, 0);
     else if (kind == 1)
         hipLaunchKernelGGL(attn_mfma_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
     else
@@ -1531,7 +1538,7 @@ extern "C" int rs_debug_attention(int kind, const void* qkv, const int* len, con
     else if (kind == 11) // attn16x3v2_kernel, R = 64 (every T <= 64)
         hipLaunchKernelGGL((attn16x3v2_kernel<false, 64>), grid, dim3(64), 0, st, (const float*)qkv, sm, 0, 0, H, (f16*)ctx, 3);
     else if (kind == 9) // fp32 VALU attention (same I/O as kind 8)
-        hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, 0, 0, H, (f16*)ctx, 3);
+        hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, 0, 0, H, (f16*)ctx, 3, 0);
     else if (kind == 6) // 16x16x32 attention
         hipLaunchKernelGGL(attn16_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
     else if (kind == 5) // head-fastest 1-D grid
@@ -1539,7 +1546,7 @@ extern "C" int rs_debug_attention(int kind, const void* qkv, const int* len, con
     else if (kind == 1)
         hipLaunchKernelGGL(attn_mfma_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
     else if (kind == 2)
-        hipLaunchKernelGGL(attn_full_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
+        hipLaunchKernelGGL(attn_full_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1, 0);
     else if (kind == 3)
         hipLaunchKernelGGL(attn_memskel_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, H, (f16*)ctx, 1);
     else   // kind 4: memory skeleton, 4 heads per 256-thread block
