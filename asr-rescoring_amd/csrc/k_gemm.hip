@@ -1219,6 +1219,17 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
 #pragma unroll
         for (int p = 0; p < 8; ++p) piece(buf, k0, p);
     };
+    // VAR 32768 (with 16): piece p of this wave (partner 0) or of wave + 4 (partner 1): the K
+    // loop's staging is issued by the older wave half alone, so the younger wave of each SIMD
+    // (at s_setprio 1) keeps the MFMA pipe busy while its partner pays the DMA issue cost
+    auto piece2 = [&](int buf, int k0, int p, int partner) {
+        const int r = p >> 1;
+        auto* dst = (__attribute__((address_space(3))) void*)(smem + buf * STAGE + r * REG +
+                                                               ((p & 1) * 8 + wave + 4 * partner) * 1024);
+        const int vo = (r < 2 ? voffA : voffW)[2 * (p & 1) + (r & 1)] +
+                       partner * (r < 2 ? 128 * (int)ld2 : 128 * ldw);     // rows + 64
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 16, vo, k0 * 2, 0, 0);
+    };
     // fragment addresses: row R, logical chunk 2s + fh -> position (fh ^ ((R >> 2) & 3)) ^ 2s;
     // rows 32 apart share the swizzle, so fragment / region offsets are immediates
     const int offA = (wm * WTM + frow) * RB + ((fh ^ (((wm * WTM + frow) >> 2) & 3)) << 4);
@@ -1323,7 +1334,14 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         acc16[4 * h + ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b, a, acc16[4 * h + ii][j], 0, 0, 0);
                     }
                     // the next step's eight DMA pieces, one per group of four MFMAs of half 0
-                    if constexpr ((VAR & 4) != 0) {
+                    if constexpr ((VAR & 32768) != 0) {
+                        const int grp = 12 * h + 4 * pr + ii;
+                        if (wave < 4 && grp < 16 && k0n < (1 << 29)) {
+                            __builtin_amdgcn_sched_barrier(0);
+                            piece2(buf ^ 1, k0n, grp & 7, grp >> 3);
+                            __builtin_amdgcn_sched_barrier(0);
+                        }
+                    } else if constexpr ((VAR & 4) != 0) {
                         // VAR 16384: the pieces spread over the whole step (every third group)
                         constexpr bool SPREAD = (VAR & 16384) != 0;
                         const int grp = 12 * h + 4 * pr + ii;
@@ -1371,7 +1389,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             asm volatile("s_barrier" ::: "memory");
             if constexpr (M16) {
                 const bool st_ok = kt + 1 < nk;
-                if ((VAR & 4) == 0 && st_ok) stage(cur ^ 1, (kt + 1) * BK);
+                if ((VAR & 4) == 0 && (VAR & 32768) == 0 && st_ok) stage(cur ^ 1, (kt + 1) * BK);
                 __builtin_amdgcn_sched_barrier(0);
                 kstep16(cur, st_ok ? (kt + 1) * BK : (1 << 29));
                 __builtin_amdgcn_sched_barrier(0);
@@ -1949,6 +1967,8 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         else if (cfg == 32 && dbg == 28) e = launch_x3s<EPI_BIAS_F32, 16 | 4 | 128 | 512>(a, w, M, N, K, ep, st);
         else if (cfg == 31 && dbg == 27) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 16384>(a, w, M, N, K, ep, st);
         else if (cfg == 31 && dbg == 28) e = launch_x3s<EPI_GELU_F16, 16 | 4 | 128 | 512>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 29) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 128 | 512 | 32768>(a, w, M, N, K, ep, st);
+        else if (cfg == 31 && dbg == 29) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 128 | 512 | 32768>(a, w, M, N, K, ep, st);
         else if (cfg == 32 && dbg == 19) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4>(a, w, M, N, K, ep, st);
         else if (cfg == 31 && dbg == 22) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512>(a, w, M, N, K, ep, st);
         else if (cfg == 31 && dbg == 19) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4>(a, w, M, N, K, ep, st);

@@ -62,14 +62,14 @@ def main():
         assert call(32, A2, W2, out32, K) == 0
         torch.cuda.synchronize()
         err32 = ((out32[:2048] - ref).abs().max() / ref.abs().max()).item()
-        for d in (0, 5, 9, 10, 16, 17, 21, 26, 27, 28):
+        for d in (0, 5, 9, 10, 16, 17, 21, 26, 27, 28, 29):
             out32.zero_()
             assert call(32, A2, W2, out32, K, d) == 0
             torch.cuda.synchronize()
             err32 = max(err32, ((out32[:2048] - ref).abs().max() / ref.abs().max()).item())
         gl = torch.nn.functional.gelu(ref)
         errg = 0.0
-        for d in (0, 16, 22, 27, 28):
+        for d in (0, 16, 22, 27, 28, 29):
             out_img.zero_()
             assert call(31, A2, W2, out_img, K, d) == 0
             torch.cuda.synchronize()
@@ -116,7 +116,8 @@ def main():
                     ("x3s16-f32-branchfree", 32, A2, W2, out32, K, 26), ("x3s16-gelu2-branchfree", 31, A2, W2, out_img, K, 26),
                     ("x3s-gelu2-prod", 31, A2, W2, out_img, K, 0),
                     ("x3s16-f32-spread", 32, A2, W2, out32, K, 27), ("x3s16-f32-noprio", 32, A2, W2, out32, K, 28),
-                    ("x3s16-gelu2-spread", 31, A2, W2, out_img, K, 27), ("x3s16-gelu2-noprio", 31, A2, W2, out_img, K, 28), ("x3s16-f32-direct", 32, A2, W2, out32, K, 21),
+                    ("x3s16-gelu2-spread", 31, A2, W2, out_img, K, 27),
+                    ("x3s16-f32-olddma", 32, A2, W2, out32, K, 29), ("x3s16-gelu2-olddma", 31, A2, W2, out_img, K, 29), ("x3s16-gelu2-noprio", 31, A2, W2, out_img, K, 28), ("x3s16-f32-direct", 32, A2, W2, out32, K, 21),
                     ("x3s-gelu2", 31, A2, W2, out_img, K, 0), ("kcat-persist-f16", 9, A3, W3, out16, 3 * K, 0)]
         if os.environ.get("VARIANTS"):
             keep = os.environ["VARIANTS"].split(",")
