@@ -43,3 +43,10 @@ hipError_t tr_loss(const float* sc, const float* tgt, const float* am, const flo
 hipError_t tr_ce(float* logits, const int* labels, int M, int V, float* row_loss, float* loss, hipStream_t s);
 hipError_t tr_adamw(float* p, const float* g, float* m, float* v, long long n, float decay, float b1w, float b2,
                     float b2w, float step_size, float bc2_sqrt, float eps, hipStream_t s);
+// fp32 GEMM on the f32-input MFMA (k_sgemm.hip): C[M][N] = A·B (+ C when accum), A read as
+// [M][lda] with k contiguous (a_kc) or [K][lda] with rows contiguous, B as [N][ldb] (b_kc)
+// or [K][ldb].  Few output tiles are split over K through ws (tr_sgemm_ws_floats floats),
+// summed in split order: deterministic.
+size_t tr_sgemm_ws_floats(int M, int N, int K);
+hipError_t tr_sgemm(int M, int N, int K, const float* A, int lda, bool a_kc, const float* B, int ldb, bool b_kc,
+                    float* C, int ldc, int accum, float* ws, size_t ws_floats, hipStream_t s);

@@ -6,14 +6,17 @@
 // the backward through the head, the encoder layers and the embeddings, then one
 // torch.optim.AdamW update.  Parameters, gradients and Adam moments are single flat fp32
 // buffers (one AdamW launch); the fused Q|K|V weight is the contiguous [q; k; v] range of
-// the three HF tensors.  GEMMs: rocBLAS sgemm (fp32, atomics disabled: deterministic);
-// all other ops: k_train.hip.  Dropout is not applied (p = 0).
+// the three HF tensors.  GEMMs: tr_sgemm (k_sgemm.hip: f32-input MFMA, exact fp32, split-K
+// through an ordered workspace sum — deterministic); RS_TRAIN_ROCBLAS=1 routes them to rocBLAS
+// sgemm instead (atomics disabled), kept as the timing / numerics baseline.
+// All other ops: k_train.hip.  Dropout is not applied (p = 0).
 #include <algorithm>
 #include <map>
 #include <string>
 #include <vector>
 #include <cstring>
 #include <cmath>
+#include <cstdlib>
 
 #include <rocblas/rocblas.h>
 
@@ -67,6 +70,7 @@ struct rs_trainer {
     int device = 0;
     bool finalized = false;
     rocblas_handle blas = nullptr;
+    bool use_rocblas = false;                                 // RS_TRAIN_ROCBLAS=1 (baseline)
     std::map<std::string, std::pair<size_t, size_t>> table;   // HF key -> (offset, numel) in floats
     std::vector<float> host;                                  // staged parameters until finalize
     std::vector<char> set;                                    // per table entry: provided?
@@ -75,7 +79,7 @@ struct rs_trainer {
     size_t o_wt = 0, o_bt = 0, o_tg = 0, o_tb = 0, o_db = 0;   // MLM head (decoder tied to o_word)
     std::vector<TLayer> lay;
     Buf P, G, M1, V1;       // parameters, gradients, Adam moments
-    Buf act, grad, meta, small;
+    Buf act, grad, meta, small, ws;   // ws: split-K partials of tr_sgemm
     long long step = 0;
     std::vector<int> h_tok, h_meta;
 };
@@ -89,20 +93,71 @@ size_t add_tensor(rs_trainer* t, const std::string& key, size_t n) {
     return off;
 }
 
-// row-major Y[M, N] = X[M, K] . W[N, K]^T (+ beta Y)
-rocblas_status gemm_nt(rocblas_handle h, int M, int N, int K, const float* X, const float* W, float* Y, float beta) {
+// rocBLAS baseline (RS_TRAIN_ROCBLAS=1): the same three forms, column-major arguments
+rocblas_status blas_nt(rocblas_handle h, int M, int N, int K, const float* X, const float* W, float* Y, float beta) {
     const float one = 1.0f;
     return rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, N, M, K, &one, W, K, X, K, &beta, Y, N);
 }
-// row-major dX[M, K] = dY[M, N] . W[N, K] (+ beta dX)
-rocblas_status gemm_nn(rocblas_handle h, int M, int N, int K, const float* dY, const float* W, float* dX, float beta) {
+rocblas_status blas_nn(rocblas_handle h, int M, int N, int K, const float* dY, const float* W, float* dX, float beta) {
     const float one = 1.0f;
     return rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_none, K, M, N, &one, W, K, dY, N, &beta, dX, K);
 }
-// row-major dW[N, K] = dY[M, N]^T . X[M, K]
-rocblas_status gemm_tn(rocblas_handle h, int M, int N, int K, const float* dY, const float* X, float* dW, float beta) {
+rocblas_status blas_tn(rocblas_handle h, int M, int N, int K, const float* dY, const float* X, float* dW, float beta) {
     const float one = 1.0f;
     return rocblas_sgemm(h, rocblas_operation_none, rocblas_operation_transpose, K, N, M, &one, X, K, dY, N, &beta, dW, K);
+}
+
+#define TRY_SG(expr)                                                                        \
+    do {                                                                                    \
+        hipError_t e_ = (expr);                                                             \
+        if (e_ != hipSuccess) return rs_fail(RS_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define RS_TRY(expr)                     \
+    do {                                 \
+        if (int r_ = (expr)) return r_;  \
+    } while (0)
+
+// row-major Y[M, N] = X[M, K] . W[N, K]^T (+ beta Y)
+int gemm_nt(rs_trainer* t, hipStream_t st, int M, int N, int K, const float* X, const float* W, float* Y, float beta) {
+    if (t->use_rocblas) {
+        TRY_BLAS(blas_nt(t->blas, M, N, K, X, W, Y, beta));
+        return RS_OK;
+    }
+    TRY_SG(tr_sgemm(M, N, K, X, K, true, W, K, true, Y, N, beta != 0.f, t->ws.f(), t->ws.bytes / 4, st));
+    return RS_OK;
+}
+// row-major dX[M, K] = dY[M, N] . W[N, K] (+ beta dX)
+int gemm_nn(rs_trainer* t, hipStream_t st, int M, int N, int K, const float* dY, const float* W, float* dX, float beta) {
+    if (t->use_rocblas) {
+        TRY_BLAS(blas_nn(t->blas, M, N, K, dY, W, dX, beta));
+        return RS_OK;
+    }
+    TRY_SG(tr_sgemm(M, K, N, dY, N, true, W, K, false, dX, K, beta != 0.f, t->ws.f(), t->ws.bytes / 4, st));
+    return RS_OK;
+}
+// row-major dW[N, K] = dY[M, N]^T . X[M, K] (+ beta dW)
+int gemm_tn(rs_trainer* t, hipStream_t st, int M, int N, int K, const float* dY, const float* X, float* dW, float beta) {
+    if (t->use_rocblas) {
+        TRY_BLAS(blas_tn(t->blas, M, N, K, dY, X, dW, beta));
+        return RS_OK;
+    }
+    TRY_SG(tr_sgemm(N, K, M, dY, N, false, X, K, false, dW, K, beta != 0.f, t->ws.f(), t->ws.bytes / 4, st));
+    return RS_OK;
+}
+
+// split-K workspace for every GEMM shape of a step over M token rows (forward, dgrad, wgrad of
+// each Linear; the MLM head's transform and tied decoder)
+size_t sgemm_ws_floats(const rs_bert_cfg& c, int M) {
+    const int H = c.hidden, F = c.intermediate, V = c.heads_mask == RS_HEAD_MLM ? c.vocab : H;
+    size_t w = 0;
+    for (int n : {3 * H, H, F, V})
+        for (int k : {H, F}) {
+            w = std::max(w, tr_sgemm_ws_floats(M, n, k));   // forward (M, n, k)
+            w = std::max(w, tr_sgemm_ws_floats(M, k, n));   // dgrad   (M, k, n)
+            w = std::max(w, tr_sgemm_ws_floats(n, k, M));   // wgrad   (n, k, M)
+        }
+    return w;
 }
 
 }  // namespace
@@ -209,6 +264,10 @@ int rs_trainer_finalize(rs_trainer* t) {
     TRY_HIP(hipMemset(t->V1.p, 0, bytes));
     TRY_BLAS(rocblas_create_handle(&t->blas));
     TRY_BLAS(rocblas_set_atomics_mode(t->blas, rocblas_atomics_not_allowed));
+    {
+        const char* v = getenv("RS_TRAIN_ROCBLAS");
+        t->use_rocblas = v && v[0] == '1';
+    }
     t->host.clear();
     t->host.shrink_to_fit();
     t->finalized = true;
@@ -351,6 +410,7 @@ int prepare(StepCtx& c, const int32_t* d_tok, const int32_t* h_off, int n_seq, c
     const size_t n_part = al(tr_colsum_scratch(M, widest) / 4);
     const size_t n_grad = 2 * MH + QKV + MF + n_part + 2 * (size_t)S + aux.size() + M + 64;
     TRY_HIP(t->grad.ensure(n_grad * 4));
+    TRY_HIP(t->ws.ensure(std::max<size_t>(sgemm_ws_floats(cf, M), 64) * 4));
     float* A = t->act.f();
     c.x0 = A;
     c.st0 = (float2*)(c.x0 + MH);
@@ -394,22 +454,21 @@ int encoder_forward(StepCtx& c) {
     const rs_bert_cfg& cf = t->cfg;
     const int H = cf.hidden, F = cf.intermediate, nh = cf.heads, M = c.M;
     float* Pm = t->P.f();
-    rocblas_handle bh = t->blas;
     hipStream_t st = c.st;
     TRY_HIP(tr_embed_ln(c.dm + c.i_tok, c.dm + c.i_pos, M, cf.vocab, Pm + t->o_word, Pm + t->o_pos, Pm + t->o_type,
                         Pm + t->o_eg, Pm + t->o_eb, cf.ln_eps, H, c.x0, c.st0, c.la[0].hin, st));
     for (int l = 0; l < cf.layers; ++l) {
         const TLayer& L = t->lay[l];
         StepCtx::LA& a = c.la[l];
-        TRY_BLAS(gemm_nt(bh, M, 3 * H, H, a.hin, Pm + L.wqkv, a.qkv, 0.f));
+        RS_TRY(gemm_nt(t, st, M, 3 * H, H, a.hin, Pm + L.wqkv, a.qkv, 0.f));
         TRY_HIP(tr_bias(a.qkv, Pm + L.bqkv, M, 3 * H, st));
         TRY_HIP(tr_attn_fwd(a.qkv, c.seq, c.i_klen ? c.dm + c.i_klen : nullptr, c.pofs, c.S, c.tmax, H, nh, a.P,
                             a.ctx, st));
-        TRY_BLAS(gemm_nt(bh, M, H, H, a.ctx, Pm + L.wo, a.x1, 0.f));
+        RS_TRY(gemm_nt(t, st, M, H, H, a.ctx, Pm + L.wo, a.x1, 0.f));
         TRY_HIP(tr_bias_res_ln(a.x1, Pm + L.bo, a.hin, M, Pm + L.g1, Pm + L.be1, cf.ln_eps, H, a.st1, a.h1, st));
-        TRY_BLAS(gemm_nt(bh, M, F, H, a.h1, Pm + L.w1, a.pre, 0.f));
+        RS_TRY(gemm_nt(t, st, M, F, H, a.h1, Pm + L.w1, a.pre, 0.f));
         TRY_HIP(tr_bias_gelu(a.pre, Pm + L.b1, a.act, M, F, st));
-        TRY_BLAS(gemm_nt(bh, M, H, F, a.act, Pm + L.w2, a.x2, 0.f));
+        RS_TRY(gemm_nt(t, st, M, H, F, a.act, Pm + L.w2, a.x2, 0.f));
         TRY_HIP(tr_bias_res_ln(a.x2, Pm + L.b2, a.h1, M, Pm + L.g2, Pm + L.be2, cf.ln_eps, H, a.st2,
                                c.la[l + 1].hin, st));
     }
@@ -425,7 +484,6 @@ int encoder_backward(StepCtx& c) {
     const size_t MH = (size_t)M * H, MF = (size_t)M * F;
     float *Pm = t->P.f(), *Gm = t->G.f();
     float *dA = c.dA, *dB = c.dB, *dF = c.dF, *dQKV = c.dQKV, *part = c.part;
-    rocblas_handle bh = t->blas;
     hipStream_t st = c.st;
     for (int l = cf.layers - 1; l >= 0; --l) {
         const TLayer& L = t->lay[l];
@@ -434,24 +492,24 @@ int encoder_backward(StepCtx& c) {
         TRY_HIP(tr_colsum(dA, nullptr, nullptr, M, H, 0, part, Gm + L.be2, 0, st));
         TRY_HIP(tr_ln_bwd(dA, a.x2, a.st2, Pm + L.g2, dB, M, H, st));              // dB = dx2
         TRY_HIP(tr_colsum(dB, nullptr, nullptr, M, H, 0, part, Gm + L.b2, 0, st));
-        TRY_BLAS(gemm_tn(bh, M, H, F, dB, a.act, Gm + L.w2, 0.f));
-        TRY_BLAS(gemm_nn(bh, M, H, F, dB, Pm + L.w2, dF, 0.f));                    // d act
+        RS_TRY(gemm_tn(t, st, M, H, F, dB, a.act, Gm + L.w2, 0.f));
+        RS_TRY(gemm_nn(t, st, M, H, F, dB, Pm + L.w2, dF, 0.f));                    // d act
         TRY_HIP(tr_gelu_bwd(dF, a.pre, (long long)MF, st));                         // d pre
         TRY_HIP(tr_colsum(dF, nullptr, nullptr, M, F, 0, part, Gm + L.b1, 0, st));
-        TRY_BLAS(gemm_tn(bh, M, F, H, dF, a.h1, Gm + L.w1, 0.f));
+        RS_TRY(gemm_tn(t, st, M, F, H, dF, a.h1, Gm + L.w1, 0.f));
         TRY_HIP(hipMemcpyAsync(dA, dB, MH * 4, hipMemcpyDeviceToDevice, st));      // residual
-        TRY_BLAS(gemm_nn(bh, M, F, H, dF, Pm + L.w1, dA, 1.f));                     // dA = d h1
+        RS_TRY(gemm_nn(t, st, M, F, H, dF, Pm + L.w1, dA, 1.f));                     // dA = d h1
         TRY_HIP(tr_colsum(dA, a.x1, a.st1, M, H, 1, part, Gm + L.g1, 0, st));
         TRY_HIP(tr_colsum(dA, nullptr, nullptr, M, H, 0, part, Gm + L.be1, 0, st));
         TRY_HIP(tr_ln_bwd(dA, a.x1, a.st1, Pm + L.g1, dB, M, H, st));              // dB = dx1
         TRY_HIP(tr_colsum(dB, nullptr, nullptr, M, H, 0, part, Gm + L.bo, 0, st));
-        TRY_BLAS(gemm_tn(bh, M, H, H, dB, a.ctx, Gm + L.wo, 0.f));
-        TRY_BLAS(gemm_nn(bh, M, H, H, dB, Pm + L.wo, dA, 0.f));                     // dA = d ctx
+        RS_TRY(gemm_tn(t, st, M, H, H, dB, a.ctx, Gm + L.wo, 0.f));
+        RS_TRY(gemm_nn(t, st, M, H, H, dB, Pm + L.wo, dA, 0.f));                     // dA = d ctx
         TRY_HIP(tr_attn_bwd(a.qkv, a.P, dA, c.seq, c.pofs, c.S, c.tmax, H, nh, dQKV, st));
         TRY_HIP(tr_colsum(dQKV, nullptr, nullptr, M, 3 * H, 0, part, Gm + L.bqkv, 0, st));
-        TRY_BLAS(gemm_tn(bh, M, 3 * H, H, dQKV, a.hin, Gm + L.wqkv, 0.f));
+        RS_TRY(gemm_tn(t, st, M, 3 * H, H, dQKV, a.hin, Gm + L.wqkv, 0.f));
         TRY_HIP(hipMemcpyAsync(dA, dB, MH * 4, hipMemcpyDeviceToDevice, st));      // residual
-        TRY_BLAS(gemm_nn(bh, M, 3 * H, H, dQKV, Pm + L.wqkv, dA, 1.f));             // dA = d h_in
+        RS_TRY(gemm_nn(t, st, M, 3 * H, H, dQKV, Pm + L.wqkv, dA, 1.f));             // dA = d h_in
     }
     TRY_HIP(tr_colsum(dA, c.x0, c.st0, M, H, 1, part, Gm + t->o_eg, 0, st));
     TRY_HIP(tr_colsum(dA, nullptr, nullptr, M, H, 0, part, Gm + t->o_eb, 0, st));
@@ -536,14 +594,13 @@ int rs_train_step_mlm(rs_trainer* t, const int32_t* d_ids, const int32_t* h_seq_
     const rs_bert_cfg& cf = t->cfg;
     const int H = cf.hidden, V = cf.vocab, M = c.M;
     float *Pm = t->P.f(), *Gm = t->G.f();
-    rocblas_handle bh = t->blas;
     hipStream_t st = c.st;
     const float* hfin = c.la[cf.layers].hin;
     // BertOnlyMLMHead: transform (dense + GELU + LN), tied decoder + bias (modeling_bert.py:466-506)
-    TRY_BLAS(gemm_nt(bh, M, H, H, hfin, Pm + t->o_wt, c.tpre, 0.f));
+    RS_TRY(gemm_nt(t, st, M, H, H, hfin, Pm + t->o_wt, c.tpre, 0.f));
     TRY_HIP(tr_bias_gelu(c.tpre, Pm + t->o_bt, c.tx, M, H, st));
     TRY_HIP(tr_bias_res_ln(c.tx, nullptr, nullptr, M, Pm + t->o_tg, Pm + t->o_tb, cf.ln_eps, H, c.tst, c.th, st));
-    TRY_BLAS(gemm_nt(bh, M, V, H, c.th, Pm + t->o_word, c.logits, 0.f));
+    RS_TRY(gemm_nt(t, st, M, V, H, c.th, Pm + t->o_word, c.logits, 0.f));
     TRY_HIP(tr_bias(c.logits, Pm + t->o_db, M, V, st));
     float* rl = c.tail;
     TRY_HIP(tr_ce(c.logits, d_labels, M, V, rl, d_loss, st));       // logits <- dlogits
@@ -555,15 +612,15 @@ int rs_train_step_mlm(rs_trainer* t, const int32_t* d_ids, const int32_t* h_seq_
     float* dT = c.dB;
     float* dT2 = c.dF;
     TRY_HIP(tr_colsum(c.logits, nullptr, nullptr, M, V, 0, c.part, Gm + t->o_db, 0, st));
-    TRY_BLAS(gemm_tn(bh, M, V, H, c.logits, c.th, Gm + t->o_word, 0.f));          // tied decoder part
-    TRY_BLAS(gemm_nn(bh, M, V, H, c.logits, Pm + t->o_word, dT, 0.f));
+    RS_TRY(gemm_tn(t, st, M, V, H, c.logits, c.th, Gm + t->o_word, 0.f));          // tied decoder part
+    RS_TRY(gemm_nn(t, st, M, V, H, c.logits, Pm + t->o_word, dT, 0.f));
     TRY_HIP(tr_colsum(dT, c.tx, c.tst, M, H, 1, c.part, Gm + t->o_tg, 0, st));
     TRY_HIP(tr_colsum(dT, nullptr, nullptr, M, H, 0, c.part, Gm + t->o_tb, 0, st));
     TRY_HIP(tr_ln_bwd(dT, c.tx, c.tst, Pm + t->o_tg, dT2, M, H, st));
     TRY_HIP(tr_gelu_bwd(dT2, c.tpre, (long long)M * H, st));
     TRY_HIP(tr_colsum(dT2, nullptr, nullptr, M, H, 0, c.part, Gm + t->o_bt, 0, st));
-    TRY_BLAS(gemm_tn(bh, M, H, H, dT2, hfin, Gm + t->o_wt, 0.f));
-    TRY_BLAS(gemm_nn(bh, M, H, H, dT2, Pm + t->o_wt, c.dA, 0.f));                  // dA = d hidden
+    RS_TRY(gemm_tn(t, st, M, H, H, dT2, hfin, Gm + t->o_wt, 0.f));
+    RS_TRY(gemm_nn(t, st, M, H, H, dT2, Pm + t->o_wt, c.dA, 0.f));                  // dA = d hidden
     if (int r = encoder_backward(c)) return r;
     if (int r = adamw(t, o, st)) return r;
     TRY_HIP(hipStreamSynchronize(st));
@@ -586,7 +643,7 @@ void rs_trainer_destroy(rs_trainer* t) {
     (void)hipSetDevice(t->device);
     (void)hipDeviceSynchronize();
     if (t->blas) (void)rocblas_destroy_handle(t->blas);
-    for (Buf* b : {&t->P, &t->G, &t->M1, &t->V1, &t->act, &t->grad, &t->meta, &t->small}) b->release();
+    for (Buf* b : {&t->P, &t->G, &t->M1, &t->V1, &t->act, &t->grad, &t->meta, &t->small, &t->ws}) b->release();
     delete t;
 }
 
