@@ -22,6 +22,7 @@
 // sum over the splits closes it — no float atomics, so a training step stays bitwise
 // reproducible.
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 #include "train.h"
@@ -80,8 +81,9 @@ __device__ __forceinline__ void sg_store_lds(float* __restrict__ s, const float4
 
 // C[M][N] (+)= A·B over k in [z·kc, min(K, (z+1)·kc)) for split z = blockIdx.z.
 // ws == nullptr: C = acc (+ C when accum).  Otherwise the partial goes to ws[z][M][N].
-template <bool AKC, bool BKC>
-__global__ void __launch_bounds__(256)
+// OCC: minimum workgroups per CU the register allocation must allow (launch-bounds hint)
+template <bool AKC, bool BKC, int OCC>
+__global__ void __launch_bounds__(256, OCC)
 sgemm_f32_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb, float* __restrict__ C,
                  int ldc, int M, int N, int K, int kc, int accum, float* __restrict__ ws) {
     __shared__ float As[SG_BK * SG_LD];
@@ -210,13 +212,26 @@ hipError_t tr_sgemm(int M, int N, int K, const float* A, int lda, bool a_kc, con
         P = ws;
     }
     const dim3 grid((N + SG_BN - 1) / SG_BN, (M + SG_BM - 1) / SG_BM, splits);
-#define SG_LAUNCH(AK, BK_)                                                                                     \
-    hipLaunchKernelGGL((sgemm_f32_kernel<AK, BK_>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K, kc, \
+#define SG_LAUNCH(AK, BK_, O)                                                                                    \
+    hipLaunchKernelGGL((sgemm_f32_kernel<AK, BK_, O>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K, kc, \
                        accum, P)
-    if (a_kc && b_kc) SG_LAUNCH(true, true);
-    else if (a_kc) SG_LAUNCH(true, false);
-    else if (b_kc) SG_LAUNCH(false, true);
-    else SG_LAUNCH(false, false);
+#define SG_FORMS(O)                                  \
+    if (a_kc && b_kc) SG_LAUNCH(true, true, O);      \
+    else if (a_kc) SG_LAUNCH(true, false, O);        \
+    else if (b_kc) SG_LAUNCH(false, true, O);        \
+    else SG_LAUNCH(false, false, O);
+    static const int occ = [] {
+        const char* v = getenv("RS_SGEMM_OCC");
+        return v ? atoi(v) : 1;
+    }();
+    if (occ >= 4) {
+        SG_FORMS(4)
+    } else if (occ == 3) {
+        SG_FORMS(3)
+    } else {
+        SG_FORMS(1)
+    }
+#undef SG_FORMS
 #undef SG_LAUNCH
     hipError_t e = hipGetLastError();
     if (e != hipSuccess || splits == 1) return e;
