@@ -70,7 +70,7 @@ def build_library(verbose: bool = False) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
         objs = list(ex.map(_compile, srcs))
-    # rocBLAS: fp32 GEMMs of the trainer (its soname matches the copy torch loads first)
+    # rocBLAS: the trainer's RS_TRAIN_ROCBLAS=1 baseline GEMMs (its soname matches the copy torch loads first)
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + \
         ["-L/opt/rocm/lib", "-lrocblas", "-lpthread"]
     if _needs(LIB, objs, cmd):

@@ -113,16 +113,26 @@ sgemm_f32_kernel(const float* __restrict__ A, int lda, const float* __restrict__
             sg_load<AKC>(A, lda, m0, M, k0 + SG_BK, ke, ra);
             sg_load<BKC>(B, ldb, n0, N, k0 + SG_BK, ke, rb);
         }
-        // MFMA step kk, lane half h: k = 2 kk + h (the instruction's A[i][k = lane >> 5] map)
+        // MFMA step kk, lane half h: k = 2 kk + h (the instruction's A[i][k = lane >> 5] map).
+        // Fragments of step kk + 1 are read before step kk's MFMAs issue, so the LDS latency
+        // runs under the MFMA pipe (hipcc otherwise waits lgkmcnt(0) before every step).
+        const float* ap = As + h * SG_LD + wm + c;
+        const float* bp = Bs + h * SG_LD + wn + c;
+        float a0 = ap[0], a1 = ap[32], b0 = bp[0], b1 = bp[32];
 #pragma unroll
         for (int kk = 0; kk < SG_BK / 2; ++kk) {
-            const float* ap = As + (2 * kk + h) * SG_LD + wm + c;
-            const float* bp = Bs + (2 * kk + h) * SG_LD + wn + c;
-            const float a0 = ap[0], a1 = ap[32], b0 = bp[0], b1 = bp[32];
+            float na0 = 0.f, na1 = 0.f, nb0 = 0.f, nb1 = 0.f;
+            if (kk + 1 < SG_BK / 2) {
+                const int o = 2 * (kk + 1) * SG_LD;
+                na0 = ap[o]; na1 = ap[o + 32]; nb0 = bp[o]; nb1 = bp[o + 32];
+            }
+            __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of this step's MFMAs
             acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
             acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
             acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
             acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
+            a0 = na0; a1 = na1; b0 = nb0; b1 = nb1;
         }
         __syncthreads();
     }

@@ -1,7 +1,7 @@
 // Training kernels (RescoreBert distillation training, backward through
 // the BERT encoder).  fp32 throughout — the reference trains in fp32 — with every reduction
 // in a fixed order (no float atomics): a training step is bitwise reproducible.
-// GEMMs are plain (transposed) fp32 GEMMs and go to rocBLAS (train_api.hip); everything
+// GEMMs are plain (transposed) fp32 GEMMs on the f32-input MFMA (k_sgemm.hip); everything
 // else is here.  One wave per token row for row-wise ops; column reductions in two stages
 // (64-row partials, then an ordered sum).
 #include "common.h"
