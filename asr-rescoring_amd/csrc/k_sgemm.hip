@@ -184,8 +184,13 @@ int sg_splits(int M, int N, int K, int* kc) {
     const int tiles = ((M + SG_BM - 1) / SG_BM) * ((N + SG_BN - 1) / SG_BN);
     const int steps = (K + SG_BK - 1) / SG_BK;
     int splits = 1;
-    // up to ~512 workgroups (two per CU); each split costs a write + read of M·N partials
-    if (tiles < 512) splits = std::max(1, std::min(std::min((512 + tiles - 1) / tiles, steps / 4), 16));
+    // up to ~512 workgroups (two per CU); each split costs a write + read of M·N partials.
+    // RS_SGEMM_SPLIT_WG overrides the workgroup target (A/B knob).
+    static const int target = [] {
+        const char* v = getenv("RS_SGEMM_SPLIT_WG");
+        return v ? std::max(1, atoi(v)) : 512;
+    }();
+    if (tiles < target) splits = std::max(1, std::min(std::min((target + tiles - 1) / tiles, steps / 4), 16));
     const int per = (steps + splits - 1) / splits;
     *kc = per * SG_BK;
     return (steps + per - 1) / per;
