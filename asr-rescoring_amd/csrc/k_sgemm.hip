@@ -81,16 +81,14 @@ __device__ __forceinline__ void sg_store_lds(float* __restrict__ s, const float4
 
 // C[M][N] (+)= A·B over k in [z·kc, min(K, (z+1)·kc)) for split z = blockIdx.z.
 // ws == nullptr: C = acc (+ C when accum).  Otherwise the partial goes to ws[z][M][N].
-// OCC: minimum workgroups per CU the register allocation must allow (launch-bounds hint)
-// ST: LDS stages — 1: store, barrier, MFMAs, barrier per K-step; 2: the next K-step's tiles go
-// to the other stage right after this step's MFMAs issue (their LDS writes overlap the MFMA
-// drain), one barrier per K-step.
-template <bool AKC, bool BKC, int OCC, int ST>
-__global__ void __launch_bounds__(256, OCC)
+// PF: K-steps of global loads in flight ahead of the one being multiplied (1 or 2; two
+// register sets of staged tiles for PF = 2).
+template <bool AKC, bool BKC, int PF>
+__global__ void __launch_bounds__(256)
 sgemm_f32_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb, float* __restrict__ C,
                  int ldc, int M, int N, int K, int kc, int accum, float* __restrict__ ws) {
-    extern __shared__ __attribute__((aligned(16))) float sg_smem[];   // ST x (A image | B image)
-    constexpr int SIMG = SG_BK * SG_LD;
+    __shared__ float As[SG_BK * SG_LD];
+    __shared__ float Bs[SG_BK * SG_LD];
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int m0 = blockIdx.y * SG_BM, n0 = blockIdx.x * SG_BN;
     const int kb = blockIdx.z * kc, ke = min(K, kb + kc);
@@ -105,27 +103,15 @@ sgemm_f32_kernel(const float* __restrict__ A, int lda, const float* __restrict__
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    float4 ra[4], rb[4];
-    sg_load<AKC>(A, lda, m0, M, kb, ke, ra);
-    sg_load<BKC>(B, ldb, n0, N, kb, ke, rb);
-    if (ST == 2) {
-        sg_store_lds<AKC>(sg_smem, ra);
-        sg_store_lds<BKC>(sg_smem + SIMG, rb);
+    // one K-step: stage the registers' tiles, refill them PF steps ahead, multiply
+    auto kstep = [&](int k0, float4 (&ra)[4], float4 (&rb)[4]) {
+        sg_store_lds<AKC>(As, ra);
+        sg_store_lds<BKC>(Bs, rb);
         __syncthreads();
-    }
-    int cur = 0;
-    for (int k0 = kb; k0 < ke; k0 += SG_BK) {
-        const bool more = k0 + SG_BK < ke;
-        const float* As = sg_smem + cur * 2 * SIMG;
-        const float* Bs = As + SIMG;
-        if (ST == 1) {
-            sg_store_lds<AKC>(sg_smem, ra);
-            sg_store_lds<BKC>(sg_smem + SIMG, rb);
-            __syncthreads();
-        }
-        if (more) {                            // next step's tiles in flight under this step's MFMAs
-            sg_load<AKC>(A, lda, m0, M, k0 + SG_BK, ke, ra);
-            sg_load<BKC>(B, ldb, n0, N, k0 + SG_BK, ke, rb);
+        const int kn = k0 + PF * SG_BK;
+        if (kn < ke) {                         // tiles PF steps ahead in flight under the MFMAs
+            sg_load<AKC>(A, lda, m0, M, kn, ke, ra);
+            sg_load<BKC>(B, ldb, n0, N, kn, ke, rb);
         }
         // MFMA step kk, lane half h: k = 2 kk + h (the instruction's A[i][k = lane >> 5] map).
         // Fragments of step kk + 1 are read before step kk's MFMAs issue, so the LDS latency
@@ -148,15 +134,29 @@ sgemm_f32_kernel(const float* __restrict__ A, int lda, const float* __restrict__
             __builtin_amdgcn_sched_barrier(0);
             a0 = na0; a1 = na1; b0 = nb0; b1 = nb1;
         }
-        if (ST == 2) {
-            if (more) {
-                float* nx = sg_smem + (cur ^ 1) * 2 * SIMG;
-                sg_store_lds<AKC>(nx, ra);
-                sg_store_lds<BKC>(nx + SIMG, rb);
-            }
-            cur ^= 1;
-        }
         __syncthreads();
+    };
+
+    float4 ra[4], rb[4];
+    sg_load<AKC>(A, lda, m0, M, kb, ke, ra);
+    sg_load<BKC>(B, ldb, n0, N, kb, ke, rb);
+    if constexpr (PF == 1) {
+        for (int k0 = kb; k0 < ke; k0 += SG_BK) kstep(k0, ra, rb);
+    } else {
+        float4 ra2[4], rb2[4];
+        if (kb + SG_BK < ke) {
+            sg_load<AKC>(A, lda, m0, M, kb + SG_BK, ke, ra2);
+            sg_load<BKC>(B, ldb, n0, N, kb + SG_BK, ke, rb2);
+        }
+        for (int k0 = kb; k0 < ke; k0 += SG_BK) {
+            kstep(k0, ra, rb);                 // refills ra / rb with step k0 + 2 BK
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {      // the next step's tiles are in the second set
+                const float4 ta = ra[i], tb = rb[i];
+                ra[i] = ra2[i]; rb[i] = rb2[i];
+                ra2[i] = ta; rb2[i] = tb;
+            }
+        }
     }
 
     // D map of the 32x32 forms: column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
@@ -249,41 +249,20 @@ hipError_t tr_sgemm(int M, int N, int K, const float* A, int lda, bool a_kc, con
         P = ws;
     }
     const dim3 grid((N + SG_BN - 1) / SG_BN, (M + SG_BM - 1) / SG_BM, splits);
-#define SG_LAUNCH(AK, BK_, O)                                                                               \
-    do {                                                                                                    \
-        constexpr int smem1 = 2 * SG_BK * SG_LD * 4;                                                        \
-        if (stages == 2) {                                                                                  \
-            static bool attr = false;                                                                       \
-            if (!attr) {                                                                                    \
-                hipError_t ea = hipFuncSetAttribute((const void*)sgemm_f32_kernel<AK, BK_, O, 2>,           \
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize, 2 * smem1); \
-                if (ea != hipSuccess) return ea;                                                            \
-                attr = true;                                                                                \
-            }                                                                                               \
-            hipLaunchKernelGGL((sgemm_f32_kernel<AK, BK_, O, 2>), grid, dim3(256), 2 * smem1, s, A, lda, B,  \
-                               ldb, C, ldc, M, N, K, kc, accum, P);                                         \
-        } else {                                                                                            \
-            hipLaunchKernelGGL((sgemm_f32_kernel<AK, BK_, O, 1>), grid, dim3(256), smem1, s, A, lda, B, ldb, \
-                               C, ldc, M, N, K, kc, accum, P);                                              \
-        }                                                                                                   \
-    } while (0)
-#define SG_FORMS(O)                                  \
-    if (a_kc && b_kc) SG_LAUNCH(true, true, O);      \
-    else if (a_kc) SG_LAUNCH(true, false, O);        \
-    else if (b_kc) SG_LAUNCH(false, true, O);        \
-    else SG_LAUNCH(false, false, O);
-    static const int stages = [] {
-        const char* v = getenv("RS_SGEMM_STAGES");
+#define SG_LAUNCH(AK, BK_, PF)                                                                                 \
+    hipLaunchKernelGGL((sgemm_f32_kernel<AK, BK_, PF>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K, kc, \
+                       accum, P)
+#define SG_FORMS(PF)                                  \
+    if (a_kc && b_kc) SG_LAUNCH(true, true, PF);      \
+    else if (a_kc) SG_LAUNCH(true, false, PF);        \
+    else if (b_kc) SG_LAUNCH(false, true, PF);        \
+    else SG_LAUNCH(false, false, PF);
+    static const int pf = [] {                         // RS_SGEMM_PF=2: A/B knob
+        const char* v = getenv("RS_SGEMM_PF");
         return v && atoi(v) == 2 ? 2 : 1;
     }();
-    static const int occ = [] {
-        const char* v = getenv("RS_SGEMM_OCC");
-        return v ? atoi(v) : 1;
-    }();
-    if (occ >= 4) {
-        SG_FORMS(4)
-    } else if (occ == 3) {
-        SG_FORMS(3)
+    if (pf == 2) {
+        SG_FORMS(2)
     } else {
         SG_FORMS(1)
     }
