@@ -59,36 +59,43 @@ __device__ __forceinline__ void sg_load(const float* __restrict__ src, int ld, i
 }
 
 // [k][row] LDS image: k-contiguous sources are transposed by the writes (4 ds_write_b32 per
-// float4), row-contiguous ones go in as one ds_write_b128
+// float4), row-contiguous ones go in as one ds_write_b128.  Piece i (0..3) of this thread.
+template <bool KC>
+__device__ __forceinline__ void sg_store_one(float* __restrict__ s, int i, const float4 v) {
+    const int idx = threadIdx.x + 256 * i;
+    if (KC) {
+        const int row = idx >> 3, k = (idx & 7) * 4;
+        s[(k + 0) * SG_LD + row] = v.x;
+        s[(k + 1) * SG_LD + row] = v.y;
+        s[(k + 2) * SG_LD + row] = v.z;
+        s[(k + 3) * SG_LD + row] = v.w;
+    } else {
+        const int k = idx >> 5, row = (idx & 31) * 4;
+        *(float4*)(s + k * SG_LD + row) = v;
+    }
+}
+
 template <bool KC>
 __device__ __forceinline__ void sg_store_lds(float* __restrict__ s, const float4 (&r)[4]) {
-    const int t = threadIdx.x;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int idx = t + 256 * i;
-        if (KC) {
-            const int row = idx >> 3, k = (idx & 7) * 4;
-            s[(k + 0) * SG_LD + row] = r[i].x;
-            s[(k + 1) * SG_LD + row] = r[i].y;
-            s[(k + 2) * SG_LD + row] = r[i].z;
-            s[(k + 3) * SG_LD + row] = r[i].w;
-        } else {
-            const int k = idx >> 5, row = (idx & 31) * 4;
-            *(float4*)(s + k * SG_LD + row) = r[i];
-        }
-    }
+    for (int i = 0; i < 4; ++i) sg_store_one<KC>(s, i, r[i]);
 }
 
 // C[M][N] (+)= A·B over k in [z·kc, min(K, (z+1)·kc)) for split z = blockIdx.z.
 // ws == nullptr: C = acc (+ C when accum).  Otherwise the partial goes to ws[z][M][N].
-// PF: K-steps of global loads in flight ahead of the one being multiplied (1 or 2; two
-// register sets of staged tiles for PF = 2).
-template <bool AKC, bool BKC, int PF>
+// MODE 1 (default): one LDS stage — store, barrier, MFMAs, barrier per K-step, the next
+// step's global loads in flight under the MFMAs.  MODE 2: the same with loads two K-steps
+// ahead (a second register set).  MODE 3: two LDS stages — the next step's tiles are
+// written to the other stage between the second half of this step's MFMAs (one float4 piece
+// after each group of four), one barrier per K-step.
+template <bool AKC, bool BKC, int MODE>
 __global__ void __launch_bounds__(256)
 sgemm_f32_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb, float* __restrict__ C,
                  int ldc, int M, int N, int K, int kc, int accum, float* __restrict__ ws) {
-    __shared__ float As[SG_BK * SG_LD];
-    __shared__ float Bs[SG_BK * SG_LD];
+    extern __shared__ __attribute__((aligned(16))) float sg_smem[];   // stages x (A image | B image)
+    constexpr int SIMG = SG_BK * SG_LD, PF = MODE == 2 ? 2 : 1;
+    float* As = sg_smem;
+    float* Bs = sg_smem + SIMG;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int m0 = blockIdx.y * SG_BM, n0 = blockIdx.x * SG_BN;
     const int kb = blockIdx.z * kc, ke = min(K, kb + kc);
@@ -140,7 +147,45 @@ sgemm_f32_kernel(const float* __restrict__ A, int lda, const float* __restrict__
     float4 ra[4], rb[4];
     sg_load<AKC>(A, lda, m0, M, kb, ke, ra);
     sg_load<BKC>(B, ldb, n0, N, kb, ke, rb);
-    if constexpr (PF == 1) {
+    if constexpr (MODE == 3) {
+        sg_store_lds<AKC>(sg_smem, ra);
+        sg_store_lds<BKC>(sg_smem + SIMG, rb);
+        __syncthreads();
+        int cur = 0;
+        for (int k0 = kb; k0 < ke; k0 += SG_BK) {
+            const bool more = k0 + SG_BK < ke;
+            if (more) {
+                sg_load<AKC>(A, lda, m0, M, k0 + SG_BK, ke, ra);
+                sg_load<BKC>(B, ldb, n0, N, k0 + SG_BK, ke, rb);
+            }
+            const float* ap = sg_smem + cur * 2 * SIMG + h * SG_LD + wm + c;
+            const float* bp = ap - (wm + c) + SIMG + wn + c;
+            float* nx = sg_smem + (cur ^ 1) * 2 * SIMG;
+            float a0 = ap[0], a1 = ap[32], b0 = bp[0], b1 = bp[32];
+#pragma unroll
+            for (int kk = 0; kk < SG_BK / 2; ++kk) {
+                float na0 = 0.f, na1 = 0.f, nb0 = 0.f, nb1 = 0.f;
+                if (kk + 1 < SG_BK / 2) {
+                    const int o = 2 * (kk + 1) * SG_LD;
+                    na0 = ap[o]; na1 = ap[o + 32]; nb0 = bp[o]; nb1 = bp[o + 32];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
+                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
+                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
+                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
+                if (kk >= 8 && more) {         // pieces 0-3 of A, then of B, half a step after their loads
+                    const int i = kk - 8;
+                    if (i < 4) sg_store_one<AKC>(nx, i, ra[i]);
+                    else sg_store_one<BKC>(nx + SIMG, i - 4, rb[i - 4]);
+                }
+                __builtin_amdgcn_sched_barrier(0);
+                a0 = na0; a1 = na1; b0 = nb0; b1 = nb1;
+            }
+            __syncthreads();
+            cur ^= 1;
+        }
+    } else if constexpr (PF == 1) {
         for (int k0 = kb; k0 < ke; k0 += SG_BK) kstep(k0, ra, rb);
     } else {
         float4 ra2[4], rb2[4];
@@ -249,19 +294,34 @@ hipError_t tr_sgemm(int M, int N, int K, const float* A, int lda, bool a_kc, con
         P = ws;
     }
     const dim3 grid((N + SG_BN - 1) / SG_BN, (M + SG_BM - 1) / SG_BM, splits);
-#define SG_LAUNCH(AK, BK_, PF)                                                                                 \
-    hipLaunchKernelGGL((sgemm_f32_kernel<AK, BK_, PF>), grid, dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K, kc, \
-                       accum, P)
-#define SG_FORMS(PF)                                  \
-    if (a_kc && b_kc) SG_LAUNCH(true, true, PF);      \
-    else if (a_kc) SG_LAUNCH(true, false, PF);        \
-    else if (b_kc) SG_LAUNCH(false, true, PF);        \
-    else SG_LAUNCH(false, false, PF);
-    static const int pf = [] {                         // RS_SGEMM_PF=2: A/B knob
-        const char* v = getenv("RS_SGEMM_PF");
-        return v && atoi(v) == 2 ? 2 : 1;
+#define SG_LAUNCH(AK, BK_, MD)                                                                              \
+    do {                                                                                                    \
+        constexpr int smem = (MD == 3 ? 4 : 2) * SG_BK * SG_LD * 4;                                          \
+        if (smem > 65536) {                                                                                 \
+            static bool attr = false;                                                                       \
+            if (!attr) {                                                                                    \
+                hipError_t ea = hipFuncSetAttribute((const void*)sgemm_f32_kernel<AK, BK_, MD>,             \
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, smem);      \
+                if (ea != hipSuccess) return ea;                                                            \
+                attr = true;                                                                                \
+            }                                                                                               \
+        }                                                                                                   \
+        hipLaunchKernelGGL((sgemm_f32_kernel<AK, BK_, MD>), grid, dim3(256), smem, s, A, lda, B, ldb, C, ldc, \
+                           M, N, K, kc, accum, P);                                                          \
+    } while (0)
+#define SG_FORMS(MD)                                  \
+    if (a_kc && b_kc) SG_LAUNCH(true, true, MD);      \
+    else if (a_kc) SG_LAUNCH(true, false, MD);        \
+    else if (b_kc) SG_LAUNCH(false, true, MD);        \
+    else SG_LAUNCH(false, false, MD);
+    static const int mode = [] {                       // RS_SGEMM_MODE=2/3: A/B knob
+        const char* v = getenv("RS_SGEMM_MODE");
+        const int m = v ? atoi(v) : 1;
+        return m == 2 || m == 3 ? m : 1;
     }();
-    if (pf == 2) {
+    if (mode == 3) {
+        SG_FORMS(3)
+    } else if (mode == 2) {
         SG_FORMS(2)
     } else {
         SG_FORMS(1)
