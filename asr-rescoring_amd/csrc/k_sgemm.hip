@@ -13,10 +13,12 @@
 // BK = 32.  Both operands are staged as [k][row] LDS images (row stride 132 floats), so every
 // fragment read is one ds_read_b32 over consecutive rows; k-contiguous sources are loaded as
 // float4 along k and transposed by the LDS writes, row-contiguous ones go in as float4.  The
-// next K-step's tiles are loaded into registers while this step's MFMAs run.  (Measured
-// against two variants on MI355X, tools/sgemm_bench.py: two LDS stages with source-oriented
-// images and ds_read_b128 fragments, and the same with a bank-split [k][row] stride, were
-// 6 % and 38 % slower over the training shapes.)
+// next K-step's tiles are loaded into registers while this step's MFMAs run, and each MFMA
+// step's fragments are read one step ahead.  (Measured on MI355X with tools/sgemm_bench.py
+// over the training shapes — DESIGN §8 "Training": two LDS stages with source-oriented images
+// and ds_read_b128 fragments, the same with a bank-split [k][row] stride, loads two K-steps
+// ahead (RS_SGEMM_MODE=2), two stages with the next step's pieces interleaved into the MFMAs
+// (RS_SGEMM_MODE=3) and launch-bounds occupancy 3–4 were all equal or slower.)
 // Few output tiles (the weight gradients of a ~1k-token batch, the projections of a small
 // batch) are split over K: each split writes its partial tile to a workspace and an ordered
 // sum over the splits closes it — no float atomics, so a training step stays bitwise
