@@ -32,6 +32,11 @@
 namespace {
 
 constexpr int SG_BM = 128, SG_BN = 128, SG_BK = 32, SG_LD = SG_BM + 4;
+// row stride of an operand's [k][row] image: 130 (≡ 2 mod 64 banks) for k-contiguous sources,
+// whose transposed scalar writes then hit 64 distinct banks per wave (132: two-way
+// conflicts); 132 for row-contiguous ones (16-B aligned rows for the float4 writes)
+template <bool KC>
+constexpr int sg_ld() { return KC ? SG_BM + 2 : SG_BM + 4; }
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // Loads one operand's [rows 128] × [k 32] tile into registers (4 float4 per thread).
@@ -67,13 +72,14 @@ __device__ __forceinline__ void sg_store_one(float* __restrict__ s, int i, const
     const int idx = threadIdx.x + 256 * i;
     if (KC) {
         const int row = idx >> 3, k = (idx & 7) * 4;
-        s[(k + 0) * SG_LD + row] = v.x;
-        s[(k + 1) * SG_LD + row] = v.y;
-        s[(k + 2) * SG_LD + row] = v.z;
-        s[(k + 3) * SG_LD + row] = v.w;
+        constexpr int L = sg_ld<true>();
+        s[(k + 0) * L + row] = v.x;
+        s[(k + 1) * L + row] = v.y;
+        s[(k + 2) * L + row] = v.z;
+        s[(k + 3) * L + row] = v.w;
     } else {
         const int k = idx >> 5, row = (idx & 31) * 4;
-        *(float4*)(s + k * SG_LD + row) = v;
+        *(float4*)(s + k * sg_ld<false>() + row) = v;
     }
 }
 
@@ -125,15 +131,16 @@ sgemm_f32_kernel(const float* __restrict__ A, int lda, const float* __restrict__
         // MFMA step kk, lane half h: k = 2 kk + h (the instruction's A[i][k = lane >> 5] map).
         // Fragments of step kk + 1 are read before step kk's MFMAs issue, so the LDS latency
         // runs under the MFMA pipe (hipcc otherwise waits lgkmcnt(0) before every step).
-        const float* ap = As + h * SG_LD + wm + c;
-        const float* bp = Bs + h * SG_LD + wn + c;
+        constexpr int LA = sg_ld<AKC>(), LB = sg_ld<BKC>();
+        const float* ap = As + h * LA + wm + c;
+        const float* bp = Bs + h * LB + wn + c;
         float a0 = ap[0], a1 = ap[32], b0 = bp[0], b1 = bp[32];
 #pragma unroll
         for (int kk = 0; kk < SG_BK / 2; ++kk) {
             float na0 = 0.f, na1 = 0.f, nb0 = 0.f, nb1 = 0.f;
             if (kk + 1 < SG_BK / 2) {
-                const int o = 2 * (kk + 1) * SG_LD;
-                na0 = ap[o]; na1 = ap[o + 32]; nb0 = bp[o]; nb1 = bp[o + 32];
+                const int oa = 2 * (kk + 1) * LA, ob = 2 * (kk + 1) * LB;
+                na0 = ap[oa]; na1 = ap[oa + 32]; nb0 = bp[ob]; nb1 = bp[ob + 32];
             }
             __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of this step's MFMAs
             acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
@@ -160,16 +167,17 @@ sgemm_f32_kernel(const float* __restrict__ A, int lda, const float* __restrict__
                 sg_load<AKC>(A, lda, m0, M, k0 + SG_BK, ke, ra);
                 sg_load<BKC>(B, ldb, n0, N, k0 + SG_BK, ke, rb);
             }
-            const float* ap = sg_smem + cur * 2 * SIMG + h * SG_LD + wm + c;
-            const float* bp = ap - (wm + c) + SIMG + wn + c;
+            constexpr int LA = sg_ld<AKC>(), LB = sg_ld<BKC>();
+            const float* ap = sg_smem + cur * 2 * SIMG + h * LA + wm + c;
+            const float* bp = sg_smem + cur * 2 * SIMG + SIMG + h * LB + wn + c;
             float* nx = sg_smem + (cur ^ 1) * 2 * SIMG;
             float a0 = ap[0], a1 = ap[32], b0 = bp[0], b1 = bp[32];
 #pragma unroll
             for (int kk = 0; kk < SG_BK / 2; ++kk) {
                 float na0 = 0.f, na1 = 0.f, nb0 = 0.f, nb1 = 0.f;
                 if (kk + 1 < SG_BK / 2) {
-                    const int o = 2 * (kk + 1) * SG_LD;
-                    na0 = ap[o]; na1 = ap[o + 32]; nb0 = bp[o]; nb1 = bp[o + 32];
+                    const int oa = 2 * (kk + 1) * LA, ob = 2 * (kk + 1) * LB;
+                    na0 = ap[oa]; na1 = ap[oa + 32]; nb0 = bp[ob]; nb1 = bp[ob + 32];
                 }
                 __builtin_amdgcn_sched_barrier(0);
                 acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
