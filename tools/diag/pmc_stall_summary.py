@@ -8,6 +8,10 @@ import sys
 
 
 def short(n):
+    m = re.search(r"sgemm_f32_kernel<(true|false), (true|false), (\d+)>", n) or \
+        re.search(r"sgemm_f32_kernelILb(\d)ELb(\d)ELi(\d+)E", n)
+    if m:
+        return f"sgemm_f32<{m.group(1)},{m.group(2)},mode{m.group(3)}>"
     m = re.search(r"gemm_x3s_kernelILi(\d+)ELi(\d+)E", n)
     if m:
         return f"x3s<{m.group(1)},{m.group(2)}>"
