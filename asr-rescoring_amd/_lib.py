@@ -36,7 +36,9 @@ RS_LOSS = {"MD": 0, "MD_MWER": 1, "MD_MWED": 2}
 class RsTrainOpts(ctypes.Structure):
     _fields_ = [("loss", ctypes.c_int32), ("md_loss_weight", ctypes.c_float), ("lr", ctypes.c_float),
                 ("beta1", ctypes.c_float), ("beta2", ctypes.c_float), ("eps", ctypes.c_float),
-                ("weight_decay", ctypes.c_float), ("update", ctypes.c_int32)]
+                ("weight_decay", ctypes.c_float), ("update", ctypes.c_int32),
+                ("hidden_dropout", ctypes.c_float), ("attn_dropout", ctypes.c_float),
+                ("dropout_seed", ctypes.c_uint32)]
 
 
 class RescoreError(RuntimeError):
@@ -73,6 +75,9 @@ _SIGS = {
     "rs_trainer_get_tensor": (ctypes.c_int, [P, ctypes.c_char_p, P, I64]),
     "rs_trainer_get_grad": (ctypes.c_int, [P, ctypes.c_char_p, P, I64]),
     "rs_trainer_reset_optimizer": (ctypes.c_int, [P]),
+    "rs_trainer_dropout_step": (I64, [P]),
+    "rs_trainer_set_dropout_step": (ctypes.c_int, [P, I64]),
+    "rs_dropout_keep": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_float, I64, P, P]),
     "rs_trainer_destroy": (None, [P]),
     "rs_bertscore_recall": (ctypes.c_int, [P, P, P, P, I32, P, P, P]),
     "rs_align": (ctypes.c_int, [P, P, P, P, I32, P, P, P, P, P, P, P, I32, P]),

@@ -8,7 +8,9 @@ on the HIP path:
 
 * ``BertScorer.embed`` — ``get_bert_embedding`` / ``bert_encode``: the last hidden state of
   the truncated encoder for every token, L2-normalised as ``greedy_cos_idf`` does first
-  (``rs_token_embed``).
+  (``rs_token_embed``).  Default precision fp16x3: the encoder's GEMMs, the embeddings (a
+  two-part fp16 image, ~22 bits) and the cosines (three fp16 MFMA products) are fp32-class,
+  as bert_score computes in fp32.
 * ``BertScorer.recall_matrix`` — ``greedy_cos_idf`` for every ordered pair (cand i, ref j)
   of each utterance's hypotheses in one fused MFMA kernel (``rs_bertscore_recall``):
   R(i|j), with P(i|j) = R(j|i) and F = 2PR / (P + R).
@@ -63,20 +65,26 @@ class BertScorer(BertEngine):
     """Encoder-only engine for the BERTScore utility (model truncated to ``num_layers``)."""
 
     def __init__(self, weights, shape: BertShape = BERT_BASE, num_layers: int = BERT_SCORE_LAYERS,
-                 device=0, max_rows: int = 65536, precision: str = "fp16"):
+                 device=0, max_rows: int = 65536, precision: str = "fp16x3"):
+        # fp16x3 (default): fp32-class encoder, two-part embeddings and split-operand cosines,
+        # as bert_score's fp32 model and matmul; "fp16" is the opt-in reduced-precision mode
         num_layers = min(num_layers, shape.layers)
         sh = dataclasses.replace(shape, layers=num_layers)
         super().__init__(truncate_weights(weights, num_layers), sh, _lib.RS_HEAD_EMB, device, max_rows,
                          precision)
 
     def embed(self, tokens, hyp_off) -> torch.Tensor:
-        """fp16 [sum T, H]: L2-normalised last hidden state of every token."""
+        """[sum T, H]: L2-normalised last hidden state of every token — float32 (hi + lo/64 of
+        the two-part image) in the fp16x3 mode, fp16 in the fp16 mode."""
         off = np.ascontiguousarray(hyp_off, np.int32)
         d_tok = self._dev_tokens(tokens)
-        out = torch.empty(int(off[-1]) if len(off) else 0, self.shape.hidden, dtype=torch.float16,
+        H, two = self.shape.hidden, self.precision == "fp16x3"
+        out = torch.empty(int(off[-1]) if len(off) else 0, H * (2 if two else 1), dtype=torch.float16,
                           device=self.device)
         _lib.check(self.lib.rs_token_embed(self.handle, _lib.ptr(d_tok), off.ctypes.data, len(off) - 1,
                                            _lib.ptr(out), _lib.stream_ptr(self.device)))
+        if two:
+            return out[:, :H].float() + out[:, H:].float() * (1.0 / 64.0)
         return out
 
     def recall_matrices(self, tokens, hyp_off, utt_off, clamped: bool = True):

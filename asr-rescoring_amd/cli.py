@@ -161,6 +161,16 @@ def _save_checkpoint(output_path: str, state: Dict[str, np.ndarray], n: int) -> 
     return path
 
 
+def _dropout_args(cfg) -> Dict[str, float]:
+    """BERT train-mode dropout of the trainers: BertConfig's defaults (hidden_dropout_prob =
+    attention_probs_dropout_prob = 0.1), which the reference's from_pretrained models train
+    with; the same keys in the YAML override them (0 = off), ``dropout_seed`` (default ``seed``)
+    keys the counter-based masks."""
+    return {"hidden_dropout": float(get(cfg, "hidden_dropout_prob", 0.1)),
+            "attn_dropout": float(get(cfg, "attention_probs_dropout_prob", 0.1)),
+            "dropout_seed": int(get(cfg, "dropout_seed", get(cfg, "seed", 0)))}
+
+
 def mlm_finetune(cfg) -> Dict[str, object]:
     """MLM_PLL/main.py:117-161 (mlm_finetune_bert) on the native trainer (``train.MLMTrainer``).
 
@@ -172,8 +182,8 @@ def mlm_finetune(cfg) -> Dict[str, object]:
     ``checkpoint_{epoch}.pth`` and ``loss.json`` (``{"train": [...], "dev": [...]}``, zeros for
     epochs not run yet, as ``:131-161`` writes it).  Extra: ``checkpoint_path`` /
     ``random_init_seed`` (initial weights: bert-base-chinese cannot be fetched offline),
-    ``train_ref_text_path`` ({utt: text}, expanded by ``do_job_rows``), ``weight_decay``.
-    ``dataloader.shuffle: True`` draws the order from torch.randperm seeded by ``seed`` (not the
+    ``train_ref_text_path`` ({utt: text}, expanded by ``do_job_rows``), ``weight_decay``,
+    dropout keys (``_dropout_args``).  ``dataloader.shuffle: True`` draws the order from torch.randperm seeded by ``seed`` (not the
     reference's sampler stream)."""
     import torch
     from .train import MLMTrainer, do_job_rows, mlm_epoch
@@ -197,7 +207,7 @@ def mlm_finetune(cfg) -> Dict[str, object]:
     if train_d is None:
         raise FileNotFoundError("train_data_path (do_job rows) or train_ref_text_path is required")
     tr = MLMTrainer(_weights(cfg, "mlm"), BERT_BASE, device=_dev(cfg), lr=float(get(cfg, "lr", 1e-5)),
-                    weight_decay=float(get(cfg, "weight_decay", 0.01)))
+                    weight_decay=float(get(cfg, "weight_decay", 0.01)), **_dropout_args(cfg))
     bs = int(get(cfg, "dataloader.batch_size", get(cfg, "batch_size", 32)))
     shuffle = bool(get(cfg, "dataloader.shuffle", False))
     gen = torch.Generator().manual_seed(int(get(cfg, "seed", 0)))
@@ -206,6 +216,7 @@ def mlm_finetune(cfg) -> Dict[str, object]:
     try:
         for ep in range(1, epochs + 1):
             tr.reset_optimizer()
+            tr.set_dropout_step(ep << 20)            # epoch-keyed masks: a resumed run draws the same
             order = torch.randperm(len(train_d[0]), generator=gen).numpy() if shuffle else None
             train_rec[ep - 1] = mlm_epoch(tr, *train_d, bs, update=True, order=order)
             print("epoch ", ep, " train loss: ", train_rec[ep - 1])
@@ -287,7 +298,7 @@ def rescorebert_train(cfg) -> Dict[str, object]:
     ``output_path``, ``resume.start_from`` / ``resume.checkpoint_path``.  Per epoch: a fresh
     AdamW (``:83-86``), the train pass, the dev loss (no update), ``checkpoint_{epoch}.pth``
     and ``loss.json``.  Extra: ``checkpoint_path`` / ``random_init_seed`` (initial weights:
-    bert-base-chinese cannot be fetched offline), ``weight_decay``."""
+    bert-base-chinese cannot be fetched offline), ``weight_decay``, dropout keys (``_dropout_args``)."""
     from .train import RescoreBertTrainer, rescorebert_epoch
     os.makedirs(cfg.output_path, exist_ok=True)
     method = str(get(cfg, "method", "MD"))
@@ -307,7 +318,7 @@ def rescorebert_train(cfg) -> Dict[str, object]:
         train_rec, dev_rec = [], []
     tr = RescoreBertTrainer(weights, BERT_BASE, device=_dev(cfg), method=method,
                             md_loss_weight=float(get(cfg, "md_loss_weight", 1.0)), lr=float(get(cfg, "lr", 1e-5)),
-                            weight_decay=float(get(cfg, "weight_decay", 0.01)))
+                            weight_decay=float(get(cfg, "weight_decay", 0.01)), **_dropout_args(cfg))
     bs, n_best = int(get(cfg, "batch_size", 1)), int(get(cfg, "n_best", 1))
 
     def epoch_pass(f, update):
@@ -319,6 +330,7 @@ def rescorebert_train(cfg) -> Dict[str, object]:
         for ep in range(int(start) if resume else 1, int(get(cfg, "epoch", 1)) + 1):
             print("Epoch {}/{}".format(ep, get(cfg, "epoch", 1)))
             tr.reset_optimizer()
+            tr.set_dropout_step(ep << 20)            # epoch-keyed masks: a resumed run draws the same
             train_rec.append(epoch_pass(train_f, True))
             print("epoch ", ep, " train loss: ", train_rec[-1], "\n")
             if dev_f is not None and all(f in dev_f["features"] for f in need):

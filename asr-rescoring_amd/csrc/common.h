@@ -166,14 +166,17 @@ hipError_t launch_ln_res_img(f16* h16, const float* o32, int rows, const float* 
 hipError_t launch_embed_unique(const int* tok, SeqMeta sm, int s0, int s1, int mask_id, int vocab,
                                const float* word, const float* pos, const float* type0, const float* g,
                                const float* b, float eps, int H, f16* h16u, int kx, hipStream_t st);
-// BERTScore recall matrix (k_bertscore.hip); items = (utterance, j0, j1, -) ref-column runs
+// BERTScore recall matrix (k_bertscore.hip); items = (utterance, j0, j1, -) ref-column runs of
+// at most bertscore_cols(two) columns; two: emb is the two-part image (split-operand cosines)
+int bertscore_cols(bool two);
 hipError_t launch_bertscore_recall(const f16* emb, int H, const int* hyp_off, const int* utt_off,
                                    const long long* mat_off, const int4* items, int n_items, float* rmat, float* rmat0,
-                                   hipStream_t st);
-// Last hidden state, L2-normalised per token, fp16 at out[(tok_off + t) * H] (BERTScore)
+                                   hipStream_t st, bool two = false);
+// Last hidden state, L2-normalised per token, at out[(tok_off + t) * H * (two ? 2 : 1)] (BERTScore):
+// fp16, or (two) the two-part image [hi | lo*64]
 hipError_t launch_embed_out(const float* x32, const float2* stats, const float* g, const float* b,
                             SeqMeta sm, int s0, int s1, int row0, int H, f16* out, hipStream_t st,
-                            const f16* himg = nullptr);
+                            const f16* himg = nullptr, bool two = false);
 // max_len: longest sequence of the launch (0 = unknown): the 16x16x32 kernel serves chunks whose
 // sequences all fit one 64-key block, the 32x32x16 kernel the others (fewer K/V reloads).
 // dedup: qkv holds unique rows; sequence s, position t reads row (t == mask_pos ? urow_m : urow_h + t)

@@ -1239,8 +1239,10 @@ hipError_t launch_embed_unique(const int* tok, SeqMeta sm, int s0, int s1, int m
 
 // BERTScore embeddings (bert_score bert_encode + greedy_cos_idf's row normalisation):
 // e = LN(x) of the last layer, rebuilt from the pre-LN stream, then e / ||e||_2 in fp32,
-// stored fp16 at the token's position in the caller's ragged token layout.
-template <int NV>
+// stored at the token's position in the caller's ragged token layout: fp16 [H] (TWO false),
+// or the two-part image [hi | lo*64] of 2H halves (TWO, the fp16x3 mode: e = hi + lo/64,
+// ~22 significant bits, which the split-operand recall kernel multiplies as three products).
+template <int NV, bool TWO>
 __global__ void __launch_bounds__(256)
 embed_out_kernel(const float* __restrict__ x32, const float2* __restrict__ stats,
                  const float* __restrict__ g, const float* __restrict__ b, SeqMeta sm, int s0,
@@ -1270,21 +1272,29 @@ embed_out_kernel(const float* __restrict__ x32, const float2* __restrict__ stats
             q += y[v].x * y[v].x + y[v].y * y[v].y + y[v].z * y[v].z + y[v].w * y[v].w;
         }
         const float nrm = sqrtf(wave_sum(q));
-        f16* o = out + (size_t)(toff + t) * H;
+        f16* o = out + (size_t)(toff + t) * H * (TWO ? 2 : 1);
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             const int c = v * 256 + lane * 4;
-            const half4 h = {(f16)(y[v].x / nrm), (f16)(y[v].y / nrm), (f16)(y[v].z / nrm), (f16)(y[v].w / nrm)};
-            *(half4*)(o + c) = h;
+            const float4 e = make_float4(y[v].x / nrm, y[v].y / nrm, y[v].z / nrm, y[v].w / nrm);
+            if constexpr (TWO) put_split4(o, c, H, 2, e);
+            else *(half4*)(o + c) = half4{(f16)e.x, (f16)e.y, (f16)e.z, (f16)e.w};
         }
     }
 }
 
 hipError_t launch_embed_out(const float* x32, const float2* stats, const float* g, const float* b,
-                            SeqMeta sm, int s0, int s1, int row0, int H, f16* out, hipStream_t st, const f16* himg) {
+                            SeqMeta sm, int s0, int s1, int row0, int H, f16* out, hipStream_t st, const f16* himg,
+                            bool two) {
     const int n = s1 - s0;
     if (n <= 0) return hipSuccess;
-#define RS_EO(NV) hipLaunchKernelGGL(embed_out_kernel<NV>, dim3(n), dim3(256), 0, st, x32, stats, g, b, sm, s0, row0, out, himg)
+#define RS_EO(NV)                                                                                                 \
+    do {                                                                                                          \
+        if (two) hipLaunchKernelGGL((embed_out_kernel<NV, true>), dim3(n), dim3(256), 0, st, x32, stats, g, b, sm, \
+                                    s0, row0, out, himg);                                                         \
+        else hipLaunchKernelGGL((embed_out_kernel<NV, false>), dim3(n), dim3(256), 0, st, x32, stats, g, b, sm,   \
+                                s0, row0, out, himg);                                                             \
+    } while (0)
     switch (H) {
         case 256: RS_EO(1); break;
         case 512: RS_EO(2); break;

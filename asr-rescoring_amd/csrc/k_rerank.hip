@@ -55,8 +55,12 @@ __device__ int myers64(const int* __restrict__ a, int m, const int* __restrict__
 }
 
 // Blocked Myers / Hyyro (the pattern cut into 64-row words, horizontal deltas carried from
-// word to word): exact global edit distance for patterns of up to RS_MAX_EDIT symbols, in
-// O(ceil(m / 64) * n) word operations; the per-word Peq bits are formed on the fly.
+// word to word): exact global edit distance for patterns of up to RS_MAX_EDIT symbols.  The
+// bit-vector recurrence is O(ceil(m / 64) * n) word operations, but the per-word Eq masks are
+// formed on the fly by comparing every pattern symbol with each text symbol, so the total is
+// O(m * n) scalar compares (no Peq table: the alphabet is open-ended code points), and Pv / Mv
+// (2 x 2 KiB per thread, dynamically indexed) live in scratch.  Only strings longer than 64
+// symbols come here; ASR hypotheses of the C5 workload never do (myers64 above).
 constexpr int RS_MAX_EDIT = 16384;
 constexpr int RS_MAX_WORDS = RS_MAX_EDIT / 64;
 

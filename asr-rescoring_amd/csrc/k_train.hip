@@ -1,5 +1,5 @@
 // Training kernels (RescoreBert distillation training, backward through
-// the BERT encoder).  fp32 throughout — the reference trains in fp32 — with every reduction
+// the BERT encoder), with BERT's train-mode dropout (train.h TrDrop).  fp32 throughout — the reference trains in fp32 — with every reduction
 // in a fixed order (no float atomics): a training step is bitwise reproducible.
 // GEMMs are plain (transposed) fp32 GEMMs on the f32-input MFMA (k_sgemm.hip); everything
 // else is here.  One wave per token row for row-wise ops; column reductions in two stages
@@ -14,7 +14,8 @@ constexpr float kInvSqrt2Pi = 0.39894228040143268f;
 
 template <int NV>
 __device__ __forceinline__ void ln_fwd_row(const float4 (&x)[NV], const float* g, const float* b, float eps,
-                                           int lane, float2* st, float* h) {
+                                           int lane, float2* st, float* h, const TrDrop& dr = TrDrop(),
+                                           unsigned long long e0 = 0) {
     constexpr int H = NV * 256;
     float s = 0.f;
 #pragma unroll
@@ -32,8 +33,12 @@ __device__ __forceinline__ void ln_fwd_row(const float4 (&x)[NV], const float* g
     for (int v = 0; v < NV; ++v) {
         const int c = v * 256 + lane * 4;
         const float4 gg = *(const float4*)(g + c), bb = *(const float4*)(b + c);
-        *(float4*)(h + c) = make_float4((x[v].x - mean) * rstd * gg.x + bb.x, (x[v].y - mean) * rstd * gg.y + bb.y,
-                                        (x[v].z - mean) * rstd * gg.z + bb.z, (x[v].w - mean) * rstd * gg.w + bb.w);
+        float4 o = make_float4((x[v].x - mean) * rstd * gg.x + bb.x, (x[v].y - mean) * rstd * gg.y + bb.y,
+                               (x[v].z - mean) * rstd * gg.z + bb.z, (x[v].w - mean) * rstd * gg.w + bb.w);
+        if (dr.thresh)
+            o = make_float4(tr_drop(dr, e0 + c, o.x), tr_drop(dr, e0 + c + 1, o.y), tr_drop(dr, e0 + c + 2, o.z),
+                            tr_drop(dr, e0 + c + 3, o.w));
+        *(float4*)(h + c) = o;
     }
 }
 
@@ -43,7 +48,7 @@ __global__ void __launch_bounds__(256)
 tr_embed_ln_kernel(const int* __restrict__ row_tok, const int* __restrict__ row_pos, int M, int vocab,
                    const float* __restrict__ word, const float* __restrict__ pos, const float* __restrict__ type0,
                    const float* __restrict__ g, const float* __restrict__ b, float eps, float* __restrict__ x0,
-                   float2* __restrict__ st, float* __restrict__ h0) {
+                   float2* __restrict__ st, float* __restrict__ h0, TrDrop dr) {
     constexpr int H = NV * 256;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= M) return;
@@ -58,15 +63,15 @@ tr_embed_ln_kernel(const int* __restrict__ row_tok, const int* __restrict__ row_
         x[v] = make_float4((w.x + ty.x) + p.x, (w.y + ty.y) + p.y, (w.z + ty.z) + p.z, (w.w + ty.w) + p.w);
         *(float4*)(x0 + (size_t)row * H + c) = x[v];
     }
-    ln_fwd_row<NV>(x, g, b, eps, lane, st + row, h0 + (size_t)row * H);
+    ln_fwd_row<NV>(x, g, b, eps, lane, st + row, h0 + (size_t)row * H, dr, (unsigned long long)row * H);
 }
 
-// y <- (y + bias) + res (pre-LN, saved), h = LN(y); bias == nullptr: plain LN of y
+// y <- drop(y + bias) + res (pre-LN, saved), h = LN(y); bias == nullptr: plain LN of y
 template <int NV>
 __global__ void __launch_bounds__(256)
 tr_bias_res_ln_kernel(float* __restrict__ y, const float* bias, const float* res,
                       int M, const float* __restrict__ g, const float* __restrict__ b, float eps,
-                      float2* __restrict__ st, float* __restrict__ h) {
+                      float2* __restrict__ st, float* __restrict__ h, TrDrop dr) {
     constexpr int H = NV * 256;
     const int row = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (row >= M) return;
@@ -78,7 +83,13 @@ tr_bias_res_ln_kernel(float* __restrict__ y, const float* bias, const float* res
         if (bias) {
             const float4 bb = *(const float4*)(bias + c);
             const float4 r = *(const float4*)(res + (size_t)row * H + c);
-            x[v] = make_float4((x[v].x + bb.x) + r.x, (x[v].y + bb.y) + r.y, (x[v].z + bb.z) + r.z, (x[v].w + bb.w) + r.w);
+            float4 o = make_float4(x[v].x + bb.x, x[v].y + bb.y, x[v].z + bb.z, x[v].w + bb.w);
+            if (dr.thresh) {
+                const unsigned long long e = (unsigned long long)row * H + c;
+                o = make_float4(tr_drop(dr, e, o.x), tr_drop(dr, e + 1, o.y), tr_drop(dr, e + 2, o.z),
+                                tr_drop(dr, e + 3, o.w));
+            }
+            x[v] = make_float4(o.x + r.x, o.y + r.y, o.z + r.z, o.w + r.w);
             *(float4*)(y + (size_t)row * H + c) = x[v];
         }
     }
@@ -128,7 +139,7 @@ __global__ void tr_bias_kernel(float* __restrict__ y, const float* __restrict__ 
 __global__ void __launch_bounds__(64)
 tr_attn_fwd_kernel(const float* __restrict__ qkv, const int* __restrict__ seq_off, const int* __restrict__ klen,
                    const long long* __restrict__ pofs, int H, int heads, float* __restrict__ P,
-                   float* __restrict__ ctx) {
+                   float* __restrict__ ctx, TrDrop dr) {
     extern __shared__ __attribute__((aligned(16))) float sm_a[];
     const int s = blockIdx.x, hd = blockIdx.y, tid = threadIdx.x;
     const int r0 = seq_off[s], T = seq_off[s + 1] - r0;
@@ -173,11 +184,13 @@ tr_attn_fwd_kernel(const float* __restrict__ qkv, const int* __restrict__ seq_of
         float o[64];
 #pragma unroll
         for (int c = 0; c < 64; ++c) o[c] = 0.f;
+        const unsigned long long e0 = (unsigned long long)(pofs[s] + (long long)hd * T * T + (long long)i * T);
         for (int j = 0; j < T; ++j) {
             const float p = Ph[(long long)i * T + j] / sum;
-            Ph[(long long)i * T + j] = p;
+            Ph[(long long)i * T + j] = p;          // saved before dropout (the backward's P)
+            const float pd = tr_drop(dr, e0 + j, p);
 #pragma unroll
-            for (int c = 0; c < 64; ++c) o[c] += p * sV[j * 64 + c];
+            for (int c = 0; c < 64; ++c) o[c] += pd * sV[j * 64 + c];
         }
         float* op = ctx + (size_t)(r0 + i) * H + hd * 64;
 #pragma unroll
@@ -190,7 +203,7 @@ tr_attn_fwd_kernel(const float* __restrict__ qkv, const int* __restrict__ seq_of
 __global__ void __launch_bounds__(64)
 tr_attn_bwd_kernel(const float* __restrict__ qkv, const float* __restrict__ P, const float* __restrict__ dctx,
                    const int* __restrict__ seq_off, const long long* __restrict__ pofs, int H, int heads,
-                   float* __restrict__ dqkv) {
+                   float* __restrict__ dqkv, TrDrop dr) {
     extern __shared__ __attribute__((aligned(16))) float sm_a[];
     const int s = blockIdx.x, hd = blockIdx.y, tid = threadIdx.x;
     const int r0 = seq_off[s], T = seq_off[s + 1] - r0;
@@ -214,11 +227,14 @@ tr_attn_bwd_kernel(const float* __restrict__ qkv, const float* __restrict__ P, c
             const float4 v = *(const float4*)(gp + c);
             g[c] = v.x; g[c + 1] = v.y; g[c + 2] = v.z; g[c + 3] = v.w;
         }
+        // d(dropped P) = dctx V^T; dP = that * mask * scale
+        const unsigned long long e0 = (unsigned long long)(pofs[s] + (long long)hd * T * T + (long long)i * T);
         float rd = 0.f;
         for (int j = 0; j < T; ++j) {
             float d = 0.f;
 #pragma unroll
             for (int c = 0; c < 64; ++c) d += g[c] * sB[j * 64 + c];
+            d = tr_drop(dr, e0 + j, d);
             sS[i * T + j] = d;
             rd += Ph[(long long)i * T + j] * d;
         }
@@ -247,8 +263,10 @@ tr_attn_bwd_kernel(const float* __restrict__ qkv, const float* __restrict__ P, c
         float dk[64], dv[64];
 #pragma unroll
         for (int c = 0; c < 64; ++c) dk[c] = 0.f, dv[c] = 0.f;
+        const unsigned long long eb = (unsigned long long)(pofs[s] + (long long)hd * T * T) + j;
         for (int i = 0; i < T; ++i) {
-            const float ds = sS[i * T + j], p = Ph[(long long)i * T + j];
+            // dv uses the dropped probabilities the forward multiplied V by
+            const float ds = sS[i * T + j], p = tr_drop(dr, eb + (unsigned long long)i * T, Ph[(long long)i * T + j]);
 #pragma unroll
             for (int c = 0; c < 64; ++c) {
                 dk[c] += ds * sA[i * 64 + c];
@@ -534,6 +552,16 @@ __global__ void tr_adamw_kernel(float* __restrict__ p, const float* __restrict__
     }
 }
 
+__global__ void tr_dropout_kernel(float* dst, const float* src, long long n, TrDrop dr) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        dst[i] = tr_drop(dr, (unsigned long long)i, src[i]);
+}
+
+__global__ void tr_dropout_keep_kernel(uint8_t* __restrict__ keep, long long n, TrDrop dr) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+        keep[i] = dr.thresh == 0 ? 1 : (uint8_t)tr_keep(dr, (unsigned long long)i);
+}
+
 int grid_for(long long n, int bs) { return (int)std::min<long long>((n + bs - 1) / bs, 8192); }
 
 }  // namespace
@@ -549,18 +577,18 @@ int grid_for(long long n, int bs) { return (int)std::min<long long>((n + bs - 1)
 
 hipError_t tr_embed_ln(const int* row_tok, const int* row_pos, int M, int vocab, const float* word,
                        const float* pos, const float* type0, const float* g, const float* b, float eps, int H,
-                       float* x0, float2* st, float* h0, hipStream_t s) {
+                       float* x0, float2* st, float* h0, hipStream_t s, const TrDrop& d) {
     if (M <= 0) return hipSuccess;
     RS_NV_SWITCH(H, hipLaunchKernelGGL(tr_embed_ln_kernel<NV>, dim3((M + 3) / 4), dim3(256), 0, s, row_tok, row_pos,
-                                       M, vocab, word, pos, type0, g, b, eps, x0, st, h0));
+                                       M, vocab, word, pos, type0, g, b, eps, x0, st, h0, d));
     return hipGetLastError();
 }
 
 hipError_t tr_bias_res_ln(float* y, const float* bias, const float* res, int M, const float* g, const float* b,
-                          float eps, int H, float2* st, float* h, hipStream_t s) {
+                          float eps, int H, float2* st, float* h, hipStream_t s, const TrDrop& d) {
     if (M <= 0) return hipSuccess;
     RS_NV_SWITCH(H, hipLaunchKernelGGL(tr_bias_res_ln_kernel<NV>, dim3((M + 3) / 4), dim3(256), 0, s, y, bias, res,
-                                       M, g, b, eps, st, h));
+                                       M, g, b, eps, st, h, bias ? d : TrDrop()));
     return hipGetLastError();
 }
 
@@ -587,22 +615,22 @@ hipError_t tr_bias(float* y, const float* bias, int M, int N, hipStream_t s) {
 static size_t attn_smem(int tmax, bool bwd) { return (size_t)(2 * tmax * 64 + (bwd ? tmax * tmax : 0)) * 4; }
 
 hipError_t tr_attn_fwd(const float* qkv, const int* seq_off, const int* klen, const long long* pofs, int S,
-                       int tmax, int H, int heads, float* P, float* ctx, hipStream_t s) {
+                       int tmax, int H, int heads, float* P, float* ctx, hipStream_t s, const TrDrop& d) {
     if (S <= 0) return hipSuccess;
     const size_t sm = attn_smem(tmax, false);
     hipError_t e = hipFuncSetAttribute((const void*)tr_attn_fwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(tr_attn_fwd_kernel, dim3(S, heads), dim3(64), sm, s, qkv, seq_off, klen, pofs, H, heads, P, ctx);
+    hipLaunchKernelGGL(tr_attn_fwd_kernel, dim3(S, heads), dim3(64), sm, s, qkv, seq_off, klen, pofs, H, heads, P, ctx, d);
     return hipGetLastError();
 }
 
 hipError_t tr_attn_bwd(const float* qkv, const float* P, const float* dctx, const int* seq_off, const long long* pofs,
-                       int S, int tmax, int H, int heads, float* dqkv, hipStream_t s) {
+                       int S, int tmax, int H, int heads, float* dqkv, hipStream_t s, const TrDrop& d) {
     if (S <= 0) return hipSuccess;
     const size_t sm = attn_smem(tmax, true);
     hipError_t e = hipFuncSetAttribute((const void*)tr_attn_bwd_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(tr_attn_bwd_kernel, dim3(S, heads), dim3(64), sm, s, qkv, P, dctx, seq_off, pofs, H, heads, dqkv);
+    hipLaunchKernelGGL(tr_attn_bwd_kernel, dim3(S, heads), dim3(64), sm, s, qkv, P, dctx, seq_off, pofs, H, heads, dqkv, d);
     return hipGetLastError();
 }
 
@@ -669,5 +697,17 @@ hipError_t tr_adamw(float* p, const float* g, float* m, float* v, long long n, f
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(tr_adamw_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, p, g, m, v, n, decay, b1w, b2, b2w,
                        step_size, bc2_sqrt, eps);
+    return hipGetLastError();
+}
+
+hipError_t tr_dropout(float* dst, const float* src, long long n, const TrDrop& d, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(tr_dropout_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, dst, src, n, d);
+    return hipGetLastError();
+}
+
+hipError_t tr_dropout_keep(uint8_t* keep, long long n, const TrDrop& d, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(tr_dropout_keep_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, keep, n, d);
     return hipGetLastError();
 }

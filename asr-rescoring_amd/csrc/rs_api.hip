@@ -10,6 +10,8 @@
 #include <vector>
 #include <cstring>
 #include <cstdio>
+#include <cmath>
+#include <algorithm>
 
 #include "common.h"
 #include "../../include/rescore.h"
@@ -85,6 +87,8 @@ struct rs_model {
     DevBuf meta, hypoff;
     f16* emb_dst = nullptr;     // MODE_EMB output (rs_token_embed / rs_bertscore_recall)
     DevBuf emb, plan;           // rs_bertscore_recall: token embeddings, work-item plan
+    DevBuf flag;                // non-finite-output flag of the last scoring call (range guard)
+    int* pinned_flag = nullptr;
     int* pinned_plan = nullptr;
     size_t pinned_plan_cap = 0;
     hipEvent_t plan_done = nullptr;
@@ -140,6 +144,46 @@ float* upload_f32(rs_model* m, const std::vector<float>& src, size_t n_pad, hipE
     m->allocs.push_back(p);
     *err = hipMemcpy(p, tmp.data(), tmp.size() * sizeof(float), hipMemcpyHostToDevice);
     return (float*)p;
+}
+
+// The fp16 operand images (fp16 and fp16x3 modes) hold |x| <= 65504: a weight beyond it
+// would become inf in its hi part (and NaN in lo), where the reference's fp32 forward stays
+// finite.  Checked once at finalize.
+bool fp16_range_ok(const std::vector<float>& v) {
+    for (float x : v)
+        if (!(std::fabs(x) <= 65504.f)) return false;
+    return true;
+}
+
+// Activations are checked through their consequence: an operand that leaves the fp16 range
+// becomes inf (hi) / NaN (lo) in its image, and inf / NaN then reaches every score that
+// depends on it (LayerNorm, softmax and the log-softmax turn it into NaN; the fp32 reference
+// stays finite there).  One pass over a call's outputs sets a flag, the call synchronises
+// its stream and fails with RS_EUNSUP instead of returning non-finite scores.
+template <class T>
+__global__ void __launch_bounds__(256) nonfinite_kernel(const T* __restrict__ v, size_t n, int* __restrict__ flag) {
+    int bad = 0;
+    for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256)
+        bad |= !__builtin_isfinite((float)v[i]);
+    if (bad) flag[0] = 1;          // plain vector store; every writer stores the same value
+}
+
+template <class T>
+int check_finite(rs_model* m, hipStream_t st, const T* p, size_t n, const char* what) {
+    if (n == 0) return RS_OK;
+    HIPTRY(m->flag.ensure(4));
+    if (!m->pinned_flag) HIPTRY(hipHostMalloc((void**)&m->pinned_flag, 4, hipHostMallocDefault));
+    HIPTRY(hipMemsetAsync(m->flag.p, 0, 4, st));
+    const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(nonfinite_kernel<T>, dim3(blocks), dim3(256), 0, st, p, n, m->flag.as<int>());
+    HIPTRY(hipGetLastError());
+    HIPTRY(hipMemcpyAsync(m->pinned_flag, m->flag.p, 4, hipMemcpyDeviceToHost, st));
+    HIPTRY(hipStreamSynchronize(st));
+    if (*m->pinned_flag)
+        return fail(RS_EUNSUP, std::string("non-finite ") + what +
+                                   ": an activation left the fp16 range of the operand images (|x| > 65504); "
+                                   "the fp32 reference stays finite here");
+    return RS_OK;
 }
 
 int reserve_impl(rs_model* m, int64_t max_rows) {
@@ -476,7 +520,8 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
     if (mode == MODE_EMB) {
         const Layer& L = m->layers[cf.layers - 1];
         ProfScope ps(m, st, RS_K_OTHER, 0);
-        HIPTRY(launch_embed_out(t32, xst, L.g2, L.be2, sm, c.s0, c.s1, 0, H, m->emb_dst, st, imgres ? h16 : nullptr));
+        HIPTRY(launch_embed_out(t32, xst, L.g2, L.be2, sm, c.s0, c.s1, 0, H, m->emb_dst, st, imgres ? h16 : nullptr,
+                                m->kx == 3));
         return RS_OK;
     }
     float* hq32 = m->hq32.as<float>();
@@ -678,7 +723,13 @@ int rs_model_finalize(rs_model* m) {
     if (!miss.empty()) return fail(RS_ESTATE, "tensor " + miss);
     hipError_t err = hipSuccess;
 #define UP32(dst, src, n) do { dst = upload_f32(m, *(src), (n), &err); if (err != hipSuccess) return fail(RS_EHIP, "upload"); } while (0)
-#define UP16(dst, src, rp, cols) do { dst = upload_f16(m, *(src), (rp), (cols), m->kx, &err); if (err != hipSuccess) return fail(RS_EHIP, "upload"); } while (0)
+#define UP16(dst, src, rp, cols) do {                                                                             \
+        if (!fp16_range_ok(*(src)))                                                                             \
+            return fail(RS_EUNSUP, std::string("weight '") + #src + "' has a value outside the fp16 range "    \
+                                   "(|w| > 65504) of the GEMM operand images");                              \
+        dst = upload_f16(m, *(src), (rp), (cols), m->kx, &err);                                                 \
+        if (err != hipSuccess) return fail(RS_EHIP, "upload");                                                 \
+    } while (0)
     UP32(m->word32, word, V * H);
     UP32(m->pos32, pos, (size_t)c.max_pos * H);
     UP32(m->type32, typ, H);     // token_type_ids are all 0 (modeling_bert.py:88-94)
@@ -786,9 +837,11 @@ int rs_pll_score(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, in
     }
     int* d_hso = nullptr;
     if (int r = run_all(m, st, d_tok, sl, MODE_MLM, rows, &hso, &d_hso)) return r;
-    ProfScope ps(m, st, RS_K_OTHER, 0);
-    HIPTRY(launch_segsum_f64(rows, d_hso, n_hyp, d_pll, st));
-    return RS_OK;
+    {
+        ProfScope ps(m, st, RS_K_OTHER, 0);
+        HIPTRY(launch_segsum_f64(rows, d_hso, n_hyp, d_pll, st));
+    }
+    return check_finite(m, st, rows, sl.size(), "masked-token log-probability");
 }
 
 int rs_masked_logprob(rs_model* m, const int32_t* d_ids, const int32_t* h_seq_off,
@@ -803,7 +856,8 @@ int rs_masked_logprob(rs_model* m, const int32_t* d_ids, const int32_t* h_seq_of
         if (h_query[s] < 0 || h_query[s] >= T) return fail(RS_EARG, "query position outside its sequence");
         sl.push(o, T, -1, h_query[s], 0);   // ids already masked by the caller
     }
-    return run_all(m, (hipStream_t)stream, d_ids, sl, MODE_MLM, d_out, nullptr, nullptr, d_label);
+    if (int r = run_all(m, (hipStream_t)stream, d_ids, sl, MODE_MLM, d_out, nullptr, nullptr, d_label)) return r;
+    return check_finite(m, (hipStream_t)stream, d_out, (size_t)n_seq, "masked-token log-probability");
 }
 
 int rs_cls_score(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, int32_t n_hyp,
@@ -816,7 +870,8 @@ int rs_cls_score(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, in
         if (T < 1) return fail(RS_EARG, "empty hypothesis");
         sl.push(o, T, -1, 0, 0);      // query = [CLS] (RescoreBert/model.py:19)
     }
-    return run_all(m, (hipStream_t)stream, d_tok, sl, MODE_CLS, d_out, nullptr, nullptr);
+    if (int r = run_all(m, (hipStream_t)stream, d_tok, sl, MODE_CLS, d_out, nullptr, nullptr)) return r;
+    return check_finite(m, (hipStream_t)stream, d_out, (size_t)n_hyp, "RescoreBert score");
 }
 
 int rs_token_embed(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, int32_t n_hyp,
@@ -832,7 +887,11 @@ int rs_token_embed(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, 
     m->emb_dst = (f16*)d_emb;
     const int r = run_all(m, (hipStream_t)stream, d_tok, sl, MODE_EMB, nullptr, nullptr, nullptr);
     m->emb_dst = nullptr;
-    return r;
+    if (r) return r;
+    // every token row of the hypotheses (contiguous from h_hyp_off[0]) is written
+    const size_t W = (size_t)m->cfg.hidden * (m->kx == 3 ? 2 : 1);
+    return check_finite(m, (hipStream_t)stream, (const f16*)d_emb + (size_t)h_hyp_off[0] * W,
+                        (size_t)(h_hyp_off[n_hyp] - h_hyp_off[0]) * W, "token embedding");
 }
 
 int rs_bertscore_recall(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off,
@@ -852,9 +911,11 @@ int rs_bertscore_recall(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_
     HIPTRY(hipSetDevice(m->device));
     const int H = m->cfg.hidden;
     const size_t n_tok = (size_t)h_hyp_off[n_hyp];
-    HIPTRY(m->emb.ensure(std::max<size_t>(n_tok, 1) * H * 2));
+    const bool two = m->kx == 3;                 // fp16x3: two-part embeddings, split-operand cosines
+    const int COLS = bertscore_cols(two);
+    HIPTRY(m->emb.ensure(std::max<size_t>(n_tok, 1) * H * 2 * (two ? 2 : 1)));
     if (int r = rs_token_embed(m, d_tok, h_hyp_off, n_hyp, m->emb.p, stream)) return r;
-    // plan: runs of whole ref hypotheses fitting one 64-column tile (a longer one alone)
+    // plan: runs of whole ref hypotheses fitting one COLS-column tile (a longer one alone)
     std::vector<int> items;
     std::vector<long long> moff(n_utt + 1, 0);
     for (int u = 0; u < n_utt; ++u) {
@@ -862,7 +923,7 @@ int rs_bertscore_recall(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_
         moff[u + 1] = moff[u] + (long long)n * n;
         for (int j = 0; j < n;) {
             int j1 = j + 1, cols = h_hyp_off[h0 + j + 1] - h_hyp_off[h0 + j];
-            while (cols <= 64 && j1 < n && cols + h_hyp_off[h0 + j1 + 1] - h_hyp_off[h0 + j1] <= 64) {
+            while (cols <= COLS && j1 < n && cols + h_hyp_off[h0 + j1 + 1] - h_hyp_off[h0 + j1] <= COLS) {
                 cols += h_hyp_off[h0 + j1 + 1] - h_hyp_off[h0 + j1];
                 ++j1;
             }
@@ -894,7 +955,7 @@ int rs_bertscore_recall(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_
     int* d = m->plan.as<int>();
     ProfScope ps(m, st, RS_K_OTHER, 0);
     HIPTRY(launch_bertscore_recall(m->emb.as<f16>(), H, d + w_items + w_moff, d + w_items + w_moff + n_hyp + 1,
-                                   (const long long*)(d + w_items), (const int4*)d, n_items, d_rmat, d_rmat0, st));
+                                   (const long long*)(d + w_items), (const int4*)d, n_items, d_rmat, d_rmat0, st, two));
     return RS_OK;
 }
 
@@ -922,10 +983,11 @@ void rs_model_destroy(rs_model* m) {
     for (void* p : m->allocs) (void)hipFree(p);
     for (DevBuf* b : {&m->xst, &m->xst1, &m->h16, &m->t32, &m->qkv, &m->ctx, &m->inter, &m->ctxq, &m->resq,
                       &m->tq32, &m->hq32, &m->hq16, &m->interq, &m->lab, &m->llog, &m->part,
-                      &m->rowlp_tmp, &m->meta, &m->hypoff, &m->emb, &m->plan})
+                      &m->rowlp_tmp, &m->meta, &m->hypoff, &m->emb, &m->plan, &m->flag})
         b->release();
     if (m->pinned) (void)hipHostFree(m->pinned);
     if (m->pinned_plan) (void)hipHostFree(m->pinned_plan);
+    if (m->pinned_flag) (void)hipHostFree(m->pinned_flag);
     if (m->plan_done) (void)hipEventDestroy(m->plan_done);
     if (m->upload_done) (void)hipEventDestroy(m->upload_done);
     for (hipEvent_t e : m->ev_pool) (void)hipEventDestroy(e);

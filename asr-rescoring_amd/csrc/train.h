@@ -11,21 +11,70 @@
 //   MD alone has weight 1; w = md_loss_weight.
 #pragma once
 #include <hip/hip_runtime.h>
+#include <stdint.h>
 #include "../../include/rescore.h"
 
+// Dropout of BERT's train mode (modeling_bert.py: BertEmbeddings.dropout after the LayerNorm,
+// the attention-probability dropout, BertSelfOutput / BertOutput dropout on the dense output
+// before the residual add), inverted scaling x * 1/(1-p) on kept elements.  The keep bit of
+// element e of site `site` in dropout step `step` is a counter-based draw,
+//   keep = Philox4x32-10(counter = (e_lo, e_hi, site, 0), key = (seed, step)).word0 >= thresh,
+//   thresh = p * 2^32,
+// so no mask is stored: the backward recomputes the same bits, and a step is bitwise
+// reproducible.  Sites: 0 = embeddings; layer l: 1 + 3l attention probabilities (element =
+// its index in the saved-P layout), 2 + 3l self-output, 3 + 3l output (element = row * H + c).
+// thresh == 0: off (p = 0, the fixture-pinned mode).
+struct TrDrop {
+    uint32_t seed = 0, step = 0, site = 0, thresh = 0;
+    float scale = 1.f;
+};
+
+__host__ __device__ inline uint32_t tr_philox_w0(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                                                 uint32_t k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+        const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0, h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+        c0 = h1 ^ c1 ^ k0;
+        c1 = l1;
+        c2 = h0 ^ c3 ^ k1;
+        c3 = l0;
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c0;
+}
+
+__host__ __device__ inline bool tr_keep(const TrDrop& d, unsigned long long e) {
+    return tr_philox_w0((uint32_t)e, (uint32_t)(e >> 32), d.site, 0u, d.seed, d.step) >= d.thresh;
+}
+
+__host__ __device__ inline float tr_drop(const TrDrop& d, unsigned long long e, float x) {
+    if (d.thresh == 0) return x;
+    return tr_keep(d, e) ? x * d.scale : 0.f;
+}
+
+// dst[e] = drop(src[e]) over n elements (dst may alias src)
+hipError_t tr_dropout(float* dst, const float* src, long long n, const TrDrop& d, hipStream_t s);
+// keep[e] = the keep bit of element e (test / export entry, rs_dropout_keep)
+hipError_t tr_dropout_keep(uint8_t* keep, long long n, const TrDrop& d, hipStream_t s);
+
+// h0 = drop(LN(x0)) (site 0); x0 and its statistics saved pre-dropout
 hipError_t tr_embed_ln(const int* row_tok, const int* row_pos, int M, int vocab, const float* word,
                        const float* pos, const float* type0, const float* g, const float* b, float eps, int H,
-                       float* x0, float2* st, float* h0, hipStream_t s);
+                       float* x0, float2* st, float* h0, hipStream_t s, const TrDrop& d = TrDrop());
+// y <- drop(y + bias) + res (saved), h = LN(y); bias == nullptr: plain LN of y (no dropout)
 hipError_t tr_bias_res_ln(float* y, const float* bias, const float* res, int M, const float* g, const float* b,
-                          float eps, int H, float2* st, float* h, hipStream_t s);
+                          float eps, int H, float2* st, float* h, hipStream_t s, const TrDrop& d = TrDrop());
 hipError_t tr_bias_gelu(float* pre, const float* bias, float* act, int M, int N, hipStream_t s);
 hipError_t tr_gelu_bwd(float* d, const float* pre, long long n, hipStream_t s);
 hipError_t tr_bias(float* y, const float* bias, int M, int N, hipStream_t s);
 // klen (nullable): sequence s attends to its first klen[s] tokens only (padded-batch rows)
+// P saved before dropout; ctx = drop(P) V
 hipError_t tr_attn_fwd(const float* qkv, const int* seq_off, const int* klen, const long long* pofs, int S,
-                       int tmax, int H, int heads, float* P, float* ctx, hipStream_t s);
+                       int tmax, int H, int heads, float* P, float* ctx, hipStream_t s, const TrDrop& d = TrDrop());
 hipError_t tr_attn_bwd(const float* qkv, const float* P, const float* dctx, const int* seq_off, const long long* pofs,
-                       int S, int tmax, int H, int heads, float* dqkv, hipStream_t s);
+                       int S, int tmax, int H, int heads, float* dqkv, hipStream_t s, const TrDrop& d = TrDrop());
 hipError_t tr_ln_bwd(const float* dy, const float* x, const float2* st, const float* g, float* dx, int M, int H,
                      hipStream_t s);
 size_t tr_colsum_scratch(int M, int N);

@@ -9,7 +9,10 @@
 // the three HF tensors.  GEMMs: tr_sgemm (k_sgemm.hip: f32-input MFMA, exact fp32, split-K
 // through an ordered workspace sum — deterministic); RS_TRAIN_ROCBLAS=1 routes them to rocBLAS
 // sgemm instead (atomics disabled), kept as the timing / numerics baseline.
-// All other ops: k_train.hip.  Dropout is not applied (p = 0).
+// All other ops: k_train.hip.  Dropout (BERT's train mode, train.h TrDrop): hidden dropout after
+// the embedding LayerNorm and on both residual branches, attention-probability dropout; the keep
+// bits are counter-based draws keyed by (dropout_seed, the trainer's dropout-step counter), so a
+// step is bitwise reproducible and the backward recomputes the mask.
 #include <algorithm>
 #include <map>
 #include <string>
@@ -81,6 +84,7 @@ struct rs_trainer {
     Buf P, G, M1, V1;       // parameters, gradients, Adam moments
     Buf act, grad, meta, small, ws;   // ws: split-K partials of tr_sgemm
     long long step = 0;
+    uint32_t drop_step = 0;         // dropout-step counter (key of the next dropout-active step)
     std::vector<int> h_tok, h_meta;
 };
 
@@ -315,7 +319,35 @@ struct StepCtx {
     // MLM head (RS_HEAD_MLM): transform pre-GELU / GELU out (pre-LN) / LN out, stats, logits
     float *tpre = nullptr, *tx = nullptr, *th = nullptr, *logits = nullptr;
     float2* tst = nullptr;
+    // dropout of this step (train mode: update >= 0 and p > 0)
+    uint32_t seed = 0, dstep = 0, th_hidden = 0, th_attn = 0;
+    float sc_hidden = 1.f, sc_attn = 1.f;
+    TrDrop drop(uint32_t site, bool attn) const {
+        TrDrop d;
+        d.seed = seed;
+        d.step = dstep;
+        d.site = site;
+        d.thresh = attn ? th_attn : th_hidden;
+        d.scale = attn ? sc_attn : sc_hidden;
+        return d;
+    }
 };
+
+uint32_t drop_thresh(float p) { return p <= 0.f ? 0u : (uint32_t)std::min(4294967295.0, (double)p * 4294967296.0); }
+
+// train mode (the reference's model.train() under grad_update) with p > 0: this step's key
+int set_dropout(StepCtx& c, const rs_train_opts* o) {
+    if (!(o->hidden_dropout >= 0.f && o->hidden_dropout < 1.f && o->attn_dropout >= 0.f && o->attn_dropout < 1.f))
+        return rs_fail(RS_EARG, "dropout probabilities must be in [0, 1)");
+    if (o->update < 0 || (o->hidden_dropout == 0.f && o->attn_dropout == 0.f)) return RS_OK;   // eval mode
+    c.seed = o->dropout_seed;
+    c.dstep = c.t->drop_step++;
+    c.th_hidden = drop_thresh(o->hidden_dropout);
+    c.th_attn = drop_thresh(o->attn_dropout);
+    c.sc_hidden = (float)(1.0 / (1.0 - (double)o->hidden_dropout));
+    c.sc_attn = (float)(1.0 / (1.0 - (double)o->attn_dropout));
+    return RS_OK;
+}
 
 // host metadata + buffers.  aux: extra int32 array uploaded with the metadata (utt_off);
 // h_klen (nullable): per-sequence key lengths (padded-batch rows, rs_train_step_mlm).
@@ -456,21 +488,22 @@ int encoder_forward(StepCtx& c) {
     float* Pm = t->P.f();
     hipStream_t st = c.st;
     TRY_HIP(tr_embed_ln(c.dm + c.i_tok, c.dm + c.i_pos, M, cf.vocab, Pm + t->o_word, Pm + t->o_pos, Pm + t->o_type,
-                        Pm + t->o_eg, Pm + t->o_eb, cf.ln_eps, H, c.x0, c.st0, c.la[0].hin, st));
+                        Pm + t->o_eg, Pm + t->o_eb, cf.ln_eps, H, c.x0, c.st0, c.la[0].hin, st, c.drop(0, false)));
     for (int l = 0; l < cf.layers; ++l) {
         const TLayer& L = t->lay[l];
         StepCtx::LA& a = c.la[l];
         RS_TRY(gemm_nt(t, st, M, 3 * H, H, a.hin, Pm + L.wqkv, a.qkv, 0.f));
         TRY_HIP(tr_bias(a.qkv, Pm + L.bqkv, M, 3 * H, st));
         TRY_HIP(tr_attn_fwd(a.qkv, c.seq, c.i_klen ? c.dm + c.i_klen : nullptr, c.pofs, c.S, c.tmax, H, nh, a.P,
-                            a.ctx, st));
+                            a.ctx, st, c.drop(1 + 3 * l, true)));
         RS_TRY(gemm_nt(t, st, M, H, H, a.ctx, Pm + L.wo, a.x1, 0.f));
-        TRY_HIP(tr_bias_res_ln(a.x1, Pm + L.bo, a.hin, M, Pm + L.g1, Pm + L.be1, cf.ln_eps, H, a.st1, a.h1, st));
+        TRY_HIP(tr_bias_res_ln(a.x1, Pm + L.bo, a.hin, M, Pm + L.g1, Pm + L.be1, cf.ln_eps, H, a.st1, a.h1, st,
+                               c.drop(2 + 3 * l, false)));
         RS_TRY(gemm_nt(t, st, M, F, H, a.h1, Pm + L.w1, a.pre, 0.f));
         TRY_HIP(tr_bias_gelu(a.pre, Pm + L.b1, a.act, M, F, st));
         RS_TRY(gemm_nt(t, st, M, H, F, a.act, Pm + L.w2, a.x2, 0.f));
         TRY_HIP(tr_bias_res_ln(a.x2, Pm + L.b2, a.h1, M, Pm + L.g2, Pm + L.be2, cf.ln_eps, H, a.st2,
-                               c.la[l + 1].hin, st));
+                               c.la[l + 1].hin, st, c.drop(3 + 3 * l, false)));
     }
     return RS_OK;
 }
@@ -491,9 +524,16 @@ int encoder_backward(StepCtx& c) {
         TRY_HIP(tr_colsum(dA, a.x2, a.st2, M, H, 1, part, Gm + L.g2, 0, st));
         TRY_HIP(tr_colsum(dA, nullptr, nullptr, M, H, 0, part, Gm + L.be2, 0, st));
         TRY_HIP(tr_ln_bwd(dA, a.x2, a.st2, Pm + L.g2, dB, M, H, st));              // dB = dx2
-        TRY_HIP(tr_colsum(dB, nullptr, nullptr, M, H, 0, part, Gm + L.b2, 0, st));
-        RS_TRY(gemm_tn(t, st, M, H, F, dB, a.act, Gm + L.w2, 0.f));
-        RS_TRY(gemm_nn(t, st, M, H, F, dB, Pm + L.w2, dF, 0.f));                    // d act
+        // BertOutput dropout: the dense branch sees dx2 * mask * scale (in the free dQKV
+        // buffer), the residual branch dx2 itself (dB, copied into dA below)
+        const float* dBo = dB;
+        if (c.th_hidden) {
+            TRY_HIP(tr_dropout(dQKV, dB, (long long)MH, c.drop(3 + 3 * l, false), st));
+            dBo = dQKV;
+        }
+        TRY_HIP(tr_colsum(dBo, nullptr, nullptr, M, H, 0, part, Gm + L.b2, 0, st));
+        RS_TRY(gemm_tn(t, st, M, H, F, dBo, a.act, Gm + L.w2, 0.f));
+        RS_TRY(gemm_nn(t, st, M, H, F, dBo, Pm + L.w2, dF, 0.f));                   // d act
         TRY_HIP(tr_gelu_bwd(dF, a.pre, (long long)MF, st));                         // d pre
         TRY_HIP(tr_colsum(dF, nullptr, nullptr, M, F, 0, part, Gm + L.b1, 0, st));
         RS_TRY(gemm_tn(t, st, M, F, H, dF, a.h1, Gm + L.w1, 0.f));
@@ -502,15 +542,23 @@ int encoder_backward(StepCtx& c) {
         TRY_HIP(tr_colsum(dA, a.x1, a.st1, M, H, 1, part, Gm + L.g1, 0, st));
         TRY_HIP(tr_colsum(dA, nullptr, nullptr, M, H, 0, part, Gm + L.be1, 0, st));
         TRY_HIP(tr_ln_bwd(dA, a.x1, a.st1, Pm + L.g1, dB, M, H, st));              // dB = dx1
-        TRY_HIP(tr_colsum(dB, nullptr, nullptr, M, H, 0, part, Gm + L.bo, 0, st));
-        RS_TRY(gemm_tn(t, st, M, H, H, dB, a.ctx, Gm + L.wo, 0.f));
-        RS_TRY(gemm_nn(t, st, M, H, H, dB, Pm + L.wo, dA, 0.f));                     // dA = d ctx
-        TRY_HIP(tr_attn_bwd(a.qkv, a.P, dA, c.seq, c.pofs, c.S, c.tmax, H, nh, dQKV, st));
+        // BertSelfOutput dropout: masked copy for the dense branch in the free dF buffer
+        const float* dBs = dB;
+        if (c.th_hidden) {
+            TRY_HIP(tr_dropout(dF, dB, (long long)MH, c.drop(2 + 3 * l, false), st));
+            dBs = dF;
+        }
+        TRY_HIP(tr_colsum(dBs, nullptr, nullptr, M, H, 0, part, Gm + L.bo, 0, st));
+        RS_TRY(gemm_tn(t, st, M, H, H, dBs, a.ctx, Gm + L.wo, 0.f));
+        RS_TRY(gemm_nn(t, st, M, H, H, dBs, Pm + L.wo, dA, 0.f));                    // dA = d ctx
+        TRY_HIP(tr_attn_bwd(a.qkv, a.P, dA, c.seq, c.pofs, c.S, c.tmax, H, nh, dQKV, st, c.drop(1 + 3 * l, true)));
         TRY_HIP(tr_colsum(dQKV, nullptr, nullptr, M, 3 * H, 0, part, Gm + L.bqkv, 0, st));
         RS_TRY(gemm_tn(t, st, M, 3 * H, H, dQKV, a.hin, Gm + L.wqkv, 0.f));
         TRY_HIP(hipMemcpyAsync(dA, dB, MH * 4, hipMemcpyDeviceToDevice, st));      // residual
         RS_TRY(gemm_nn(t, st, M, 3 * H, H, dQKV, Pm + L.wqkv, dA, 1.f));             // dA = d h_in
     }
+    // embedding dropout: d(LN output) = d h0 * mask * scale
+    if (c.th_hidden) TRY_HIP(tr_dropout(dA, dA, (long long)MH, c.drop(0, false), st));
     TRY_HIP(tr_colsum(dA, c.x0, c.st0, M, H, 1, part, Gm + t->o_eg, 0, st));
     TRY_HIP(tr_colsum(dA, nullptr, nullptr, M, H, 0, part, Gm + t->o_eb, 0, st));
     TRY_HIP(tr_ln_bwd(dA, c.x0, c.st0, Pm + t->o_eg, dB, M, H, st));                // dB = dx0
@@ -553,6 +601,7 @@ int rs_train_step_cls(rs_trainer* t, const int32_t* d_tok, const int32_t* h_hyp_
     StepCtx c;
     c.t = t;
     c.st = (hipStream_t)stream;
+    if (int r = set_dropout(c, o)) return r;
     if (int r = prepare(c, d_tok, h_hyp_off, n_hyp, std::vector<int>(h_utt_off, h_utt_off + n_utt + 1))) return r;
     if (int r = encoder_forward(c)) return r;
     const int H = t->cfg.hidden, S = c.S;
@@ -589,6 +638,7 @@ int rs_train_step_mlm(rs_trainer* t, const int32_t* d_ids, const int32_t* h_seq_
     StepCtx c;
     c.t = t;
     c.st = (hipStream_t)stream;
+    if (int r = set_dropout(c, o)) return r;
     if (int r = prepare(c, d_ids, h_seq_off, n_seq, {}, h_key_len)) return r;
     if (int r = encoder_forward(c)) return r;
     const rs_bert_cfg& cf = t->cfg;
@@ -635,6 +685,26 @@ int rs_trainer_reset_optimizer(rs_trainer* t) {
     TRY_HIP(hipMemset(t->M1.p, 0, t->n_params * 4));
     TRY_HIP(hipMemset(t->V1.p, 0, t->n_params * 4));
     t->step = 0;
+    return RS_OK;
+}
+
+int64_t rs_trainer_dropout_step(const rs_trainer* t) { return t ? (int64_t)t->drop_step : -1; }
+
+int rs_trainer_set_dropout_step(rs_trainer* t, int64_t step) {
+    if (!t || step < 0 || step > 0xFFFFFFFFll) return rs_fail(RS_EARG, "bad argument");
+    t->drop_step = (uint32_t)step;
+    return RS_OK;
+}
+
+int rs_dropout_keep(uint32_t seed, uint32_t step, uint32_t site, float p, int64_t n, uint8_t* d_keep, void* stream) {
+    if (n < 0 || (n > 0 && !d_keep)) return rs_fail(RS_EARG, "null argument");
+    if (!(p >= 0.f && p < 1.f)) return rs_fail(RS_EARG, "p must be in [0, 1)");
+    TrDrop d;
+    d.seed = seed;
+    d.step = step;
+    d.site = site;
+    d.thresh = drop_thresh(p);
+    TRY_HIP(tr_dropout_keep(d_keep, (long long)n, d, (hipStream_t)stream));
     return RS_OK;
 }
 

@@ -82,11 +82,26 @@ def shard_of(nb: NBest, world: int, rank: int, mode: str = "pll") -> Tuple[int, 
     return plan_shards(utterance_costs(nb, mode), world)[rank]
 
 
+def exchange_device(backend, lm_device, device=None) -> torch.device:
+    """Where the (am, lm) block must live for the all-gather: CPU under gloo; under nccl
+    (RCCL) always this rank's GPU — also on a rank whose shard is empty, where the scorer
+    never ran and there is no device tensor to take it from (an empty CPU block would make
+    RCCL raise or hang the group)."""
+    if backend == "gloo":
+        return torch.device("cpu")
+    if device is not None:
+        return torch.device(device)
+    if backend is not None:
+        return torch.device("cuda", torch.cuda.current_device())
+    return torch.device(lm_device)
+
+
 def score_sharded(nb: NBest, score_fn, mode: str = "pll", device=None, group=None) -> torch.Tensor:
     """Utterance-sharded scoring with one all-gather (MLM_PLL/main.py:164-203 on
     N ranks).  ``score_fn(sub_nbest) -> lm [H_local]`` scores this rank's utterances (the HIP
     scorer in the product; any callable in tests).  Returns the (am, lm) float64 block
-    [2, H] of EVERY hypothesis, in global order, on every rank."""
+    [2, H] of EVERY hypothesis, in global order, on every rank.  A rank may own no
+    utterance (fewer utterances than ranks, or a few costly ones taking the prefix sum)."""
     world = dist.get_world_size(group) if dist.is_initialized() else 1
     rank = dist.get_rank(group) if dist.is_initialized() else 0
     parts = plan_shards(utterance_costs(nb, mode), world)
@@ -95,9 +110,7 @@ def score_sharded(nb: NBest, score_fn, mode: str = "pll", device=None, group=Non
     h0, h1 = int(nb.utt_off[u0]), int(nb.utt_off[u1])
     lm = score_fn(sub) if h1 > h0 else torch.zeros(0, dtype=torch.float64)
     lm = torch.as_tensor(lm).to(torch.float64)
-    dev = lm.device if device is None else torch.device(device)
-    if world > 1 and dist.get_backend(group) == "gloo":
-        dev = torch.device("cpu")
+    dev = exchange_device(dist.get_backend(group) if world > 1 else None, lm.device, device)
     am = torch.from_numpy(np.ascontiguousarray(nb.am[h0:h1], np.float64)).to(dev)
     local = torch.stack([am, lm.to(dev)])
     if world == 1:

@@ -14,8 +14,15 @@ consecutive hypotheses (the reference's ``reshape(-1, n_best)``; ``reference_gro
   MD_MWED  sum_g KL(softmax(cer) || softmax((s + am) / T)) + md_loss_weight * MD,
            T = sum(s + am) / sum(cer) per group, differentiated through
 Pinned against the reference's own training loop (tests/golden/make_golden_train.py, F6/F7:
-losses, dev scores and parameter updates after two epochs).  Dropout is not applied (the
-fixtures switch it off through the model config; the reference's p = 0.1 mask is RNG-bound).
+losses, dev scores and parameter updates after two epochs, with dropout off as the fixtures
+run it).  Dropout: the reference trains under ``model.train()`` with BertConfig's defaults
+(hidden_dropout_prob = attention_probs_dropout_prob = 0.1), and so do these trainers by default
+— hidden dropout after the embedding LayerNorm and on both residual branches, dropout on the
+attention probabilities, inverted scaling, on every training step (not on the dev-loss pass).
+The masks are counter-based draws (Philox4x32-10 keyed by ``dropout_seed`` and the trainer's
+dropout-step counter, ``csrc/train.h``): bitwise reproducible, and exportable
+(``dropout_keep``) so the tests feed the very same masks to the CPU oracle.  torch's RNG stream
+itself cannot be matched, so a reference run with dropout is matched in distribution, not bits.
 
 ``MLMTrainer`` (BertForMaskedLM, decoder tied to the word embeddings) takes the reference's
 padded batches (``pad_rows``: collate of MLM_PLL/main.py:28-54 — ids and labels padded with
@@ -68,7 +75,8 @@ class _Trainer:
 
     def __init__(self, weights: Dict[str, np.ndarray], shape: BertShape = BERT_BASE, device=0,
                  method: str = "MD", md_loss_weight: float = 1.0, lr: float = 1e-5, betas=(0.9, 0.999),
-                 eps: float = 1e-8, weight_decay: float = 0.01):
+                 eps: float = 1e-8, weight_decay: float = 0.01, hidden_dropout: float = 0.1,
+                 attn_dropout: float = 0.1, dropout_seed: int = 0):
         if not torch.cuda.is_available():
             raise RuntimeError("librescore needs a HIP GPU (no CPU fallback)")
         self.lib = _lib.load()
@@ -77,8 +85,11 @@ class _Trainer:
         torch.cuda.set_device(self.device)
         if method not in _lib.RS_LOSS:
             raise ValueError(f"unknown method {method!r} (MD, MD_MWER, MD_MWED)")
+        self.method = method
+        if not (0.0 <= hidden_dropout < 1.0 and 0.0 <= attn_dropout < 1.0):
+            raise ValueError("dropout probabilities must be in [0, 1)")
         self.opts = _lib.RsTrainOpts(_lib.RS_LOSS[method], md_loss_weight, lr, betas[0], betas[1], eps,
-                                     weight_decay, 1)
+                                     weight_decay, 1, hidden_dropout, attn_dropout, int(dropout_seed) & 0xFFFFFFFF)
         self.shapes = param_shapes(shape, self.HEAD)
         self.extra = {k: np.asarray(v) for k, v in weights.items()
                       if k.startswith("bert.pooler.") or (self.HEAD == "mlm" and k.startswith("cls.predictions.decoder."))}
@@ -110,6 +121,13 @@ class _Trainer:
             self.close()
         except Exception:
             pass
+
+    def dropout_step(self) -> int:
+        """Key (dropout-step counter) of the next training step that applies dropout."""
+        return int(self.lib.rs_trainer_dropout_step(self.handle))
+
+    def set_dropout_step(self, step: int) -> None:
+        _lib.check(self.lib.rs_trainer_set_dropout_step(self.handle, int(step)))
 
     def reset_optimizer(self):
         """A fresh AdamW (moments and step count zeroed): the reference builds its optimizer
@@ -236,9 +254,11 @@ def rescorebert_epoch(tr: RescoreBertTrainer, tokens, hyp_off, target, am, cer, 
                       update=True) -> float:
     """One pass of RescoreBert/main.py:82-163 run_one_epoch(train=True) over the hypotheses in
     order: batches of ``batch_size * n_best`` rows (set_dataloader :71-79, shuffle False),
-    groups of ``n_best`` (``reference_groups``); ``update`` True = grad_update (the caller
-    resets AdamW first, as the reference builds it per call), "loss" = the dev pass.
-    Returns the epoch loss (mean of the batch losses)."""
+    groups of ``n_best`` (``reference_groups``) for MD_MWER / MD_MWED, which reshape the batch
+    to (-1, n_best) (RescoreBert/main.py:116,132); MD is a plain MSELoss(sum) over the batch
+    (:104-110) and takes any batch, ragged last batch and short N-best lists included;
+    ``update`` True = grad_update (the caller resets AdamW first, as the reference builds it per
+    call), "loss" = the dev pass.  Returns the epoch loss (mean of the batch losses)."""
     hoff = np.asarray(hyp_off, np.int64)
     n = len(hoff) - 1
     rows = batch_size * n_best
@@ -246,8 +266,9 @@ def rescorebert_epoch(tr: RescoreBertTrainer, tokens, hyp_off, target, am, cer, 
     for b0 in range(0, n, rows):
         b1 = min(n, b0 + rows)
         t0, t1 = int(hoff[b0]), int(hoff[b1])
+        groups = np.array([0, b1 - b0], np.int32) if tr.method == "MD" else reference_groups(b1 - b0, n_best)
         loss, _ = tr.step(np.asarray(tokens[t0:t1]), (hoff[b0:b1 + 1] - t0).astype(np.int32),
-                          reference_groups(b1 - b0, n_best), target[b0:b1], am[b0:b1], cer[b0:b1], update=update)
+                          groups, target[b0:b1], am[b0:b1], cer[b0:b1], update=update)
         tot += loss
         nb += 1
     return tot / max(nb, 1)
@@ -266,3 +287,16 @@ def mlm_epoch(tr: MLMTrainer, seqs: Sequence[Sequence[int]], labels: Sequence[Se
         tot += tr.step(ids, off, lab, klen, update=update)
         nb += 1
     return tot / max(nb, 1)
+
+
+def dropout_keep(seed: int, step: int, site: int, p: float, n: int, device=0) -> np.ndarray:
+    """The keep bits (uint8 [n]) the trainer's kernels use for element e of dropout site
+    ``site`` in dropout step ``step`` (``csrc/train.h``: 0 = embeddings; layer l: 1 + 3l
+    attention probabilities in the saved-P layout, 2 + 3l self-output, 3 + 3l output, element
+    = row * hidden + column), generated by the same device function."""
+    lib = _lib.load()
+    dev = torch.device("cuda", device if isinstance(device, int) else torch.device(device).index)
+    out = torch.empty(max(int(n), 1), dtype=torch.uint8, device=dev)
+    _lib.check(lib.rs_dropout_keep(int(seed) & 0xFFFFFFFF, int(step) & 0xFFFFFFFF, int(site), float(p), int(n),
+                                   _lib.ptr(out), _lib.stream_ptr(dev)))
+    return out[:int(n)].cpu().numpy()

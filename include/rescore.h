@@ -11,7 +11,8 @@
  *   - d_* pointers are device memory owned by the caller (e.g. the PyTorch caching
  *     allocator); h_* pointers are host memory read during the call only.
  *   - stream is a hipStream_t (torch.cuda.current_stream().cuda_stream); every call is
- *     asynchronous on it unless stated.  No C++ exception crosses the ABI.
+ *     asynchronous on it unless stated (the scoring calls synchronise at their end: range
+ *     guard below).  No C++ exception crosses the ABI.
  *   - return 0 on success, a negative RS_E* code on failure; rs_last_error() gives a
  *     thread-local message.
  *   - A model handle is bound to one device and must not be used by two host threads
@@ -63,11 +64,15 @@ typedef struct rs_bert_cfg {
     int32_t precision;    /* RS_PREC_FP16 or RS_PREC_FP16X3 */
 } rs_bert_cfg;
 
-/* GEMM operand precision.  FP16: fp16 MFMA inputs, fp32 accumulation (MLM_PLL default:
- * per-row log-probs within 1e-4 relative of fp32).  FP16X3: each fp32 operand is split
- * into fp16 hi + lo and the three significant products are accumulated by the same MFMA
- * kernel along a 3x longer K (fp32-level accuracy at 1/3 the fp16 rate; RescoreBert
- * default, whose O(1) CLS scores need it for 1e-3 relative). */
+/* GEMM operand precision.  FP16X3 (the default of every scorer): each fp32 operand x is
+ * split into fp16 hi + lo (lo scaled by 64) and the three significant products
+ * A_hi.W_hi + A_hi.W_lo + A_lo.W_hi are accumulated in fp32 on the fp16 MFMA — by the
+ * split-operand kernel from two-part images, the third product's factors formed in registers
+ * (fp32-level accuracy: PLL ~1e-7 relative of the fp32 reference, 3 MFMA products per
+ * algorithmic one).  FP16: fp16 MFMA inputs, fp32 accumulation (opt-in reduced-precision
+ * mode: per-row log-probs within ~1e-4 relative).  Both modes hold operands in fp16 images,
+ * so |x| <= 65504: weights beyond it fail rs_model_finalize, activations beyond it make the
+ * scoring call fail with RS_EUNSUP (range guard, below). */
 #define RS_PREC_FP16 0
 #define RS_PREC_FP16X3 1
 
@@ -92,7 +97,13 @@ int rs_model_finalize(rs_model* m);
  * (>= 512).  Optional: scoring calls reserve a default on first use. */
 int rs_model_reserve(rs_model* m, int64_t max_rows);
 
-/* MLM_PLL scoring (MLM_PLL/preprocess.py:9-30 + MLM_PLL/main.py:83-107):
+/* Range guard of the scoring calls (rs_pll_score, rs_masked_logprob, rs_cls_score,
+ * rs_token_embed, rs_bertscore_recall): after the last launch the call checks its outputs
+ * for non-finite values (an operand image that overflowed fp16 turns every dependent score
+ * into inf / NaN), synchronises `stream` and returns RS_EUNSUP with a message instead of
+ * handing back non-finite scores.  These calls therefore return with their work complete.
+ *
+ * MLM_PLL scoring (MLM_PLL/preprocess.py:9-30 + MLM_PLL/main.py:83-107):
  *   d_tok      int32 [h_hyp_off[n_hyp]]  hypotheses as [CLS] w_1..w_L [SEP]
  *   h_hyp_off  int32 [n_hyp + 1]         host offsets into d_tok (T_h = L_h + 2 >= 3)
  *   d_pll      float64 [n_hyp]           sum_p log p(w_p | w_{\p}) accumulated in row
@@ -149,8 +160,10 @@ int rs_pairwise_edit(const int32_t* d_chars, const int32_t* d_str_off, const int
 /* Token embeddings of the BERTScore utility (RMBR/utility_functions.py:9-22 ->
  * bert_score.utils.get_bert_embedding / bert_encode with the model truncated to cfg.layers
  * layers — bert_score uses 8 for bert-base-chinese — and greedy_cos_idf's per-token L2
- * normalisation): d_emb fp16 [hyp_off[n_hyp], hidden], row = token position in d_tok
- * (h_hyp_off: host int32 [n_hyp+1], hypotheses as [CLS] w.. [SEP]). */
+ * normalisation), row = token position in d_tok (h_hyp_off: host int32 [n_hyp+1], hypotheses
+ * as [CLS] w.. [SEP]).  d_emb layout by the model's precision: RS_PREC_FP16X3 — the two-part
+ * image fp16 [hyp_off[n_hyp], 2*hidden], row = [hi | lo*64], e = hi + lo/64 (fp32-class, ~22
+ * bits); RS_PREC_FP16 — fp16 [hyp_off[n_hyp], hidden]. */
 int rs_token_embed(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, int32_t n_hyp,
                    void* d_emb, void* stream);
 
@@ -159,7 +172,9 @@ int rs_token_embed(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, 
  *   d_rmat[mat_off(u) + i*n_u + j] = R(cand = hyp_i, ref = hyp_j),
  *   mat_off(u) = sum_{v<u} n_v^2 (n_u = h_utt_off[u+1] - h_utt_off[u]);
  * P(i|j) = R(j|i), F = 2PR/(P+R).  R = mean over ref j's tokens except [CLS]/[SEP] of the max
- * cosine over all of cand i's tokens; 0 when either hypothesis is empty (T == 2).
+ * cosine over all of cand i's tokens; 0 when either hypothesis is empty (T == 2).  Cosines:
+ * RS_PREC_FP16X3 three fp16 products of the two-part embeddings, fp32 accumulation (fp32-class);
+ * RS_PREC_FP16 one.
  * d_rmat0 (optional, same layout): each maximum taken as max(m, 0) — bert_score's value when
  * the cand is shorter than the longest cand of its pair batch (the padded positions' masked
  * cosine 0 joins the max, bert_score/utils.py greedy_cos_idf); the caller picks R or R0 per
@@ -205,7 +220,13 @@ int rs_align(const int32_t* d_ref, const int32_t* d_ref_off, const int32_t* d_hy
  *   MD_MWER = sum_g sum_i softmax(c_g)_i (cer_i - mean_g cer) + md_loss_weight * MD
  *   MD_MWED = sum_g KL(softmax(cer_g) || softmax(c_g / T_g)) + md_loss_weight * MD,
  *             T_g = sum c_g / sum cer_g (differentiated through), c = s + am.
- * Dropout is not applied (the reference's p = 0.1 mask is RNG-bound). */
+ * Dropout (BERT train mode; the reference trains under model.train(), p = 0.1 by default):
+ * hidden_dropout after the embedding LayerNorm and on the BertSelfOutput / BertOutput dense
+ * outputs, attn_dropout on the attention probabilities, inverted scaling, on steps with
+ * update >= 0 (the dev-loss pass, update = -1, is eval mode).  The keep bits are
+ * counter-based (Philox4x32-10 keyed by dropout_seed and the trainer's dropout-step counter,
+ * rs_trainer_dropout_step), so a step is bitwise reproducible; torch's RNG stream cannot be
+ * matched, and the fixture-pinned runs use p = 0. */
 typedef struct rs_trainer rs_trainer;
 typedef struct rs_train_opts {
     int32_t loss;          /* RS_LOSS_MD / RS_LOSS_MWER / RS_LOSS_MWED */
@@ -213,6 +234,9 @@ typedef struct rs_train_opts {
     float lr, beta1, beta2, eps, weight_decay;   /* torch.optim.AdamW arguments */
     int32_t update;        /* 1: backward + AdamW step; 0: backward only (gradients kept);
                               -1: forward + loss only (the reference's dev-loss pass) */
+    float hidden_dropout;  /* BertConfig.hidden_dropout_prob (0 = off) */
+    float attn_dropout;    /* BertConfig.attention_probs_dropout_prob (0 = off) */
+    uint32_t dropout_seed;
 } rs_train_opts;
 
 /* cfg->heads_mask: RS_HEAD_CLS (RescoreBert) or RS_HEAD_MLM (MLM fine-tuning); shapes as
@@ -241,6 +265,16 @@ int rs_train_step_cls(rs_trainer* t, const int32_t* d_tok, const int32_t* h_hyp_
 int rs_train_step_mlm(rs_trainer* t, const int32_t* d_ids, const int32_t* h_seq_off, int32_t n_seq,
                       const int32_t* h_key_len, const int32_t* d_labels, const rs_train_opts* opts,
                       float* d_loss, void* stream);
+/* The dropout-step counter: the key the next dropout-active step uses (then incremented). */
+int64_t rs_trainer_dropout_step(const rs_trainer* t);
+/* Sets it (0 .. 2^32-1): part of the resume state — the CLI keys each epoch's first step by
+ * the epoch number, so a run resumed at epoch k draws the masks of the straight run. */
+int rs_trainer_set_dropout_step(rs_trainer* t, int64_t step);
+/* d_keep uint8 [n]: the keep bit the trainer's kernels use for element e of dropout site
+ * `site` (0 = embeddings; layer l: 1 + 3l attention probabilities in the saved-P layout,
+ * 2 + 3l self-output, 3 + 3l output, element = row * hidden + column) in dropout step `step`
+ * with probability p.  Test / export entry (masks fed to the CPU oracle). */
+int rs_dropout_keep(uint32_t seed, uint32_t step, uint32_t site, float p, int64_t n, uint8_t* d_keep, void* stream);
 /* Synchronous copies of one parameter / its last gradient (numel must match). */
 int rs_trainer_get_tensor(rs_trainer* t, const char* hf_key, void* host_out, int64_t numel);
 int rs_trainer_get_grad(rs_trainer* t, const char* hf_key, void* host_out, int64_t numel);

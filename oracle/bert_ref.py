@@ -56,8 +56,13 @@ class TorchBert:
                              eps=self.s.ln_eps)
 
     def encoder(self, input_ids: torch.Tensor, attention_mask: torch.Tensor,
-                last_layer_rows: torch.Tensor | None = None) -> torch.Tensor:
-        """input_ids/attention_mask int64 [B, T] → last hidden [B, T, H] (modeling_bert.py:53-351)."""
+                last_layer_rows: torch.Tensor | None = None, drop: dict | None = None) -> torch.Tensor:
+        """input_ids/attention_mask int64 [B, T] → last hidden [B, T, H] (modeling_bert.py:53-351).
+
+        ``drop`` (training with dropout): multipliers (0 or 1/(1-p)) at the places BERT's train
+        mode applies nn.Dropout — "emb" [B, T, H] after the embedding LayerNorm; per layer i
+        ("attn", i) [B, heads, T, T] on the attention probabilities, ("so", i) / ("out", i)
+        [B, T, H] on the BertSelfOutput / BertOutput dense outputs before the residual add."""
         s = self.s
         B, T = input_ids.shape
         pos = torch.arange(T, device=self.device)
@@ -68,6 +73,8 @@ class TorchBert:
              + self.w[e + "token_type_embeddings.weight"][0]
              + self.w[e + "position_embeddings.weight"][pos][None])
         x = self._ln(x, e + "LayerNorm")
+        if drop is not None:
+            x = x * drop["emb"]
         # additive mask: 0 keep, finfo.min drop (transformers bidirectional mask semantics)
         add = (1.0 - attention_mask[:, None, None, :].to(x.dtype)) * torch.finfo(x.dtype).min
         nh, hd = s.heads, s.head_dim
@@ -78,10 +85,18 @@ class TorchBert:
             v = self._lin(x, p + "attention.self.value").view(B, T, nh, hd).transpose(1, 2)
             sc = torch.matmul(q, k.transpose(2, 3)) * (hd ** -0.5) + add
             pr = torch.softmax(sc, dim=-1)
+            if drop is not None:
+                pr = pr * drop[("attn", i)]
             ctx = torch.matmul(pr, v).transpose(1, 2).reshape(B, T, s.hidden)
-            x = self._ln(self._lin(ctx, p + "attention.output.dense") + x, p + "attention.output.LayerNorm")
+            so = self._lin(ctx, p + "attention.output.dense")
+            if drop is not None:
+                so = so * drop[("so", i)]
+            x = self._ln(so + x, p + "attention.output.LayerNorm")
             it = Fn.gelu(self._lin(x, p + "intermediate.dense"))
-            x = self._ln(self._lin(it, p + "output.dense") + x, p + "output.LayerNorm")
+            out = self._lin(it, p + "output.dense")
+            if drop is not None:
+                out = out * drop[("out", i)]
+            x = self._ln(out + x, p + "output.LayerNorm")
         return x
 
     def mlm_logits(self, hidden: torch.Tensor) -> torch.Tensor:

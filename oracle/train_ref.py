@@ -2,7 +2,8 @@
 reference's training steps, used to check the native trainer (train_api.hip).
 
 Model: ``oracle.bert_ref.TorchBert`` (pinned against transformers via the golden fixtures)
-with every parameter a leaf tensor, no dropout.
+with every parameter a leaf tensor; dropout only as explicit multipliers (``drop``: the masks
+the native trainer drew, exported by ``train.dropout_keep`` and laid out by ``padded_drop``).
   * RescoreBert (RescoreBert/main.py:31-79 collate + :98-154 run_one_epoch): a batch is padded
     to its longest hypothesis (pad 0, attention mask), scores are the CLS linear head, and the
     losses are the reference's expressions (``rescorebert_loss``).
@@ -61,20 +62,21 @@ class TorchTrainer:
     def reset_optimizer(self):
         self.opt = torch.optim.AdamW(list(self.model.w.values()), **self.hp)
 
-    def scores(self, seqs: Sequence[Sequence[int]]) -> torch.Tensor:
+    def scores(self, seqs: Sequence[Sequence[int]], drop=None) -> torch.Tensor:
         T = max(len(s) for s in seqs)
         ids = torch.zeros(len(seqs), T, dtype=torch.long)
         am = torch.zeros(len(seqs), T, dtype=torch.long)
         for i, s in enumerate(seqs):
             ids[i, :len(s)] = torch.as_tensor(list(s))
             am[i, :len(s)] = 1
-        return self.model.cls_score(self.model.encoder(ids, am))
+        return self.model.cls_score(self.model.encoder(ids, am, drop=drop))
 
-    def step(self, seqs, target, am=None, cer=None, n_best=1, method="MD", md_loss_weight=1.0, update=True):
+    def step(self, seqs, target, am=None, cer=None, n_best=1, method="MD", md_loss_weight=1.0, update=True,
+             drop=None):
         """update: True (backward + AdamW), False (backward only), "loss" (no backward)."""
         self.opt.zero_grad(set_to_none=False)
         with torch.set_grad_enabled(update != "loss"):
-            sc = self.scores(seqs)
+            sc = self.scores(seqs, drop)
             loss = rescorebert_loss(sc, target, am, cer, n_best, method, md_loss_weight)
             if update != "loss":
                 loss.backward()
@@ -88,7 +90,8 @@ class TorchTrainer:
     def tensor(self, key: str) -> np.ndarray:
         return self.model.w[key].detach().numpy()
 
-    def step_mlm(self, seqs: Sequence[Sequence[int]], labels: Sequence[Sequence[int]], update=True) -> float:
+    def step_mlm(self, seqs: Sequence[Sequence[int]], labels: Sequence[Sequence[int]], update=True,
+                 drop=None) -> float:
         """One reference MLM batch: pad_sequence(ids / labels, 0), attention mask, CE mean over
         all B*T positions (pads included), AdamW."""
         T = max(len(s) for s in seqs)
@@ -101,13 +104,49 @@ class TorchTrainer:
             lab[i, :len(lb)] = torch.as_tensor(np.asarray(lb, np.int64))
         self.opt.zero_grad(set_to_none=False)
         with torch.set_grad_enabled(update != "loss"):
-            logits = self.model.mlm_logits(self.model.encoder(x, am))
+            logits = self.model.mlm_logits(self.model.encoder(x, am, drop=drop))
             loss = torch.nn.functional.cross_entropy(logits.view(-1, logits.shape[-1]), lab.view(-1))
             if update != "loss":
                 loss.backward()
         if update is True:
             self.opt.step()
         return float(loss.detach())
+
+
+def padded_drop(keep_fn, seq_lens: Sequence[int], hidden: int, heads: int, layers: int, p_hidden: float,
+                p_attn: float, T: int | None = None) -> dict:
+    """The native trainer's dropout masks laid out for ``TorchBert.encoder(drop=...)``.
+
+    ``keep_fn(site, n)`` returns the keep bits (uint8 [n]) of a site in the trainer's ragged
+    layout (train.h: site 0 embeddings, layer l 1 + 3l attention probabilities at
+    pofs[s] + h T_s^2 + i T_s + j, 2 + 3l / 3 + 3l the residual branches at row * H + c);
+    rows are the sequences' tokens back to back.  Multipliers: keep / (1 - p) in float32."""
+    lens = [int(x) for x in seq_lens]
+    B, Tm = len(lens), (T or max(lens))
+    offs = np.concatenate([[0], np.cumsum(lens)])
+    M = int(offs[-1])
+    sh = np.float32(1.0 / (1.0 - p_hidden))
+    sa = np.float32(1.0 / (1.0 - p_attn))
+
+    def hid(site):
+        k = keep_fn(site, M * hidden).reshape(M, hidden).astype(np.float32) * sh
+        out = np.ones((B, Tm, hidden), np.float32)
+        for b in range(B):
+            out[b, :lens[b]] = k[offs[b]:offs[b + 1]]
+        return torch.from_numpy(out)
+
+    pofs = np.concatenate([[0], np.cumsum([heads * t * t for t in lens])])
+    drop = {"emb": hid(0)}
+    for i in range(layers):
+        k = keep_fn(1 + 3 * i, int(pofs[-1])).astype(np.float32) * sa
+        a = np.ones((B, heads, Tm, Tm), np.float32)
+        for b in range(B):
+            t = lens[b]
+            a[b, :, :t, :t] = k[pofs[b]:pofs[b + 1]].reshape(heads, t, t)
+        drop[("attn", i)] = torch.from_numpy(a)
+        drop[("so", i)] = hid(2 + 3 * i)
+        drop[("out", i)] = hid(3 + 3 * i)
+    return drop
 
 
 def _split(tokens, hyp_off):

@@ -287,3 +287,36 @@ def test_residual_paths_golden(pll_base16, golden_dir, env, same, monkeypatch):
         assert np.array_equal(pll, base)
     else:
         assert not np.array_equal(pll, base)      # the variant really ran a different path
+
+
+@pytest.mark.parametrize("precision", ["fp16x3", "fp16"])
+def test_fp16_range_guard(w_tiny, precision):
+    """The operand images hold |x| <= 65504 (fp16); the fp32 reference has no such limit.
+    A weight beyond it is refused at finalize; an activation beyond it (the embedding
+    LayerNorm's gamma scaled until its output, the first GEMM operand, crosses 65504) makes
+    the scoring call fail with RS_EUNSUP instead of returning inf / NaN scores.  Just inside
+    the range the same path scores finite."""
+    from asr_rescoring_amd._lib import RescoreError
+    from asr_rescoring_amd.scorer import PLLScorer, RescoreBertScorer
+    nb = D.synthetic_nbest(2, 3, seed=5, vocab=BERT_TINY.vocab, len_lo=3, len_hi=12)
+    w = dict(w_tiny)
+    k = "bert.encoder.layer.0.intermediate.dense.weight"
+    w[k] = w[k].copy()
+    w[k][0, 0] = 1e5
+    with pytest.raises(RescoreError, match="fp16 range"):
+        PLLScorer(w, BERT_TINY, device=0, max_rows=2048, precision=precision)
+    g = "bert.embeddings.LayerNorm.weight"
+    for scale, ok in ((30.0, True), (1e6, False)):
+        w = dict(w_tiny)
+        w[g] = w_tiny[g] * scale
+        for cls in (PLLScorer, RescoreBertScorer):
+            s = cls(w, BERT_TINY, device=0, max_rows=2048, precision=precision)
+            try:
+                if ok:
+                    out = s.score_nbest(nb.tokens, nb.hyp_off).cpu().numpy()
+                    assert np.isfinite(out).all()
+                else:
+                    with pytest.raises(RescoreError, match="non-finite"):
+                        s.score_nbest(nb.tokens, nb.hyp_off)
+            finally:
+                s.close()

@@ -1,13 +1,16 @@
 """GPU parity at the shapes of BASELINE.json's configs (C2, C3, C5), and the reference's
 own drop-in entry points on the reference's own input formats.
 
-* C3 (MLM_PLL full PLL, bert-base, N=50, L ~ U{24..40}): 2 utterances x 50 hypotheses,
+* C3 (MLM_PLL full PLL, bert-base, N=50, L ~ U{24..40}): 6 utterances x 50 hypotheses,
   HIP vs the oracle's fp32 restatement of run_one_epoch (MLM_PLL/main.py:73-114): every
   masked row and every PLL within 1e-3 relative; then the 101-weight fusion sweep of
   rescore.py:25-58 fed the ORACLE's lm and fed the HIP lm gives the same argmax for every
   weight, the same best weight and the same CER (the north-star rerank-index check).  The
   "hard" synthetic variant (reference hypothesis not first, AM unsorted) makes the argmax
   move with the weight.
+* C4 (MLM_PLL, N=100, real alfred lengths): 2 utterances x 100 plus a T > 64 utterance in one
+  launch chunk (mixed attention kernels), rows / PLL / rerank argmax vs the oracle, and
+  ``cli mlm_pll`` as 1 rank vs 2 ranks bitwise.
 * C2 (RescoreBert, N=50): 10 utterances x 50 hypotheses vs the oracle's RescoreBert batches.
 * C5 (RMBR CER utility + fusion, N=100, real lengths): 3 utterances x 100 hypotheses, the
   pairwise edit matrices, MBR scores for several k (float32, bit-exact) and the fusion argmax
@@ -64,7 +67,7 @@ def test_c3_shape_pll_rows_and_rerank(w_base, oracle_model):
     from asr_rescoring_amd import rerank
     from oracle import rescore_ref as RR
     from oracle.bert_ref import pll_reference_pattern
-    nb = D.synthetic_nbest(2, 50, seed=31, hard=True)
+    nb = D.synthetic_nbest(6, 50, seed=31, hard=True)
     s = PLLScorer(w_base, BERT_BASE, device=0, max_rows=65536)
     try:
         pll, rows = s.score_nbest(nb.tokens, nb.hyp_off, return_rows=True)
@@ -223,3 +226,99 @@ def test_cli_rescorebert_vs_f2(golden_dir, tmp_path):
     got = np.array([v for u in lm.values() for v in u.values()], np.float64)
     err = np.abs(got - g["cls"])
     assert (err <= np.maximum(REL * np.abs(g["cls"]), 1e-4)).all(), err.max()
+
+
+def _concat(parts):
+    """One NBest of several (utterances in order)."""
+    toks, hoff, uoff, am, refs, uids, hids = [], [0], [0], [], [], [], []
+    for nb in parts:
+        toks.append(nb.tokens)
+        hoff.extend((np.asarray(nb.hyp_off[1:], np.int64) + hoff[-1]).tolist())
+        uoff.extend((np.asarray(nb.utt_off[1:], np.int64) + uoff[-1]).tolist())
+        am.append(nb.am)
+        refs += nb.refs
+        hids += nb.hyp_ids
+    uids = [f"utt_{u}" for u in range(len(uoff) - 1)]
+    return D.NBest(np.concatenate(toks).astype(np.int32), np.asarray(hoff, np.int32), np.asarray(uoff, np.int32),
+                   np.concatenate(am), refs, uids, hids)
+
+
+def test_c4_shape_real_lengths_mixed_chunk_and_ranks(w_base, oracle_model, golden_dir, tmp_path):
+    """C4 (MLM_PLL utterance-sharded, full dev set, N=100; MLM_PLL/main.py:164-203) at test
+    scale: 2 utterances x N=100 with base lengths drawn from the alfred test histogram
+    (mean T ~17; its longest reference has 37 characters, so every C4 sequence has T <= 64),
+    plus one utterance of T ~ 68-72 hypotheses scored in the SAME launch chunk, so the chunk
+    mixes T <= 64 sequences (16x16 attention) with T > 64 ones (online-softmax attention) and
+    layer-0 dedup is off for it.  Every masked row and PLL within 1e-3 of the oracle; the
+    101-weight fusion argmax from the oracle's lm equals the one from the HIP lm for the two
+    N=100 utterances; ``cli mlm_pll`` on the same texts as 1 rank and as 2 ranks (gloo
+    exchange, both on this GPU) writes bitwise-equal scores that match the scorer's."""
+    import socket
+    import subprocess
+    import sys
+    import yaml
+    from conftest import REPO
+    from asr_rescoring_amd.scorer import PLLScorer
+    from oracle import rescore_ref as RR
+    from oracle.bert_ref import pll_reference_pattern
+    nb_a = D.synthetic_nbest(2, 100, seed=41, lengths=_lengths(golden_dir), hard=True)
+    nb_b = D.synthetic_nbest(1, 10, seed=42, len_lo=66, len_hi=70, hard=True)
+    nb = _concat([nb_a, nb_b])
+    T = np.diff(nb.hyp_off)
+    assert T[:200].max() <= 64 < T[200:].min()
+    assert int(((T - 2) * T).sum()) <= 131072      # one launch chunk
+    s = PLLScorer(w_base, BERT_BASE, device=0, max_rows=131072)
+    try:
+        pll, rows = s.score_nbest(nb.tokens, nb.hyp_off, return_rows=True)
+        pll, rows = pll.cpu().numpy(), rows.cpu().numpy()
+    finally:
+        s.close()
+    ref_rows, ref_pll = pll_reference_pattern(oracle_model, nb.tokens, nb.hyp_off, batch_size=64,
+                                              full_head=False)
+    assert rel_err(rows, ref_rows).max() < REL
+    assert rel_err(pll, ref_pll).max() < REL
+    hyps, N = _oracle_hyps(nb_a)
+    am = nb_a.am.reshape(nb_a.n_utt, N)
+    bw_o, cer_o, arg_o = RR.find_best_weight(am, ref_pll[:200].reshape(2, N), hyps, nb_a.refs, n_best=N)
+    bw_h, cer_h, arg_h = RR.find_best_weight(am, pll[:200].reshape(2, N), hyps, nb_a.refs, n_best=N)
+    assert np.array_equal(arg_o, arg_h) and bw_o == bw_h and cer_o == cer_h
+    assert len({tuple(a) for a in arg_o}) > 1, "the argmax never moved: the check would be vacuous"
+
+    # cli mlm_pll (text -> native BertTokenizer-compatible tokenizer -> sharded scoring)
+    used = sorted({int(t) for t in nb.tokens if t >= D.FIRST_WORD_ID})
+    ch = {t: chr(0x4E00 + t - D.FIRST_WORD_ID) for t in used}
+    special = {0: "[PAD]", 100: "[UNK]", 101: "[CLS]", 102: "[SEP]", 103: "[MASK]"}
+    vocab = [special.get(i, ch.get(i, f"[unused{i}]")) for i in range(BERT_BASE.vocab)]
+    (tmp_path / "vocab.txt").write_text("\n".join(vocab) + "\n", encoding="utf-8")
+    text = {}
+    for u in range(nb.n_utt):
+        for k, h in enumerate(range(nb.utt_off[u], nb.utt_off[u + 1])):
+            text.setdefault(f"utt_{u}", {})[f"hyp_{k + 1}"] = "".join(ch[int(t)] for t in nb.hyp_words(h))
+    json.dump(text, open(tmp_path / "hyps.json", "w", encoding="utf-8"), ensure_ascii=False)
+    outs = {}
+    for world in (1, 2):
+        out = tmp_path / f"w{world}"
+        out.mkdir()
+        cfg = tmp_path / f"score_w{world}.yaml"
+        cfg.write_text(yaml.safe_dump({
+            "task": "scoring", "device": "cuda:0", "random_init_seed": 1234, "max_rows": 131072,
+            "dev_hyps_text_path": str(tmp_path / "hyps.json"), "output_path": str(out) + "/",
+            "model": {"bert": "bert-base-chinese", "vocab": str(tmp_path / "vocab.txt")}}, allow_unicode=True))
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+        sk.close()
+        code = ("import sys; sys.path.insert(0, %r); import __graft_entry__ as g; g._import_pkg(); "
+                "from asr_rescoring_amd import cli; sys.exit(cli.main(['mlm_pll', '--config', %r]))" % (REPO, str(cfg)))
+        procs = [subprocess.Popen([sys.executable, "-c", code],
+                                  env=dict(os.environ, WORLD_SIZE=str(world), RANK=str(r), LOCAL_RANK="0",
+                                           MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RS_DIST_BACKEND="gloo"))
+                 for r in range(world)]
+        for p in procs:
+            assert p.wait(timeout=300) == 0
+        outs[world] = json.load(open(out / "dev_lm.json", encoding="utf-8"))
+    assert list(outs[1]) == list(outs[2]) == [f"utt_{u}" for u in range(nb.n_utt)]
+    a = np.array([v for u in outs[1].values() for v in u.values()])
+    b = np.array([v for u in outs[2].values() for v in u.values()])
+    assert np.array_equal(a, b), np.abs(a - b).max()
+    assert np.array_equal(a, pll), np.abs(a - pll).max()

@@ -72,6 +72,53 @@ def test_gloo_world2_gather_matches_single_process():
     assert np.array_equal(got[1], lm)
 
 
+def test_exchange_device_rules():
+    from asr_rescoring_amd.shard import exchange_device
+    assert exchange_device("gloo", torch.device("cpu")) == torch.device("cpu")
+    assert exchange_device("gloo", torch.device("cpu"), "cuda:0") == torch.device("cpu")
+    assert exchange_device(None, torch.device("cpu")) == torch.device("cpu")
+    assert exchange_device("nccl", torch.device("cpu"), "cuda:1") == torch.device("cuda", 1)
+    if torch.cuda.is_available():
+        # an empty shard's CPU placeholder goes to this rank's GPU under RCCL
+        assert exchange_device("nccl", torch.device("cpu")).type == "cuda"
+
+
+def _tok_sum_fn(sub):
+    return torch.tensor([float(sub.tokens[sub.hyp_off[h]:sub.hyp_off[h + 1]].sum()) for h in range(sub.n_hyp)],
+                        dtype=torch.float64)
+
+
+def _worker_empty(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from asr_rescoring_amd.shard import score_sharded
+    nb = D.synthetic_nbest(1, 6, seed=13)          # one utterance, two ranks: rank 1 owns nothing
+    calls = []
+    both = score_sharded(nb, lambda sub: (calls.append(sub.n_utt), _tok_sum_fn(sub))[1])
+    q.put((rank, both.numpy(), calls))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_empty_shard():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker_empty, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, (b, c)) for r, b, c in (q.get(timeout=120), q.get(timeout=120)))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    nb = D.synthetic_nbest(1, 6, seed=13)
+    want = np.stack([nb.am, _tok_sum_fn(nb).numpy()])
+    # one rank owns the utterance, the other none and never calls the scorer
+    assert sorted([got[0][1], got[1][1]]) == [[], [1]]
+    for r in (0, 1):
+        assert np.array_equal(got[r][0], want)
+
+
 def _oracle_pll_fn(model):
     """Per-hypothesis oracle PLL (CPU fp32, batch = one hypothesis' rows): independent of how
     utterances are split, so sharded and single-process scores must be bitwise equal."""

@@ -83,10 +83,14 @@ def c4():
     nb = D.synthetic_nbest(718, 100, seed=1, lengths=_lengths())
     d_tok = torch.from_numpy(nb.tokens).cuda()
     dt = _timed(lambda: sc.score_nbest(d_tok, nb.hyp_off), steps=1)
+    prec = sc.precision
     sc.close()
     lens = np.diff(nb.hyp_off)
     return [{"workload": "C4 MLM_PLL real-length (718 of 7176 utts) N=100", "value": round(nb.n_forwards() / dt, 1),
-             "unit": "masked fwd/s", "forwards": nb.n_forwards(), "mean_T": round(float(np.average(lens, weights=lens - 2)), 2),
+             "unit": "masked fwd/s", "precision": prec,
+             "dtype": "fp16x3-split (fp32-accurate)" if prec == "fp16x3" else "fp16 (reduced precision)",
+             "parity": "tests/test_gpu_configs.py::test_c4_shape_real_lengths_mixed_chunk_and_ranks (rows/PLL vs oracle <1e-3, rerank argmax equal, 1 vs 2 ranks bitwise)",
+             "forwards": nb.n_forwards(), "mean_T": round(float(np.average(lens, weights=lens - 2)), 2),
              "ms_per_step": round(dt * 1e3, 1)}]
 
 
