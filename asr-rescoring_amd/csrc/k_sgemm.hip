@@ -4,25 +4,31 @@
 //
 // The reference trains in fp32, so these run on the f32-input MFMA (v_mfma_f32_32x32x2_f32:
 // exact f32, every result a k-ordered fmaf chain) rather than on the fp16 split-operand
-// kernels of the scoring path.  One kernel serves the three operand forms a Linear's
-// forward / backward needs, chosen by where k is contiguous in each operand:
-//   forward  Y  = X  · Wᵀ   A = X  [M][K] (k contiguous)   B = W [N][K] (k contiguous)
-//   dgrad    dX = dY · W    A = dY [M][N] (k contiguous)   B = W [N][K] (n contiguous)
-//   wgrad    dW = dYᵀ· X    A = dY [M][N] (m contiguous)   B = X [M][K] (n contiguous)
-// Tiles: 128×128 outputs per workgroup (4 waves, 64×64 each = 2×2 MFMA tiles of 32×32),
-// BK = 32.  Both operands are staged as [k][row] LDS images (row stride 132 floats), so every
-// fragment read is one ds_read_b32 over consecutive rows; k-contiguous sources are loaded as
-// float4 along k and transposed by the LDS writes, row-contiguous ones go in as float4.  The
-// next K-step's tiles are loaded into registers while this step's MFMAs run, and each MFMA
-// step's fragments are read one step ahead.  (Measured on MI355X with tools/sgemm_bench.py
-// over the training shapes — DESIGN §8 "Training": two LDS stages with source-oriented images
-// and ds_read_b128 fragments, the same with a bank-split [k][row] stride, loads two K-steps
-// ahead (RS_SGEMM_MODE=2), two stages with the next step's pieces interleaved into the MFMAs
-// (RS_SGEMM_MODE=3) and launch-bounds occupancy 3–4 were all equal or slower.)
+// kernels of the scoring path.  C[m][n] = sum_k A(m, k) B(n, k); each operand is read either
+// with k contiguous ("KC": [row][ld]) or with its output dimension contiguous ("MC":
+// [k][ld]), which covers the three forms a Linear needs:
+//   forward  Y  = X  · Wᵀ   A = X  (KC)   B = W  (KC)
+//   dgrad    dX = dY · W    A = dY (KC)   B = W  (MC: W[n][k'] read with k' = output column)
+//   wgrad    dW = dYᵀ· X    A = dY (MC)   B = X  (MC)
+//
+// Tiles (by shape, sg_pick): 128×128 (4 waves of 64×64, two workgroups per CU), 256×128 (8
+// waves of 64×64) and 256×256 (8 waves of 128×64); BK = 32; two LDS stages filled by LDS-DMA
+// (buffer_load_dwordx4 … lds, 1 KiB per wave-instruction) with one barrier per K-step and two
+// waves per SIMD.  No register staging and no transposing LDS writes: the DMA writes each
+// operand's natural image —
+//   KC: [row][32 k] rows of 128 B, 16-B chunks XOR-swizzled by (row >> 1) & 7 on the source
+//       address, so a wave's ds_read_b128 of 16 rows × one chunk hits 64 distinct banks;
+//   MC: [k][R rows] rows of 4R bytes (fragment reads are ds_read_b32 of 32 consecutive rows).
+// The K index inside a K-step is permuted (A and B alike, so the product is unchanged):
+// MFMA step kk of lane half h takes k = 16h + kk, which makes a KC lane's 16 values of a
+// K-step 64 contiguous bytes (4 × ds_read_b128).  All of a K-step's fragments are read into
+// registers before the next K-step's DMA is issued, so no LDS read follows an in-flight DMA
+// into the same LDS object (the compiler would wait vmcnt(0) before it).
 // Few output tiles (the weight gradients of a ~1k-token batch, the projections of a small
 // batch) are split over K: each split writes its partial tile to a workspace and an ordered
 // sum over the splits closes it — no float atomics, so a training step stays bitwise
-// reproducible.
+// reproducible.  Edges: lanes whose row or k lies outside the operand load from an offset past
+// the buffer descriptor's extent, which the hardware returns as zeros.
 #include <algorithm>
 #include <cstdlib>
 
@@ -31,193 +37,263 @@
 
 namespace {
 
-constexpr int SG_BM = 128, SG_BN = 128, SG_BK = 32, SG_LD = SG_BM + 4;
-// row stride of an operand's [k][row] image: 130 (≡ 2 mod 64 banks) for k-contiguous sources,
-// whose transposed scalar writes then hit 64 distinct banks per wave (132: two-way
-// conflicts); 132 for row-contiguous ones (16-B aligned rows for the float4 writes)
-template <bool KC>
-constexpr int sg_ld() { return KC ? SG_BM + 2 : SG_BM + 4; }
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
 
-// Loads one operand's [rows 128] × [k 32] tile into registers (4 float4 per thread).
-// KC: the source is [row][ld] with k contiguous; otherwise [k][ld] with rows contiguous.
-template <bool KC>
-__device__ __forceinline__ void sg_load(const float* __restrict__ src, int ld, int row0, int rows, int k0, int kend,
-                                        float4 (&r)[4]) {
-    const int t = threadIdx.x;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t sg_rsrc(const float* p, unsigned bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
+}
+
+// One operand's image of R rows × BK: its DMA source for this wave's pieces of a K-step (1 KiB
+// each; NP of them) and its fragment reads.  rows: operand rows (M or N) in [0, rows); k in
+// [kb, ke).  KC image: [R][BK] floats (rows of 4 BK bytes = NCH 16-B chunks), chunk c of row r
+// stored at position c ^ ((r >> SH) & (NCH - 1)) (SH: log2 of the rows per 256-B bank row), so
+// the ds_read_b128 of 16 rows × one chunk hits 64 distinct banks; MC image: [BK][R] floats.
+template <bool KC, int R, int NW, int BK>
+struct SgOperand {
+    static constexpr int NP = R * BK * 4 / 1024 / NW;        // pieces per wave per K-step
+    static constexpr int NCH = BK / 4, RP = 1024 / (BK * 4), SH = BK == 32 ? 1 : 2;
+    static_assert(BK == 16 || BK == 32, "BK");
+    static_assert(NP >= 1 && NP * NW * 1024 == R * BK * 4, "pieces must split evenly over the waves");
+    __amdgpu_buffer_rsrc_t rs;
+    unsigned oob;                // an offset past the descriptor's extent: loads return 0
+    unsigned voff[NP];           // per piece: byte offset of this lane's 16 B at k0 = 0 (oob: row outside)
+    int krow[NP];                // KC: the lane's k within the step (4 lc); MC: its k-row
+    int ld;
+
+    __device__ void init(const float* src, int ld_, int rows, int row0, int wave, int lane) {
+        ld = ld_;
+        oob = 0x7FFFFFF0u;       // the operand's extent is host-checked below 2^31 bytes
+        rs = sg_rsrc(src, oob);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int idx = t + 256 * i;
-        int row, k;
-        if (KC) {
-            row = idx >> 3;
-            k = (idx & 7) * 4;
-        } else {
-            k = idx >> 5;
-            row = (idx & 31) * 4;
+        for (int i = 0; i < NP; ++i) {
+            const int p = NW * i + wave;
+            if (KC) {
+                const int r = RP * p + lane / NCH;                          // image row of this lane
+                const int lc = (lane % NCH) ^ ((r >> SH) & (NCH - 1));      // logical 16-B chunk
+                krow[i] = 4 * lc;
+                voff[i] = row0 + r < rows ? (unsigned)(((row0 + r) * ld + 4 * lc) * 4) : oob;
+            } else {
+                const int byte = p * 1024 + lane * 16;
+                const int kr = byte / (R * 4), c = row0 + (byte % (R * 4)) / 4;
+                krow[i] = kr;
+                voff[i] = c < rows ? (unsigned)((kr * ld + c) * 4) : oob;
+            }
         }
-        const int gr = row0 + row, gk = k0 + k;
-        // extents along the contiguous dimension are multiples of 4 (host-checked): a float4
-        // is either wholly inside or wholly outside
-        const bool ok = gr < rows && gk < kend;
-        r[i] = ok ? (KC ? *(const float4*)(src + (size_t)gr * ld + gk) : *(const float4*)(src + (size_t)gk * ld + gr))
-                  : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-}
-
-// [k][row] LDS image: k-contiguous sources are transposed by the writes (4 ds_write_b32 per
-// float4), row-contiguous ones go in as one ds_write_b128.  Piece i (0..3) of this thread.
-template <bool KC>
-__device__ __forceinline__ void sg_store_one(float* __restrict__ s, int i, const float4 v) {
-    const int idx = threadIdx.x + 256 * i;
-    if (KC) {
-        const int row = idx >> 3, k = (idx & 7) * 4;
-        constexpr int L = sg_ld<true>();
-        s[(k + 0) * L + row] = v.x;
-        s[(k + 1) * L + row] = v.y;
-        s[(k + 2) * L + row] = v.z;
-        s[(k + 3) * L + row] = v.w;
-    } else {
-        const int k = idx >> 5, row = (idx & 31) * 4;
-        *(float4*)(s + k * sg_ld<false>() + row) = v;
-    }
-}
-
-template <bool KC>
-__device__ __forceinline__ void sg_store_lds(float* __restrict__ s, const float4 (&r)[4]) {
+    // DMA this wave's pieces of K-step k0 into the image at lds.  The lane offsets are fixed
+    // per workgroup (k0 rides in the scalar offset), so each piece's offset stays in its own
+    // register across the loop and the DMAs issue back to back (an offset re-formed per piece
+    // in one reused VGPR makes every v_cndmask wait for the previous buffer_load to read it).
+    // Only a K-step that crosses ke (the tail of K) masks lanes per step.  (The builtin's
+    // arguments are plain locals on purpose: with a conditional expression or an array element
+    // written in place as the offset argument, hipcc / ROCm 7.2 silently emitted no host launch
+    // stub for the MC instantiations — an undefined symbol at load time.)
+    __device__ __forceinline__ void stage(char* lds, int wave, int k0, int ke) const {
+        const int so = KC ? k0 * 4 : k0 * ld * 4;
+        if (k0 + BK <= ke) {                     // wave-uniform: every K-step but the tail
 #pragma unroll
-    for (int i = 0; i < 4; ++i) sg_store_one<KC>(s, i, r[i]);
-}
+            for (int i = 0; i < NP; ++i) {
+                const unsigned vo = voff[i];
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void*)(lds + (NW * i + wave) * 1024), 16, vo, so, 0, 0);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < NP; ++i) {
+                const bool in = k0 + krow[i] < ke;
+                const unsigned vo = in ? voff[i] : oob;
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(
+                    rs, (__attribute__((address_space(3))) void*)(lds + (NW * i + wave) * 1024), 16, vo, so, 0, 0);
+            }
+        }
+    }
+    // fragments of one 32-row MFMA tile for a K-step: f[kk] = operand(row r, k = (BK/2) h + kk)
+    __device__ __forceinline__ static void frag(const char* img, int r, int h, float (&f)[BK / 2]) {
+        if (KC) {
+#pragma unroll
+            for (int q = 0; q < BK / 8; ++q) {
+                const int pc = ((BK / 8) * h + q) ^ ((r >> SH) & (NCH - 1));
+                const float4 v = *(const float4*)(img + r * BK * 4 + pc * 16);
+                f[4 * q] = v.x; f[4 * q + 1] = v.y; f[4 * q + 2] = v.z; f[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int kk = 0; kk < BK / 2; ++kk) f[kk] = *(const float*)(img + ((BK / 2) * h + kk) * R * 4 + r * 4);
+        }
+    }
+};
 
 // C[M][N] (+)= A·B over k in [z·kc, min(K, (z+1)·kc)) for split z = blockIdx.z.
 // ws == nullptr: C = acc (+ C when accum).  Otherwise the partial goes to ws[z][M][N].
-// MODE 1 (default): one LDS stage — store, barrier, MFMAs, barrier per K-step, the next
-// step's global loads in flight under the MFMAs.  MODE 2: the same with loads two K-steps
-// ahead (a second register set).  MODE 3: two LDS stages — the next step's tiles are
-// written to the other stage between the second half of this step's MFMAs (one float4 piece
-// after each group of four), one barrier per K-step.
-template <bool AKC, bool BKC, int MODE>
-__global__ void __launch_bounds__(256)
-sgemm_f32_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb, float* __restrict__ C,
+// Tile BM × BN × BK, waves of TM × 64 (TM/32 × 2 MFMA tiles of 32×32), OCC workgroups per CU.
+template <bool AKC, bool BKC, int BM, int BN, int TM, int BK, int OCC>
+__global__ void __launch_bounds__((BM / TM) * (BN / 64) * 64, OCC * (BM / TM) * (BN / 64) / 4)
+sgemm_dma_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb, float* __restrict__ C,
                  int ldc, int M, int N, int K, int kc, int accum, float* __restrict__ ws) {
-    extern __shared__ __attribute__((aligned(16))) float sg_smem[];   // stages x (A image | B image)
-    constexpr int SIMG = SG_BK * SG_LD, PF = MODE == 2 ? 2 : 1;
-    float* As = sg_smem;
-    float* Bs = sg_smem + SIMG;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int m0 = blockIdx.y * SG_BM, n0 = blockIdx.x * SG_BN;
+    constexpr int WM = BM / TM, WN = BN / 64, NW = WM * WN, MT = TM / 32, HK = BK / 2;
+    constexpr int IMG_A = BM * BK * 4, STAGE = (BM + BN) * BK * 4;
+    using OA = SgOperand<AKC, BM, NW, BK>;
+    using OB = SgOperand<BKC, BN, NW, BK>;
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
     const int kb = blockIdx.z * kc, ke = min(K, kb + kc);
-    const int wm = (w & 1) * 64, wn = (w >> 1) * 64;
+    const int wm = (wave % WM) * TM, wn = (wave / WM) * 64;
     const int h = lane >> 5, c = lane & 31;
 
-    f32x16 acc[2][2];
+    OA oa;
+    OB ob;
+    oa.init(A, lda, M, m0, wave, lane);
+    ob.init(B, ldb, N, n0, wave, lane);
+
+    f32x16_t acc[MT][2];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    // one K-step: stage the registers' tiles, refill them PF steps ahead, multiply
-    auto kstep = [&](int k0, float4 (&ra)[4], float4 (&rb)[4]) {
-        sg_store_lds<AKC>(As, ra);
-        sg_store_lds<BKC>(Bs, rb);
+    oa.stage(smem, wave, kb, ke);
+    ob.stage(smem + IMG_A, wave, kb, ke);
+    int buf = 0;
+    for (int k0 = kb; k0 < ke; k0 += BK) {
+        // this K-step landed for this wave; the barrier: for every wave, and every wave is done
+        // reading the other buffer (its fragments of the previous step are in registers)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        const int kn = k0 + PF * SG_BK;
-        if (kn < ke) {                         // tiles PF steps ahead in flight under the MFMAs
-            sg_load<AKC>(A, lda, m0, M, kn, ke, ra);
-            sg_load<BKC>(B, ldb, n0, N, kn, ke, rb);
-        }
-        // MFMA step kk, lane half h: k = 2 kk + h (the instruction's A[i][k = lane >> 5] map).
-        // Fragments of step kk + 1 are read before step kk's MFMAs issue, so the LDS latency
-        // runs under the MFMA pipe (hipcc otherwise waits lgkmcnt(0) before every step).
-        constexpr int LA = sg_ld<AKC>(), LB = sg_ld<BKC>();
-        const float* ap = As + h * LA + wm + c;
-        const float* bp = Bs + h * LB + wn + c;
-        float a0 = ap[0], a1 = ap[32], b0 = bp[0], b1 = bp[32];
+        const char* st = smem + buf * STAGE;
+        float fa[MT][HK], fb[2][HK];
 #pragma unroll
-        for (int kk = 0; kk < SG_BK / 2; ++kk) {
-            float na0 = 0.f, na1 = 0.f, nb0 = 0.f, nb1 = 0.f;
-            if (kk + 1 < SG_BK / 2) {
-                const int oa = 2 * (kk + 1) * LA, ob = 2 * (kk + 1) * LB;
-                na0 = ap[oa]; na1 = ap[oa + 32]; nb0 = bp[ob]; nb1 = bp[ob + 32];
-            }
-            __builtin_amdgcn_sched_barrier(0);   // keep the reads ahead of this step's MFMAs
-            acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-            acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-            acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-            acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-            __builtin_amdgcn_sched_barrier(0);
-            a0 = na0; a1 = na1; b0 = nb0; b1 = nb1;
-        }
-        __syncthreads();
-    };
-
-    float4 ra[4], rb[4];
-    sg_load<AKC>(A, lda, m0, M, kb, ke, ra);
-    sg_load<BKC>(B, ldb, n0, N, kb, ke, rb);
-    if constexpr (MODE == 3) {
-        sg_store_lds<AKC>(sg_smem, ra);
-        sg_store_lds<BKC>(sg_smem + SIMG, rb);
-        __syncthreads();
-        int cur = 0;
-        for (int k0 = kb; k0 < ke; k0 += SG_BK) {
-            const bool more = k0 + SG_BK < ke;
-            if (more) {
-                sg_load<AKC>(A, lda, m0, M, k0 + SG_BK, ke, ra);
-                sg_load<BKC>(B, ldb, n0, N, k0 + SG_BK, ke, rb);
-            }
-            constexpr int LA = sg_ld<AKC>(), LB = sg_ld<BKC>();
-            const float* ap = sg_smem + cur * 2 * SIMG + h * LA + wm + c;
-            const float* bp = sg_smem + cur * 2 * SIMG + SIMG + h * LB + wn + c;
-            float* nx = sg_smem + (cur ^ 1) * 2 * SIMG;
-            float a0 = ap[0], a1 = ap[32], b0 = bp[0], b1 = bp[32];
+        for (int i = 0; i < MT; ++i) OA::frag(st, wm + 32 * i + c, h, fa[i]);
 #pragma unroll
-            for (int kk = 0; kk < SG_BK / 2; ++kk) {
-                float na0 = 0.f, na1 = 0.f, nb0 = 0.f, nb1 = 0.f;
-                if (kk + 1 < SG_BK / 2) {
-                    const int oa = 2 * (kk + 1) * LA, ob = 2 * (kk + 1) * LB;
-                    na0 = ap[oa]; na1 = ap[oa + 32]; nb0 = bp[ob]; nb1 = bp[ob + 32];
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc[0][0], 0, 0, 0);
-                acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc[0][1], 0, 0, 0);
-                acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc[1][0], 0, 0, 0);
-                acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc[1][1], 0, 0, 0);
-                if (kk >= 8 && more) {         // pieces 0-3 of A, then of B, half a step after their loads
-                    const int i = kk - 8;
-                    if (i < 4) sg_store_one<AKC>(nx, i, ra[i]);
-                    else sg_store_one<BKC>(nx + SIMG, i - 4, rb[i - 4]);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-                a0 = na0; a1 = na1; b0 = nb0; b1 = nb1;
-            }
-            __syncthreads();
-            cur ^= 1;
+        for (int j = 0; j < 2; ++j) OB::frag(st + IMG_A, wn + 32 * j + c, h, fb[j]);
+        // fragments in registers before the next K-step's DMA goes into the other buffer
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        if (k0 + BK < ke) {
+            char* nx = smem + (buf ^ 1) * STAGE;
+            oa.stage(nx, wave, k0 + BK, ke);
+            ob.stage(nx + IMG_A, wave, k0 + BK, ke);
         }
-    } else if constexpr (PF == 1) {
-        for (int k0 = kb; k0 < ke; k0 += SG_BK) kstep(k0, ra, rb);
-    } else {
-        float4 ra2[4], rb2[4];
-        if (kb + SG_BK < ke) {
-            sg_load<AKC>(A, lda, m0, M, kb + SG_BK, ke, ra2);
-            sg_load<BKC>(B, ldb, n0, N, kb + SG_BK, ke, rb2);
-        }
-        for (int k0 = kb; k0 < ke; k0 += SG_BK) {
-            kstep(k0, ra, rb);                 // refills ra / rb with step k0 + 2 BK
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {      // the next step's tiles are in the second set
-                const float4 ta = ra[i], tb = rb[i];
-                ra[i] = ra2[i]; rb[i] = rb2[i];
-                ra2[i] = ta; rb2[i] = tb;
-            }
-        }
+        for (int kk = 0; kk < HK; ++kk)
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][kk], fb[j][kk], acc[i][j], 0, 0, 0);
+        buf ^= 1;
     }
 
     // D map of the 32x32 forms: column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
     float* P = ws ? ws + (size_t)blockIdx.z * M * N : nullptr;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = n0 + wn + 32 * j + c;
+            if (col >= N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (row >= M) continue;
+                if (P) {
+                    P[(size_t)row * N + col] = acc[i][j][r];
+                } else {
+                    float* o = C + (size_t)row * ldc + col;
+                    *o = accum ? acc[i][j][r] + *o : acc[i][j][r];
+                }
+            }
+        }
+}
+
+// Software-pipelined form: a 3-stage LDS ring, the DMA two K-steps ahead, and the next
+// K-step's fragments read from LDS while this K-step's MFMAs run (two fragment sets in
+// registers).  The plain form above runs barrier -> fragment reads -> DMA issue -> MFMAs in
+// every wave, so the two workgroups sharing a SIMD fall into lockstep and the MFMA pipe idles
+// through both waves' read / issue / barrier phases; here those phases of step t+1 hide under
+// step t's MFMAs.  Per iteration t: vmcnt(0) (step t+1's DMA, issued one iteration ago, landed
+// for this wave), barrier (landed for every wave; every wave finished reading buffer (t-1)%3),
+// fragment reads of step t+1 (issued first: an LDS read placed after an LDS-DMA issue would get
+// a compiler vmcnt(0) in front of it), DMA of step t+2 into buffer (t+2)%3 = (t-1)%3, MFMAs of
+// step t.
+template <bool AKC, bool BKC, int BM, int BN, int TM, int BK, int OCC>
+__global__ void __launch_bounds__((BM / TM) * (BN / 64) * 64, OCC * (BM / TM) * (BN / 64) / 4)
+sgemm_pipe_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb, float* __restrict__ C,
+                  int ldc, int M, int N, int K, int kc, int accum, float* __restrict__ ws) {
+    constexpr int WM = BM / TM, WN = BN / 64, NW = WM * WN, MT = TM / 32, HK = BK / 2;
+    constexpr int IMG_A = BM * BK * 4, STAGE = (BM + BN) * BK * 4;
+    using OA = SgOperand<AKC, BM, NW, BK>;
+    using OB = SgOperand<BKC, BN, NW, BK>;
+    __shared__ __attribute__((aligned(16))) char smem[3 * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
+    const int kb = blockIdx.z * kc, ke = min(K, kb + kc);
+    const int nt = (ke - kb + BK - 1) / BK;
+    const int wm = (wave % WM) * TM, wn = (wave / WM) * 64;
+    const int h = lane >> 5, c = lane & 31;
+
+    OA oa;
+    OB ob;
+    oa.init(A, lda, M, m0, wave, lane);
+    ob.init(B, ldb, N, n0, wave, lane);
+
+    f32x16_t acc[MT][2];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    auto stage = [&](int t) {
+        char* dst = smem + (t % 3) * STAGE;
+        oa.stage(dst, wave, kb + t * BK, ke);
+        ob.stage(dst + IMG_A, wave, kb + t * BK, ke);
+    };
+    float fa[MT][HK], fb[2][HK], ga[MT][HK], gb[2][HK];
+    auto frags = [&](int t, float (&xa)[MT][HK], float (&xb)[2][HK]) {
+        const char* st = smem + (t % 3) * STAGE;
+#pragma unroll
+        for (int i = 0; i < MT; ++i) OA::frag(st, wm + 32 * i + c, h, xa[i]);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) OB::frag(st + IMG_A, wn + 32 * j + c, h, xb[j]);
+    };
+    stage(0);
+    if (nt > 1) stage(1);
+    if (nt > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OA::NP + OB::NP) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    frags(0, fa, fb);
+    // one K-step: MFMAs on (xa, xb) = step t's fragments while step t+1's are read into (ya, yb);
+    // the loop runs two steps per trip with the register sets swapping roles (no copies)
+    auto step = [&](int t, float (&xa)[MT][HK], float (&xb)[2][HK], float (&ya)[MT][HK], float (&yb)[2][HK]) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t + 1 < nt) frags(t + 1, ya, yb);
+        __builtin_amdgcn_sched_barrier(0);
+        if (t + 2 < nt) stage(t + 2);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kk = 0; kk < HK; ++kk)
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[i][kk], xb[j][kk], acc[i][j], 0, 0, 0);
+    };
+    for (int t = 0; t < nt; t += 2) {
+        step(t, fa, fb, ga, gb);
+        if (t + 1 < nt) step(t + 1, ga, gb, fa, fb);
+    }
+
+    float* P = ws ? ws + (size_t)blockIdx.z * M * N : nullptr;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) {
             const int col = n0 + wn + 32 * j + c;
@@ -257,37 +333,66 @@ sgemm_splitk_sum_kernel(const float* __restrict__ ws, int splits, int M, int N, 
     *o = s;
 }
 
-int sg_splits(int M, int N, int K, int* kc) {
-    const int tiles = ((M + SG_BM - 1) / SG_BM) * ((N + SG_BN - 1) / SG_BN);
-    const int steps = (K + SG_BK - 1) / SG_BK;
+// Tile configurations: 0 = 128×128×32 (4 waves of 64×64, 2 workgroups per CU, 64 KiB LDS),
+// 1 = 128×128×16 (the same waves, 4 workgroups per CU, 32 KiB LDS: a mid-size GEMM's tiles all
+// resident at once), 2 = 256×128×32 (8 waves of 64×64, 1 per CU; half the operand bytes per
+// FLOP of a 128×128 tile on the A side).
+struct SgCfg { int bm, bn, bk, occ; };
+constexpr int kSgNCfg = 5;
+constexpr SgCfg kSgCfg[kSgNCfg] = {{128, 128, 32, 2}, {128, 128, 16, 4}, {256, 128, 32, 1},
+                                   {128, 128, 16, 3}, {128, 128, 32, 1}};   // 3, 4: sgemm_pipe_kernel
+
+int sg_splits(int cfg, int M, int N, int K, int* kc) {
+    const SgCfg& g = kSgCfg[cfg];
+    const int tiles = ((M + g.bm - 1) / g.bm) * ((N + g.bn - 1) / g.bn);
+    const int steps = (K + g.bk - 1) / g.bk;
     int splits = 1;
-    // up to ~512 workgroups (two per CU); each split costs a write + read of M·N partials.
+    // up to ~target workgroups; each split costs a write + read of M·N partials.
     // RS_SGEMM_SPLIT_WG overrides the workgroup target (A/B knob).
-    static const int target = [] {
+    static const int target_env = [] {
         const char* v = getenv("RS_SGEMM_SPLIT_WG");
-        return v ? std::max(1, atoi(v)) : 512;
+        return v ? std::max(1, atoi(v)) : 0;
     }();
+    const int target = target_env ? target_env : 256 * g.occ;
     if (tiles < target) splits = std::max(1, std::min(std::min((target + tiles - 1) / tiles, steps / 4), 16));
     const int per = (steps + splits - 1) / splits;
-    *kc = per * SG_BK;
+    *kc = per * g.bk;
     return (steps + per - 1) / per;
+}
+
+// RS_SGEMM_CFG=0/1/2 forces a tile configuration (A/B knob); default: by shape
+int sg_pick(int M, int N, int K) {
+    static const int forced = [] {
+        const char* v = getenv("RS_SGEMM_CFG");
+        return v ? atoi(v) : -1;
+    }();
+    if (forced >= 0 && forced < kSgNCfg) return forced;
+    (void)M; (void)N; (void)K;
+    return 1;
 }
 
 }  // namespace
 
 size_t tr_sgemm_ws_floats(int M, int N, int K) {
-    int kc = 0;
-    const int s = sg_splits(M, N, K, &kc);
-    return s > 1 ? (size_t)s * M * N : 0;
+    size_t w = 0;
+    for (int cfg = 0; cfg < kSgNCfg; ++cfg) {  // any configuration the picker or the knob may choose
+        int kc = 0;
+        const int s = sg_splits(cfg, M, N, K, &kc);
+        if (s > 1) w = std::max(w, (size_t)s * M * N);
+    }
+    return w;
 }
 
-hipError_t tr_sgemm(int M, int N, int K, const float* A, int lda, bool a_kc, const float* B, int ldb, bool b_kc,
-                    float* C, int ldc, int accum, float* ws, size_t ws_floats, hipStream_t s) {
+static hipError_t sg_run(int cfg, int M, int N, int K, const float* A, int lda, bool a_kc, const float* B, int ldb,
+                         bool b_kc, float* C, int ldc, int accum, float* ws, size_t ws_floats, hipStream_t s) {
     if (M <= 0 || N <= 0) return hipSuccess;
-    // float4 loads along each operand's contiguous dimension and along C's rows (split-K sum)
-    if (N % 4 || lda % 4 || ldb % 4 || ldc % 4 || (a_kc ? K % 4 : M % 4) || (b_kc && K % 4) ||
-        ((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16)
+    // 16-B DMA pieces along each operand's contiguous dimension, float4 rows of C (split-K sum)
+    if (N % 4 || lda % 4 || ldb % 4 || ldc % 4 || (a_kc ? K % 4 : M % 4) || (b_kc ? K % 4 : N % 4) ||
+        ((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 || cfg < 0 || cfg >= kSgNCfg)
         return hipErrorInvalidValue;
+    // 32-bit byte offsets into each operand (buffer descriptors)
+    const long long ea = (long long)(a_kc ? M : K) * lda * 4, eb = (long long)(b_kc ? N : K) * ldb * 4;
+    if (ea >= 0x7FFFFFF0ll || eb >= 0x7FFFFFF0ll) return hipErrorInvalidValue;
     if (K <= 0) {   // empty reduction: C = 0 (+ C)
         if (accum) return hipSuccess;
         for (int r = 0; r < M; ++r) {
@@ -297,45 +402,29 @@ hipError_t tr_sgemm(int M, int N, int K, const float* A, int lda, bool a_kc, con
         return hipSuccess;
     }
     int kc = 0;
-    const int splits = sg_splits(M, N, K, &kc);
+    const int splits = sg_splits(cfg, M, N, K, &kc);
     float* P = nullptr;
     if (splits > 1) {
         if (!ws || ws_floats < (size_t)splits * M * N) return hipErrorInvalidValue;
         P = ws;
     }
-    const dim3 grid((N + SG_BN - 1) / SG_BN, (M + SG_BM - 1) / SG_BM, splits);
-#define SG_LAUNCH(AK, BK_, MD)                                                                              \
-    do {                                                                                                    \
-        constexpr int smem = (MD == 3 ? 4 : 2) * SG_BK * SG_LD * 4;                                          \
-        if (smem > 65536) {                                                                                 \
-            static bool attr = false;                                                                       \
-            if (!attr) {                                                                                    \
-                hipError_t ea = hipFuncSetAttribute((const void*)sgemm_f32_kernel<AK, BK_, MD>,             \
-                                                    hipFuncAttributeMaxDynamicSharedMemorySize, smem);      \
-                if (ea != hipSuccess) return ea;                                                            \
-                attr = true;                                                                                \
-            }                                                                                               \
-        }                                                                                                   \
-        hipLaunchKernelGGL((sgemm_f32_kernel<AK, BK_, MD>), grid, dim3(256), smem, s, A, lda, B, ldb, C, ldc, \
-                           M, N, K, kc, accum, P);                                                          \
+    const SgCfg& g = kSgCfg[cfg];
+    const dim3 grid((N + g.bn - 1) / g.bn, (M + g.bm - 1) / g.bm, splits);
+#define SG_LAUNCH(KER, AK, BK_, BM_, BN_, TM_, KB_, OCC_)                                                    \
+    hipLaunchKernelGGL((KER<AK, BK_, BM_, BN_, TM_, KB_, OCC_>), grid, dim3((BM_ / TM_) * (BN_ / 64) * 64), 0, s, \
+                       A, lda, B, ldb, C, ldc, M, N, K, kc, accum, P)
+#define SG_FORMS(KER, BM_, BN_, TM_, KB_, OCC_)                                   \
+    do {                                                                          \
+        if (a_kc && b_kc) SG_LAUNCH(KER, true, true, BM_, BN_, TM_, KB_, OCC_);   \
+        else if (a_kc) SG_LAUNCH(KER, true, false, BM_, BN_, TM_, KB_, OCC_);     \
+        else if (b_kc) SG_LAUNCH(KER, false, true, BM_, BN_, TM_, KB_, OCC_);     \
+        else SG_LAUNCH(KER, false, false, BM_, BN_, TM_, KB_, OCC_);              \
     } while (0)
-#define SG_FORMS(MD)                                  \
-    if (a_kc && b_kc) SG_LAUNCH(true, true, MD);      \
-    else if (a_kc) SG_LAUNCH(true, false, MD);        \
-    else if (b_kc) SG_LAUNCH(false, true, MD);        \
-    else SG_LAUNCH(false, false, MD);
-    static const int mode = [] {                       // RS_SGEMM_MODE=2/3: A/B knob
-        const char* v = getenv("RS_SGEMM_MODE");
-        const int m = v ? atoi(v) : 1;
-        return m == 2 || m == 3 ? m : 1;
-    }();
-    if (mode == 3) {
-        SG_FORMS(3)
-    } else if (mode == 2) {
-        SG_FORMS(2)
-    } else {
-        SG_FORMS(1)
-    }
+    if (cfg == 0) SG_FORMS(sgemm_dma_kernel, 128, 128, 64, 32, 2);
+    else if (cfg == 1) SG_FORMS(sgemm_dma_kernel, 128, 128, 64, 16, 4);
+    else if (cfg == 2) SG_FORMS(sgemm_dma_kernel, 256, 128, 64, 32, 1);
+    else if (cfg == 3) SG_FORMS(sgemm_pipe_kernel, 128, 128, 64, 16, 3);
+    else SG_FORMS(sgemm_pipe_kernel, 128, 128, 64, 32, 1);
 #undef SG_FORMS
 #undef SG_LAUNCH
     hipError_t e = hipGetLastError();
@@ -346,11 +435,16 @@ hipError_t tr_sgemm(int M, int N, int K, const float* A, int lda, bool a_kc, con
     return hipGetLastError();
 }
 
+hipError_t tr_sgemm(int M, int N, int K, const float* A, int lda, bool a_kc, const float* B, int ldb, bool b_kc,
+                    float* C, int ldc, int accum, float* ws, size_t ws_floats, hipStream_t s) {
+    return sg_run(sg_pick(M, N, K), M, N, K, A, lda, a_kc, B, ldb, b_kc, C, ldc, accum, ws, ws_floats, s);
+}
+
 // Test / timing entry (not part of the scoring path): one trainer GEMM in the given operand
-// form; the split-K workspace is a grow-only buffer kept across calls (single-threaded use).
-// Returns 0 on success.
-extern "C" int rs_debug_sgemm(int M, int N, int K, const float* A, int lda, int a_kc, const float* B, int ldb, int b_kc,
-                              float* C, int ldc, int accum, void* stream) {
+// form (cfg -1: the shape's pick, 0..2: a tile configuration); the split-K workspace is a
+// grow-only buffer kept across calls (single-threaded use).  Returns 0 on success.
+extern "C" int rs_debug_sgemm_cfg(int cfg, int M, int N, int K, const float* A, int lda, int a_kc, const float* B,
+                                  int ldb, int b_kc, float* C, int ldc, int accum, void* stream) {
     static float* ws = nullptr;
     static size_t ws_cap = 0;
     const size_t wsf = tr_sgemm_ws_floats(M, N, K);
@@ -364,7 +458,12 @@ extern "C" int rs_debug_sgemm(int M, int N, int K, const float* A, int lda, int 
         if (hipMalloc(&ws, wsf * 4) != hipSuccess) return -3;
         ws_cap = wsf;
     }
-    hipError_t e = tr_sgemm(M, N, K, A, lda, a_kc != 0, B, ldb, b_kc != 0, C, ldc, accum, ws, ws_cap,
-                            (hipStream_t)stream);
+    hipError_t e = sg_run(cfg < 0 ? sg_pick(M, N, K) : cfg, M, N, K, A, lda, a_kc != 0, B, ldb, b_kc != 0, C, ldc,
+                          accum, ws, ws_cap, (hipStream_t)stream);
     return e == hipSuccess ? 0 : -2;
+}
+
+extern "C" int rs_debug_sgemm(int M, int N, int K, const float* A, int lda, int a_kc, const float* B, int ldb, int b_kc,
+                              float* C, int ldc, int accum, void* stream) {
+    return rs_debug_sgemm_cfg(-1, M, N, K, A, lda, a_kc, B, ldb, b_kc, C, ldc, accum, stream);
 }

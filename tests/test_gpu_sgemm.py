@@ -20,29 +20,29 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module")
 def sgemm():
     lib = _lib.load()
-    fn = lib.rs_debug_sgemm
+    fn = lib.rs_debug_sgemm_cfg
     fn.restype = ctypes.c_int
-    fn.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+    fn.argtypes = [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
                                         ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     st = torch.cuda.current_stream().cuda_stream
 
-    def run(form, dY_or_X, W_or_X, out, accum):
+    def run(form, dY_or_X, W_or_X, out, accum, cfg=-1):
         """form nt: out[M,N] = A[M,K] . B[N,K]^T; nn: out[M,K] = A[M,N] . B[N,K];
-        tn: out[N,K] = A[M,N]^T . B[M,K]"""
+        tn: out[N,K] = A[M,N]^T . B[M,K].  cfg: tile configuration (-1: the shape's pick)."""
         A, B = dY_or_X, W_or_X
         if form == "nt":
             M, K = A.shape
             N = B.shape[0]
-            r = fn(M, N, K, A.data_ptr(), K, 1, B.data_ptr(), K, 1, out.data_ptr(), out.stride(0), accum, st)
+            r = fn(cfg, M, N, K, A.data_ptr(), K, 1, B.data_ptr(), K, 1, out.data_ptr(), out.stride(0), accum, st)
         elif form == "nn":
             M, N = A.shape
             K = B.shape[1]
-            r = fn(M, K, N, A.data_ptr(), N, 1, B.data_ptr(), K, 0, out.data_ptr(), out.stride(0), accum, st)
+            r = fn(cfg, M, K, N, A.data_ptr(), N, 1, B.data_ptr(), K, 0, out.data_ptr(), out.stride(0), accum, st)
         else:
             M, N = A.shape
             K = B.shape[1]
-            r = fn(N, K, M, A.data_ptr(), N, 0, B.data_ptr(), K, 0, out.data_ptr(), out.stride(0), accum, st)
+            r = fn(cfg, N, K, M, A.data_ptr(), N, 0, B.data_ptr(), K, 0, out.data_ptr(), out.stride(0), accum, st)
         assert r == 0
         torch.cuda.synchronize()
         return out
@@ -75,7 +75,9 @@ CASES = [("nt", 1037, 2304, 768), ("nt", 1037, 768, 3072), ("nt", 301, 21128, 76
 
 @pytest.mark.parametrize("form,M,N,K", CASES)
 @pytest.mark.parametrize("accum", [0, 1])
-def test_sgemm_forms_vs_float64(sgemm, form, M, N, K, accum):
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
+def test_sgemm_forms_vs_float64(sgemm, form, M, N, K, accum, cfg):
+    """Every tile configuration (k_sgemm.hip kSgCfg) on every form and edge."""
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)
     if form == "nt":
         A = torch.randn(M, K, device="cuda", generator=g)
@@ -92,13 +94,13 @@ def test_sgemm_forms_vs_float64(sgemm, form, M, N, K, accum):
     C0 = torch.randn(*shape, device="cuda", generator=g) if accum else \
         torch.full(shape, float("nan"), device="cuda")
     ref = _ref(form, A, B) + (C0.double() if accum else 0.0)
-    out = sgemm(form, A, B, C0.clone(), accum)
+    out = sgemm(form, A, B, C0.clone(), accum, cfg)
     err = (out.double() - ref).abs()
     bound = _abs_bound(form, A, B) + (C0.double().abs() * 2.0 ** -23 if accum else 0.0)
     assert torch.isfinite(out).all()
     assert (err <= bound).all(), (form, M, N, K, float((err / bound).max()))
     # same inputs, same bits (ordered split-K sum, no atomics)
-    again = sgemm(form, A, B, C0.clone(), accum)
+    again = sgemm(form, A, B, C0.clone(), accum, cfg)
     assert torch.equal(out, again)
 
 

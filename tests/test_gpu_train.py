@@ -295,6 +295,8 @@ def test_dropout_gradients_match_oracle_fed_the_same_masks(method):
                            0.1, 0.1)
         ref.step(seqs, target, am, cer, n_best=4, method=method, md_loss_weight=0.5, update=True, drop=drop)
         for k in tr.shapes:
+            if k.endswith("attention.self.key.bias"):
+                continue        # exactly-zero gradient: AdamW steps on rounding noise (check_updates)
             d, rd = tr.tensor(k) - w[k].reshape(tr.shapes[k]), ref.tensor(k) - w[k].reshape(tr.shapes[k])
             assert np.linalg.norm(d - rd) <= 2e-2 * max(np.linalg.norm(rd), 1e-12), k
     finally:

@@ -12,6 +12,9 @@ def short(n):
         re.search(r"sgemm_f32_kernelILb(\d)ELb(\d)ELi(\d+)E", n)
     if m:
         return f"sgemm_f32<{m.group(1)},{m.group(2)},mode{m.group(3)}>"
+    m = re.search(r"sgemm_dma_kernelILb(\d)ELb(\d)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)ELi(\d+)E", n)
+    if m:
+        return f"sgemm_dma<{m.group(1)},{m.group(2)},{m.group(3)}x{m.group(4)}x{m.group(6)},occ{m.group(7)}>"
     m = re.search(r"gemm_x3s_kernelILi(\d+)ELi(\d+)E", n)
     if m:
         return f"x3s<{m.group(1)},{m.group(2)}>"

@@ -1,7 +1,8 @@
-"""Trainer fp32 GEMM (k_sgemm.hip, rs_debug_sgemm) vs torch fp32 matmul (rocBLAS / hipBLASLt)
+"""Trainer fp32 GEMM (k_sgemm.hip, rs_debug_sgemm_cfg) vs torch fp32 matmul (rocBLAS / hipBLASLt)
 at the bert-base training shapes: forward / dgrad / wgrad of each Linear and the tied MLM
-decoder, for a 1.1k-token MLM batch and a 5.3k-token RescoreBert batch.
-Usage: python tools/sgemm_bench.py"""
+decoder, for a 1.1k-token MLM batch and a 5.3k-token RescoreBert batch; every tile
+configuration (0: 128x128, 1: 256x128, 2: 256x256) and the shape's pick (-1), interleaved in
+one process.  Usage: python tools/sgemm_bench.py"""
 import ctypes
 import json
 import os
@@ -18,9 +19,9 @@ from asr_rescoring_amd import _lib  # noqa: E402
 
 def main():
     lib = _lib.load()
-    fn = lib.rs_debug_sgemm
+    fn = lib.rs_debug_sgemm_cfg
     fn.restype = ctypes.c_int
-    fn.argtypes = [ctypes.c_int] * 3 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
+    fn.argtypes = [ctypes.c_int] * 4 + [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int,
                                         ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     st = torch.cuda.current_stream().cuda_stream
 
@@ -34,7 +35,9 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / reps
-    tot_mine = tot_ref = 0.0
+    CFGS = (-1, 0, 1, 2, 3, 4)
+    tot = {c: 0.0 for c in CFGS}
+    tot_ref = 0.0
     for T in (1100, 5300):
         for (O, I) in [(2304, 768), (768, 768), (3072, 768), (768, 3072), (21128, 768)]:
             if O == 21128 and T > 2000:
@@ -46,20 +49,30 @@ def main():
             dX = torch.empty(T, I, device="cuda")
             dW = torch.empty(O, I, device="cuda")
             for form, mine, ref in [
-                ("fwd", lambda: fn(T, O, I, X.data_ptr(), I, 1, W.data_ptr(), I, 1, Y.data_ptr(), O, 0, st),
+                ("fwd", lambda c: fn(c, T, O, I, X.data_ptr(), I, 1, W.data_ptr(), I, 1, Y.data_ptr(), O, 0, st),
                  lambda: torch.matmul(X, W.t(), out=Y)),
-                ("dgrad", lambda: fn(T, I, O, dY.data_ptr(), O, 1, W.data_ptr(), I, 0, dX.data_ptr(), I, 0, st),
+                ("dgrad", lambda c: fn(c, T, I, O, dY.data_ptr(), O, 1, W.data_ptr(), I, 0, dX.data_ptr(), I, 0, st),
                  lambda: torch.matmul(dY, W, out=dX)),
-                ("wgrad", lambda: fn(O, I, T, dY.data_ptr(), O, 0, X.data_ptr(), I, 0, dW.data_ptr(), I, 0, st),
+                ("wgrad", lambda c: fn(c, O, I, T, dY.data_ptr(), O, 0, X.data_ptr(), I, 0, dW.data_ptr(), I, 0, st),
                  lambda: torch.matmul(dY.t(), X, out=dW))]:
-                a, b = timed(mine), timed(ref)
                 fl = 2.0 * T * O * I
-                tot_mine += a
+                ms = {c: [] for c in CFGS}
+                mr = []
+                for _ in range(3):                       # interleaved rounds, median
+                    for c in CFGS:
+                        ms[c].append(timed(lambda: mine(c)))
+                    mr.append(timed(ref))
+                med = {c: sorted(v)[1] for c, v in ms.items()}
+                b = sorted(mr)[1]
+                for c in CFGS:
+                    tot[c] += med[c]
                 tot_ref += b
-                print(json.dumps({"tokens": T, "out": O, "in": I, "form": form, "ms_native": round(a, 4),
-                                  "ms_torch": round(b, 4), "tflops_native": round(fl / a / 1e9, 1),
+                print(json.dumps({"tokens": T, "out": O, "in": I, "form": form, "ms_torch": round(b, 4),
+                                  "ms_pick": round(med[-1], 4), "ms_cfg": [round(med[c], 4) for c in CFGS[1:]],
+                                  "tflops_pick": round(fl / med[-1] / 1e9, 1),
                                   "tflops_torch": round(fl / b / 1e9, 1)}), flush=True)
-    print(json.dumps({"total_ms_native": round(tot_mine, 3), "total_ms_torch": round(tot_ref, 3)}))
+    print(json.dumps({"total_ms_pick": round(tot[-1], 3), "total_ms_cfg": [round(tot[c], 3) for c in CFGS[1:]],
+                      "total_ms_torch": round(tot_ref, 3), "pick_vs_torch": round(tot_ref / tot[-1], 3)}))
 
 
 if __name__ == "__main__":
