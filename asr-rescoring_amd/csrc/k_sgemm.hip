@@ -43,6 +43,26 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t sg_rsrc(const float* p, unsign
     return __builtin_amdgcn_make_buffer_rsrc((void*)p, (short)0, (int)bytes, 0x00020000);
 }
 
+// Workgroup -> (split z, output tile) with an XCD-aware bijective remap (MI355X_MICROARCH:
+// blocks b and b + 8 share an XCD): each XCD takes a contiguous range of the work list, and
+// inside a split the tiles go in groups of 8 row panels walked column by column, so the
+// ~64 workgroups an XCD runs at once share 8 A panels and 8 B panels in its L2 instead of
+// touching every panel of the operands (the row-major grid dealt every tile row's column
+// tiles to all eight XCDs).
+__device__ __forceinline__ void sg_tile(int tiles_m, int tiles_n, int& tm, int& tn, int& z) {
+    const int nwg = gridDim.x, b = blockIdx.x;
+    const int xcd = b & 7, pos = b >> 3, q = nwg >> 3, r = nwg & 7;
+    const int w = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+    const int per = tiles_m * tiles_n;
+    z = w / per;
+    const int t = w - z * per;
+    constexpr int GM = 8;
+    const int g = t / (GM * tiles_n), loc = t - g * GM * tiles_n;
+    const int gm = min(GM, tiles_m - g * GM);
+    tn = loc / gm;
+    tm = g * GM + (loc - tn * gm);
+}
+
 // One operand's image of R rows × BK: its DMA source for this wave's pieces of a K-step (1 KiB
 // each; NP of them) and its fragment reads.  rows: operand rows (M or N) in [0, rows); k in
 // [kb, ke).  KC image: [R][BK] floats (rows of 4 BK bytes = NCH 16-B chunks), chunk c of row r
@@ -123,7 +143,7 @@ struct SgOperand {
     }
 };
 
-// C[M][N] (+)= A·B over k in [z·kc, min(K, (z+1)·kc)) for split z = blockIdx.z.
+// C[M][N] (+)= A·B over k in [z·kc, min(K, (z+1)·kc)) for split z (sg_tile).
 // ws == nullptr: C = acc (+ C when accum).  Otherwise the partial goes to ws[z][M][N].
 // Tile BM × BN × BK, waves of TM × 64 (TM/32 × 2 MFMA tiles of 32×32), OCC workgroups per CU.
 template <bool AKC, bool BKC, int BM, int BN, int TM, int BK, int OCC>
@@ -137,8 +157,10 @@ sgemm_dma_kernel(const float* __restrict__ A, int lda, const float* __restrict__
     __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-    const int kb = blockIdx.z * kc, ke = min(K, kb + kc);
+    int tm, tn, z;
+    sg_tile((M + BM - 1) / BM, (N + BN - 1) / BN, tm, tn, z);
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kb = z * kc, ke = min(K, kb + kc);
     const int wm = (wave % WM) * TM, wn = (wave / WM) * 64;
     const int h = lane >> 5, c = lane & 31;
 
@@ -189,7 +211,7 @@ sgemm_dma_kernel(const float* __restrict__ A, int lda, const float* __restrict__
     }
 
     // D map of the 32x32 forms: column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
-    float* P = ws ? ws + (size_t)blockIdx.z * M * N : nullptr;
+    float* P = ws ? ws + (size_t)z * M * N : nullptr;
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -231,8 +253,10 @@ sgemm_pipe_kernel(const float* __restrict__ A, int lda, const float* __restrict_
     __shared__ __attribute__((aligned(16))) char smem[3 * STAGE];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-    const int kb = blockIdx.z * kc, ke = min(K, kb + kc);
+    int tm, tn, z;
+    sg_tile((M + BM - 1) / BM, (N + BN - 1) / BN, tm, tn, z);
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kb = z * kc, ke = min(K, kb + kc);
     const int nt = (ke - kb + BK - 1) / BK;
     const int wm = (wave % WM) * TM, wn = (wave / WM) * 64;
     const int h = lane >> 5, c = lane & 31;
@@ -291,7 +315,7 @@ sgemm_pipe_kernel(const float* __restrict__ A, int lda, const float* __restrict_
         if (t + 1 < nt) step(t + 1, ga, gb, fa, fb);
     }
 
-    float* P = ws ? ws + (size_t)blockIdx.z * M * N : nullptr;
+    float* P = ws ? ws + (size_t)z * M * N : nullptr;
 #pragma unroll
     for (int i = 0; i < MT; ++i)
 #pragma unroll
@@ -346,21 +370,40 @@ int sg_splits(int cfg, int M, int N, int K, int* kc) {
     const SgCfg& g = kSgCfg[cfg];
     const int tiles = ((M + g.bm - 1) / g.bm) * ((N + g.bn - 1) / g.bn);
     const int steps = (K + g.bk - 1) / g.bk;
-    int splits = 1;
-    // up to ~target workgroups; each split costs a write + read of M·N partials.
-    // RS_SGEMM_SPLIT_WG overrides the workgroup target (A/B knob).
-    static const int target_env = [] {
-        const char* v = getenv("RS_SGEMM_SPLIT_WG");
+    // Split K so the work list fills the chip in whole rounds: the occ workgroups a CU holds run
+    // in about the time of one (measured: a CU with two resident 128×128 tiles finishes them as
+    // fast as one alone), so the time is ~ rounds × K-steps per workgroup, rounds =
+    // ceil(tiles · splits / (CUs · occ)).  Each split also writes and re-reads an M·N partial:
+    // a quarter K-step per extra split breaks ties towards fewer.  RS_SGEMM_SPLITS forces a
+    // split count (A/B knob).
+    static const int forced = [] {
+        const char* v = getenv("RS_SGEMM_SPLITS");
         return v ? std::max(1, atoi(v)) : 0;
     }();
-    const int target = target_env ? target_env : 256 * g.occ;
-    if (tiles < target) splits = std::max(1, std::min(std::min((target + tiles - 1) / tiles, steps / 4), 16));
+    const long long slots = 256ll * g.occ;
+    int splits = 1;
+    if (forced) {
+        splits = std::min(forced, std::max(1, steps));
+    } else {
+        double best = 1e30;
+        for (int sp = 1; sp <= 16 && sp <= std::max(1, steps / 4); ++sp) {
+            const long long rounds = ((long long)tiles * sp + slots - 1) / slots;
+            const double cost = (double)rounds * ((steps + sp - 1) / sp) + 0.25 * (sp - 1);
+            if (cost < best) {
+                best = cost;
+                splits = sp;
+            }
+        }
+    }
     const int per = (steps + splits - 1) / splits;
     *kc = per * g.bk;
     return (steps + per - 1) / per;
 }
 
-// RS_SGEMM_CFG=0/1/2 forces a tile configuration (A/B knob); default: by shape
+// RS_SGEMM_CFG=0..4 forces a tile configuration (A/B knob).  Default cfg 0 (128×128, BK 32,
+// two workgroups per CU): the lowest total over the trainer's shape set (tools/sgemm_bench.py);
+// the others win single shapes by 5–15%, not enough to justify a shape table whose choice
+// would also change the split-K order (and so the bits) from one batch shape to the next.
 int sg_pick(int M, int N, int K) {
     static const int forced = [] {
         const char* v = getenv("RS_SGEMM_CFG");
@@ -368,7 +411,7 @@ int sg_pick(int M, int N, int K) {
     }();
     if (forced >= 0 && forced < kSgNCfg) return forced;
     (void)M; (void)N; (void)K;
-    return 1;
+    return 0;
 }
 
 }  // namespace
@@ -409,7 +452,7 @@ static hipError_t sg_run(int cfg, int M, int N, int K, const float* A, int lda, 
         P = ws;
     }
     const SgCfg& g = kSgCfg[cfg];
-    const dim3 grid((N + g.bn - 1) / g.bn, (M + g.bm - 1) / g.bm, splits);
+    const dim3 grid(((N + g.bn - 1) / g.bn) * ((M + g.bm - 1) / g.bm) * splits);   // sg_tile remaps
 #define SG_LAUNCH(KER, AK, BK_, BM_, BN_, TM_, KB_, OCC_)                                                    \
     hipLaunchKernelGGL((KER<AK, BK_, BM_, BN_, TM_, KB_, OCC_>), grid, dim3((BM_ / TM_) * (BN_ / 64) * 64), 0, s, \
                        A, lda, B, ldb, C, ldc, M, N, K, kc, accum, P)
