@@ -21,6 +21,9 @@ enum EpiKind {
     EPI_BIAS_F32 = 5,   // out32 = acc + bias                      (QKV in the fp16x3 precision mode)
     EPI_RESLN_F32 = 6,  // out32 = acc + bias + LN(res32)          (same, residual kept pre-LN:
                         //   LN rebuilt from res_stats/res_g/res_b; out may alias res)
+    EPI_LNRES_IMG = 7,  // h <- image(LN(acc + bias + h)), h the two-part image in out, in place
+                        //   (split-operand residual blocks; row statistics exchanged between the
+                        //   column tiles of a row panel inside the launch: gemm_x3s_kernel)
 };
 
 struct EpiArgs {
@@ -47,7 +50,18 @@ struct EpiArgs {
     const float2* res_stats0;
     const float* res_g0;
     const float* res_b0;
+    // EPI_LNRES_IMG: LN = (res_g, res_b, ln_eps) over nlog columns; lnx [M/256][N/256][256]
+    // per-tile row statistics (sum, M2), lncnt = lnres_words(M) words zeroed by the launch:
+    // [0] first-tile claims, [2] row-panel claims, [4 + p] arrivals at row panel p, [4 + P + p]
+    // the panel claimed after p (+1); lnerr (sticky, the caller's): set to 1 when a statistics
+    // wait timed out
+    float2* lnx;
+    unsigned* lncnt;
+    unsigned* lnerr;
+    float ln_eps;
+    int diag;              // EPI_LNRES_IMG timing diagnostics (RS_LNFUSE_DIAG; 0 in production)
 };
+inline size_t lnres_words(int m_pad) { return ((size_t)4 + 2 * (m_pad / 256) + 3) / 4 * 4; }
 
 // fp16 operand image of an fp32 activation row with logical width K:
 //   kx == 1: [hi]                          (RS_PREC_FP16)

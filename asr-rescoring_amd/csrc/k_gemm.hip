@@ -1135,7 +1135,10 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     constexpr int REG = BM * RB;                 // one 256-row region: 16 KiB
     constexpr int STAGE = 4 * REG;               // A_hi | A_lo | W_hi | W_lo
     constexpr int NSTORE = EPI == EPI_BIAS_F16 ? 16 : 32;
-    static_assert(EPI == EPI_BIAS_F32 || EPI == EPI_GELU_F16 || EPI == EPI_BIAS_F16, "x3s epilogues");
+    static_assert(EPI == EPI_BIAS_F32 || EPI == EPI_GELU_F16 || EPI == EPI_BIAS_F16 || EPI == EPI_LNRES_IMG,
+                  "x3s epilogues");
+    constexpr bool LNR = EPI == EPI_LNRES_IMG;
+    static_assert(!LNR || ((VAR & 128) != 0 && (VAR & 2) == 0), "the LayerNorm epilogue is written for the 16x16 form");
     extern __shared__ __attribute__((aligned(16))) char smem[];        // the LDS-DMA ring (2 stages)
     // wave-private epilogue slabs: a separate LDS object, so the compiler can tell the slab
     // reads do not alias the LDS-DMA writes in flight (no vmcnt wait before them)
@@ -1147,11 +1150,36 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     const int frow = lane & 31, fh = lane >> 5;
     const int nk = K / BK;
     int t = blockIdx.x;
+    typedef __attribute__((address_space(1))) unsigned gu32;
+    typedef __attribute__((address_space(1))) unsigned long long gu64;
+    if constexpr (LNR) {
+        // first tiles by ticket, in the order workgroups start (the grid is whole row panels and
+        // fits the chip at one per CU): each row panel's column tiles form a gang that stays
+        // together for the launch — after each statistics exchange the gang's last arriver claims
+        // the next row panel for all of them (lnres_epilogue).  A workgroup never holds a tile it
+        // has not started, so no wait can be on a tile whose owner is itself waiting.
+        if (tid == 0) {
+            const unsigned c = __hip_atomic_fetch_add((gu32*)ep.lncnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            *(unsigned*)(slabs + 2048) = c;
+        }
+        __syncthreads();
+        t = (int)*(const unsigned*)(slabs + 2048);
+    }
     if (t >= n_tiles) return;
     if constexpr ((VAR & 262144) != 0) {
         if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
     }
     auto tile_of = [&](int tt, int& m0, int& n0) {
+        if constexpr (LNR) {                      // claim order: a row panel's column tiles in a row
+            m0 = (tt / n_tiles_n) * BM;
+            n0 = (tt - (tt / n_tiles_n) * n_tiles_n) * BM;
+            return;
+        }
+        if constexpr (LNR) {                      // claim order: a row panel's column tiles in a row
+            m0 = (tt / n_tiles_n) * BM;
+            n0 = (tt - (tt / n_tiles_n) * n_tiles_n) * BM;
+            return;
+        }
         const int xcd = tt & 7, pos = tt >> 3, q = n_tiles >> 3, r = n_tiles & 7;
         const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
         const int GM = ep.group_m, n_tiles_m = n_tiles / n_tiles_n, per_group = GM * n_tiles_n;
@@ -1474,14 +1502,19 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                          : "memory");
         }
         // the next tile's stage 0 (into the buffer step nk-2 used) lands while this epilogue runs
-        t += gridDim.x;
-        const bool more = t < n_tiles;
-        if (more) {
-            tile_of(t, m0, n0);
-            set_src(m0, n0);
-            set_rsrc(m0, n0);
-            stage(last ^ 1, 0);
-        }
+        // (LNR: once the claimed index has been shared, inside the epilogue)
+        bool more = false;
+        auto next_tile = [&](int tt) {
+            t = tt;
+            more = t < n_tiles;
+            if (more) {
+                tile_of(t, m0, n0);
+                set_src(m0, n0);
+                set_rsrc(m0, n0);
+                stage(last ^ 1, 0);
+            }
+        };
+        if constexpr (!LNR) next_tile(t + gridDim.x);
         if constexpr (M16) {
             // bias (+ GELU) of row blocks [i0, i1)
             auto finish = [&](int i0, int i1) {
@@ -1497,10 +1530,207 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                             acc16[i][j][e + 1] = v.y;
                         }
             };
+            // EPI_LNRES_IMG: h <- image(LN(acc + bias + h)) over whole rows.  This tile's 256
+            // columns give per-row partials (sum, M2 about the tile's own mean); the column tiles
+            // of a row panel hand them to each other through lnx with 8-B sc1 stores and loads
+            // (MI355X_MICROARCH inter-workgroup visibility, table row 1: every storing wave drains,
+            // one lane adds to the panel's arrival counter behind a barrier and polls it, the other
+            // waves load behind the barrier it then joins), and every tile combines the partials
+            // in column-tile order (Chan's pairwise form), so a row's tiles normalise with
+            // bit-identical statistics.  The poll is bounded: a timeout sets *lnerr (the host
+            // fails the call) instead of hanging the launch.
+            auto lnres_epilogue = [&]() {
+                const int H = ep.nlog, ldc = ep.ldc, ntn = n_tiles_n;
+                const int panel = cm0 / BM, tcol = cn0 / BM;
+                const f16* img = (const f16*)ep.out;
+                const int c0 = cn0 + wn * WTN + 4 * q4;
+                // x = (acc + bias) + h, the residual image h = hi + lo/64 read in the accumulator
+                // layout, four row blocks at a time (as ln_res_img forms it)
+#pragma unroll
+                for (int hh = 0; hh < 2; ++hh) {
+                    half4 rh[4][4], rl[4][4];
+                    const int rskip = (ep.diag & 4) ? 0 : 1;     // diag 4: residual rows of tile row 0
+#pragma unroll
+                    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j) {
+                            const f16* p = img + (size_t)(cm0 + rskip * (wm * WTM + 16 * (4 * hh + ii) + r16)) * ldc + c0 + 16 * j;
+                            rh[ii][j] = *(const half4*)p;
+                            rl[ii][j] = *(const half4*)(p + H);
+                        }
+#pragma unroll
+                    for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+#pragma unroll
+                            for (int e = 0; e < 4; ++e)
+                                acc16[4 * hh + ii][j][e] = (acc16[4 * hh + ii][j][e] + bq[j][e]) +
+                                                           ((float)rh[ii][j][e] + (float)rl[ii][j][e] * X3_DOWN);
+                }
+                // row partials over the wave's 64 columns (lanes l, l^16, l^32, l^48 share a row),
+                // then over the four waves of the row half through their slabs
+                float* red = (float*)(slabs + wave * 4096);
+                auto slab_of = [&](int w2) { return (const float*)(slabs + (wm * WN + w2) * 4096); };
+                float tsum[8], tmean[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    float a = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) a += (acc16[i][j][0] + acc16[i][j][1]) + (acc16[i][j][2] + acc16[i][j][3]);
+                    a += __shfl_xor(a, 16);
+                    a += __shfl_xor(a, 32);
+                    tsum[i] = a;
+                }
+                if (q4 == 0) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) red[16 * i + r16] = tsum[i];
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    float a = 0.f;
+#pragma unroll
+                    for (int w2 = 0; w2 < WN; ++w2) a += slab_of(w2)[16 * i + r16];
+                    tsum[i] = a;
+                    tmean[i] = a * (1.f / BM);
+                }
+                float tm2[8];
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    float q = 0.f;
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const float d = acc16[i][j][e] - tmean[i];
+                            q = __builtin_fmaf(d, d, q);
+                        }
+                    q += __shfl_xor(q, 16);
+                    q += __shfl_xor(q, 32);
+                    tm2[i] = q;
+                }
+                if (q4 == 0) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) red[128 + 16 * i + r16] = tm2[i];
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    float a = 0.f;
+#pragma unroll
+                    for (int w2 = 0; w2 < WN; ++w2) a += slab_of(w2)[128 + 16 * i + r16];
+                    tm2[i] = a;
+                }
+                // publish (sum, M2) of the tile's rows: waves wn == 0, one lane per row
+                float2* xt = ep.lnx + ((size_t)panel * ntn + tcol) * BM + wm * WTM;
+                if (wn == 0 && q4 == 0) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i) {
+                        const unsigned long long v = (unsigned long long)__float_as_uint(tsum[i]) |
+                                                     ((unsigned long long)__float_as_uint(tm2[i]) << 32);
+                        __hip_atomic_store((gu64*)(xt + 16 * i + r16), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // every storing wave drains
+                asm volatile("s_barrier" ::: "memory");
+                if (tid == 0) {
+                    // arrival; the panel's column tiles then move on together (a gang): the last
+                    // arriver claims the next panel for all of them and posts it, each takes the
+                    // column of its arrival rank — the gang's tiles start together, so they also
+                    // reach the next statistics exchange together
+                    const int npanels = n_tiles / ntn;
+                    gu32* pc = (gu32*)(ep.lncnt + 4 + panel);
+                    gu32* pn = (gu32*)(ep.lncnt + 4 + npanels + panel);
+                    const unsigned rank = __hip_atomic_fetch_add(pc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    unsigned np = 0;
+                    if (rank + 1 == (unsigned)ntn) {
+                        np = gridDim.x / ntn +
+                             __hip_atomic_fetch_add((gu32*)ep.lncnt + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(pn, np + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    } else {
+                        // the statistics first (the arrival counter: what orders the partials),
+                        // then the posted panel; diag 1 (timing only, wrong statistics): no wait
+                        unsigned spins = 0;
+                        for (int ph = 0; ph < 2; ++ph) {
+                            for (;;) {
+                                if (ph == 0 && (ep.diag & 1)) break;
+                                const unsigned v = __hip_atomic_load(ph ? pn : pc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                if (ph ? v != 0u : v >= (unsigned)ntn) {
+                                    np = v - 1;
+                                    break;
+                                }
+                                if (ep.diag & 2) __builtin_amdgcn_s_sleep(16);
+                                else __builtin_amdgcn_s_sleep(1);
+                                if (++spins == (1u << 21)) {
+                                    __hip_atomic_store((gu32*)ep.lnerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                    np = (unsigned)npanels;                // give up: leave the launch
+                                    break;
+                                }
+                            }
+                            if (spins >= (1u << 21)) break;
+                        }
+                    }
+                    // to every wave through the ring buffer this tile's last K-step read (no DMA
+                    // enters it before the next tile's first barrier; the slabs are rewritten by
+                    // the store pass below)
+                    *(unsigned*)(smem + last * STAGE) = np * ntn + rank;
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                next_tile((int)*(const volatile unsigned*)(smem + last * STAGE));
+                // combine the panel's partials: lane l does rows l and l + 64 of the row half
+                float2* st2 = (float2*)(slabs + wave * 4096 + 1024);
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int rr = lane + 64 * k;
+                    // (diag 1: the tile's own partials only, as if the row were 256 wide)
+                    const int c_lo = (ep.diag & 1) ? tcol : 0, c_hi = (ep.diag & 1) ? tcol + 1 : ntn;
+                    const float inv_n = (ep.diag & 1) ? 1.f / BM : 1.f / H;
+                    float ts[4], tq[4], tot = 0.f;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        ts[c] = 0.f;
+                        tq[c] = 0.f;
+                        if (c >= c_lo && c < c_hi) {
+                            const unsigned long long v = __hip_atomic_load(
+                                (gu64*)(ep.lnx + ((size_t)panel * ntn + c) * BM + wm * WTM + rr), __ATOMIC_RELAXED,
+                                __HIP_MEMORY_SCOPE_AGENT);
+                            ts[c] = __uint_as_float((unsigned)v);
+                            tq[c] = __uint_as_float((unsigned)(v >> 32));
+                            tot += ts[c];
+                        }
+                    }
+                    const float mean = tot * inv_n;
+                    float m2 = 0.f;
+#pragma unroll
+                    for (int c = 0; c < 4; ++c) {
+                        if (c >= c_lo && c < c_hi) {
+                            const float d = ts[c] * (1.f / BM) - mean;
+                            m2 += __builtin_fmaf((float)BM * d, d, tq[c]);
+                        }
+                    }
+                    st2[rr] = make_float2(mean, 1.0f / sqrtf(__builtin_fmaf(m2, inv_n, ep.ln_eps)));
+                }
+                f32x4 gq[4], bb[4];                      // LayerNorm weight / bias of the lane's columns
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    gq[j] = *(const f32x4*)(ep.res_g + c0 + 16 * j);
+                    bb[j] = *(const f32x4*)(ep.res_b + c0 + 16 * j);
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const float2 st = st2[16 * i + r16];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) acc16[i][j][e] = ln_apply(acc16[i][j][e], st, gq[j][e], bb[j][e]);
+                }
+            };
             // VAR 512 (fp16-image epilogues): each row-block pair's bias + GELU right before its
             // slab pass, so that VALU work overlaps the previous pair's LDS and global stores
-            constexpr bool LATE = (VAR & 512) != 0 && EPI != EPI_BIAS_F32 && (VAR & 2) == 0;
-            if constexpr (!LATE) finish(0, 8);
+            constexpr bool LATE = (VAR & 512) != 0 && EPI != EPI_BIAS_F32 && (VAR & 2) == 0 && !LNR;
+            if constexpr (LNR) lnres_epilogue();
+            else if constexpr (!LATE) finish(0, 8);
             if constexpr ((VAR & 2) != 0) {      // diagnostic: no epilogue stores (acc kept alive)
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
@@ -1544,8 +1774,8 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                     }
             } else {
                 // fp16 image(s) in 32 x 64 slab blocks (row blocks 2 i2 + a, all four column
-                // blocks): image 0 = hi, image 1 (GELU, two-part) = lo*64
-                constexpr int NIMG = EPI == EPI_GELU_F16 ? 2 : 1;
+                // blocks): image 0 = hi, image 1 (GELU / LayerNorm, two-part) = lo*64
+                constexpr int NIMG = EPI == EPI_GELU_F16 || LNR ? 2 : 1;
                 // row-block pair outermost: its accumulators die after both images are out
 #pragma unroll
                 for (int i2 = 0; i2 < 4; ++i2) {
@@ -1681,7 +1911,18 @@ hipError_t launch_x3s(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
     }
     const int ntn = N_pad / 256, n_tiles = (M_pad / 256) * ntn;
     const int cus = n_cus() / 8 * 8;
-    const int grid = n_tiles <= cus ? n_tiles : cus;
+    int grid = n_tiles <= cus ? n_tiles : cus;
+    if constexpr (EPI == EPI_LNRES_IMG) {
+        // the image is rewritten in place over whole rows (N_pad = the hidden size, <= 4 column
+        // tiles); the claim / arrival words start at zero every launch
+        if (!ep.lnx || !ep.lncnt || !ep.lnerr || N_pad > 1024 || ep.nlog != N_pad || ep.ldc != 2 * N_pad)
+            return hipErrorInvalidValue;
+        // whole row panels per round: the initial tiles form complete gangs (every workgroup
+        // resident at one per CU)
+        grid = std::min(n_tiles, cus / ntn * ntn);
+        hipError_t e = hipMemsetAsync(ep.lncnt, 0, lnres_words(M_pad) * 4, st);
+        if (e != hipSuccess) return e;
+    }
     static const int gm_env = getenv("RS_GEMM_GROUP_M_X3S") ? atoi(getenv("RS_GEMM_GROUP_M_X3S")) : 0;
     EpiArgs e2 = ep;
     e2.group_m = gm_env > 0 ? gm_env : 8;
@@ -1877,6 +2118,8 @@ hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_p
         case EPI_BIAS_F16:
             return mf32 ? launch_x3s<EPI_BIAS_F16, V32>(A, W, M_pad, N_pad, K, ep, st, ldw)
                         : launch_x3s<EPI_BIAS_F16, V>(A, W, M_pad, N_pad, K, ep, st, ldw);
+        case EPI_LNRES_IMG:
+            return launch_x3s<EPI_LNRES_IMG, V>(A, W, M_pad, N_pad, K, ep, st, ldw);
     }
     return hipErrorInvalidValue;
 }

@@ -83,6 +83,8 @@ struct rs_model {
     int kx = 1;                 // fp16 operand image width (1: fp16, 3: fp16x3)
     DevBuf xst, h16, t32, qkv, ctx, inter;   // xst: (mean, rstd) of the pre-LN rows in t32
     DevBuf xst1;                // statistics of the post-attention stream (deferred residual)
+    DevBuf lnx, lncnt, lnerr;   // EPI_LNRES_IMG: per-tile row statistics, claim / arrival words,
+                                // sticky statistics-wait timeout flag
     DevBuf ctxq, resq, tq32, hq32, hq16, interq, lab, llog, part, rowlp_tmp;
     DevBuf meta, hypoff;
     f16* emb_dst = nullptr;     // MODE_EMB output (rs_token_embed / rs_bertscore_recall)
@@ -172,13 +174,20 @@ template <class T>
 int check_finite(rs_model* m, hipStream_t st, const T* p, size_t n, const char* what) {
     if (n == 0) return RS_OK;
     HIPTRY(m->flag.ensure(4));
-    if (!m->pinned_flag) HIPTRY(hipHostMalloc((void**)&m->pinned_flag, 4, hipHostMallocDefault));
+    if (!m->pinned_flag) HIPTRY(hipHostMalloc((void**)&m->pinned_flag, 8, hipHostMallocDefault));
     HIPTRY(hipMemsetAsync(m->flag.p, 0, 4, st));
     const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 2048);
     hipLaunchKernelGGL(nonfinite_kernel<T>, dim3(blocks), dim3(256), 0, st, p, n, m->flag.as<int>());
     HIPTRY(hipGetLastError());
     HIPTRY(hipMemcpyAsync(m->pinned_flag, m->flag.p, 4, hipMemcpyDeviceToHost, st));
+    m->pinned_flag[1] = 0;
+    if (m->lnerr.p) HIPTRY(hipMemcpyAsync(m->pinned_flag + 1, m->lnerr.p, 4, hipMemcpyDeviceToHost, st));
     HIPTRY(hipStreamSynchronize(st));
+    if (m->pinned_flag[1]) {
+        HIPTRY(hipMemset(m->lnerr.p, 0, 4));
+        return fail(RS_EHIP, "a residual-LayerNorm GEMM timed out waiting for its row statistics "
+                                  "(set RS_LNFUSE=0 to use the separate LayerNorm pass)");
+    }
     if (*m->pinned_flag)
         return fail(RS_EUNSUP, std::string("non-finite ") + what +
                                    ": an activation left the fp16 range of the operand images (|x| > 65504); "
@@ -200,6 +209,10 @@ int reserve_impl(rs_model* m, int64_t max_rows) {
     const size_t kx = m->kx;
     HIPTRY(m->xst.ensure(M * sizeof(float2)));
     HIPTRY(m->xst1.ensure(M * sizeof(float2)));
+    HIPTRY(m->lnx.ensure(M * 4 * sizeof(float2)));            // <= 4 column tiles per row
+    HIPTRY(m->lncnt.ensure(lnres_words((int)M) * 4));
+    HIPTRY(m->lnerr.ensure(16));
+    HIPTRY(hipMemset(m->lnerr.p, 0, 16));
     HIPTRY(m->h16.ensure(M * H * 2 * kx));
     HIPTRY(m->t32.ensure(M * H * 4));
     HIPTRY(m->qkv.ensure(M * 3 * H * (kx == 3 ? 4 : 2)));
@@ -325,6 +338,13 @@ bool x3s_imgres_on() {
     const char* e = getenv("RS_X3S_IMGRES");
     return !(e && !strcmp(e, "0"));
 }
+// RS_LNFUSE=1 (image-held residual; default 0): the residual add + LayerNorm of both blocks run
+// in the O-projection / BertOutput GEMM epilogues (EPI_LNRES_IMG: full rows through an in-launch
+// exchange of row statistics) instead of as ln_res_img passes.  Read per call.
+bool lnfuse_on(const rs_bert_cfg& cf) {
+    const char* e = getenv("RS_LNFUSE");
+    return e && !strcmp(e, "1") && cf.hidden % 256 == 0 && cf.hidden <= 1024;
+}
 
 // Runs the encoder + head over sequences [c.s0, c.s1) (one chunk).
 int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, const Chunk& c,
@@ -338,6 +358,7 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
     const bool x3s = kx == 3 && x3s_on(cf);   // split-operand GEMMs: full-row images are two-part
     const int kxf = x3s ? 2 : kx;             // width factor of the full-row operand images
     const bool imgres = x3s && x3s_imgres_on();  // residual stream = the two-part image in h16
+    const bool lnfuse = imgres && lnfuse_on(cf);  // ... closed in the residual GEMMs' epilogues
     float2* xst = m->xst.as<float2>();
     f16* h16 = m->h16.as<f16>();
     float* t32 = m->t32.as<float>();     // residual stream, pre-LN fp32 (LN rebuilt from xst)
@@ -427,18 +448,35 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
                 HIPTRY(launch_attention_full(qkv, true, sm, c.s0, c.s1, 0, H, nh, ctx, 2, st, uq, c.max_len));
             }
             float* o32 = (float*)qkv;
-            ep = EpiArgs{}; ep.bias = L.bo; ep.out = o32; ep.ldc = H;
-            if (int r = gx(RS_K_OPROJ, EPI_BIAS_F32, ctx, L.wo, 3 * H, rows, H, H, ep, H)) return r;
-            {
+            // residual block: h16 <- image(LN(A·Wᵀ + b + h16)) in the GEMM epilogue (lnfuse), or
+            // an fp32 GEMM output closed by a separate residual + LayerNorm pass
+            auto lnres_ep = [&](const float* bias, const float* g, const float* be) {
+                EpiArgs e{};
+                e.bias = bias; e.out = h16; e.ldc = 2 * H; e.nlog = H; e.res_g = g; e.res_b = be;
+                e.ln_eps = cf.ln_eps; e.lnx = m->lnx.as<float2>(); e.lncnt = m->lncnt.as<unsigned>();
+                e.lnerr = m->lnerr.as<unsigned>();
+                static const int diag = getenv("RS_LNFUSE_DIAG") ? atoi(getenv("RS_LNFUSE_DIAG")) : 0;
+                e.diag = diag;
+                return e;
+            };
+            if (lnfuse) {
+                if (int r = gx(RS_K_OPROJ, EPI_LNRES_IMG, ctx, L.wo, 3 * H, rows, H, H, lnres_ep(L.bo, L.g1, L.be1), H))
+                    return r;
+            } else {
+                ep = EpiArgs{}; ep.bias = L.bo; ep.out = o32; ep.ldc = H;
+                if (int r = gx(RS_K_OPROJ, EPI_BIAS_F32, ctx, L.wo, 3 * H, rows, H, H, ep, H)) return r;
                 ProfScope ps(m, st, RS_K_OTHER, 0);
                 if (imgres) HIPTRY(launch_ln_res_img(h16, o32, rows, L.g1, L.be1, cf.ln_eps, H, st));
                 else HIPTRY(launch_ln_res32(t32, xst, xst, pg, pb, o32, rows, L.g1, L.be1, cf.ln_eps, H, h16, 2, st));
             }
             ep = EpiArgs{}; ep.bias = L.b1; ep.out = inter; ep.ldc = 2 * F; ep.kx = 2; ep.nlog = F;
             if (int r = gx(RS_K_FFN1, EPI_GELU_F16, h16, L.w1, 3 * H, rows, F, H, ep, F)) return r;
-            ep = EpiArgs{}; ep.bias = L.b2; ep.out = o32; ep.ldc = H;
-            if (int r = gx(RS_K_FFN2, EPI_BIAS_F32, inter, L.w2, 3 * F, rows, H, F, ep, H)) return r;
-            {
+            if (lnfuse) {
+                if (int r = gx(RS_K_FFN2, EPI_LNRES_IMG, inter, L.w2, 3 * F, rows, H, F, lnres_ep(L.b2, L.g2, L.be2), H))
+                    return r;
+            } else {
+                ep = EpiArgs{}; ep.bias = L.b2; ep.out = o32; ep.ldc = H;
+                if (int r = gx(RS_K_FFN2, EPI_BIAS_F32, inter, L.w2, 3 * F, rows, H, F, ep, H)) return r;
                 ProfScope ps(m, st, RS_K_OTHER, 0);
                 if (imgres) HIPTRY(launch_ln_res_img(h16, o32, rows, L.g2, L.be2, cf.ln_eps, H, st));
                 else HIPTRY(launch_ln_res32(t32, xst, xst, L.g1, L.be1, o32, rows, L.g2, L.be2, cf.ln_eps, H, h16, 2, st));
@@ -983,7 +1021,8 @@ void rs_model_destroy(rs_model* m) {
     for (void* p : m->allocs) (void)hipFree(p);
     for (DevBuf* b : {&m->xst, &m->xst1, &m->h16, &m->t32, &m->qkv, &m->ctx, &m->inter, &m->ctxq, &m->resq,
                       &m->tq32, &m->hq32, &m->hq16, &m->interq, &m->lab, &m->llog, &m->part,
-                      &m->rowlp_tmp, &m->meta, &m->hypoff, &m->emb, &m->plan, &m->flag})
+                      &m->rowlp_tmp, &m->meta, &m->hypoff, &m->emb, &m->plan, &m->flag, &m->lnx, &m->lncnt,
+                      &m->lnerr})
         b->release();
     if (m->pinned) (void)hipHostFree(m->pinned);
     if (m->pinned_plan) (void)hipHostFree(m->pinned_plan);

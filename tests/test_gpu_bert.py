@@ -99,13 +99,16 @@ def test_pll_tiny_golden(pll_tiny, golden_dir):
     assert rel_err(rows.cpu().numpy(), g["row_lp"]).max() < REL
 
 
-@pytest.mark.parametrize("x3s", ["1", "0"])
-def test_pll_fp16x3_golden(w_base, golden_dir, monkeypatch, x3s):
+@pytest.mark.parametrize("x3s,lnfuse", [("1", "1"), ("1", "0"), ("0", "1")])
+def test_pll_fp16x3_golden(w_base, golden_dir, monkeypatch, x3s, lnfuse):
     """Split-fp16 (x3) precision mode: fp32-level accuracy from fp16 MFMA, with the split-operand
     GEMMs (RS_X3S=1, default: two-part images, three products in registers) and with the
-    K-concatenated three-part form (RS_X3S=0)."""
+    K-concatenated three-part form (RS_X3S=0); split-operand layers with the residual +
+    LayerNorm in the O-projection / BertOutput epilogues (RS_LNFUSE=1, default) and as separate
+    ln_res_img passes (RS_LNFUSE=0)."""
     from asr_rescoring_amd.scorer import PLLScorer
     monkeypatch.setenv("RS_X3S", x3s)
+    monkeypatch.setenv("RS_LNFUSE", lnfuse)
     g = _load(golden_dir, "pll_base.npz")
     s = PLLScorer(w_base, BERT_BASE, device=0, max_rows=4096, precision="fp16x3")
     pll, rows = s.score_nbest(g["tokens"], g["hyp_off"], return_rows=True)
@@ -114,6 +117,30 @@ def test_pll_fp16x3_golden(w_base, golden_dir, monkeypatch, x3s):
     # range (common.h put_split); 2e-5 / 2e-5 before, when the f16 MFMA flushed them
     assert rel_err(pll.cpu().numpy(), g["pll"]).max() < 1e-6
     assert rel_err(rows.cpu().numpy(), g["row_lp"]).max() < 5e-6
+
+
+@pytest.mark.parametrize("max_rows", [4096, 65536, 262144])
+def test_lnfuse_matches_separate_pass(w_base, monkeypatch, max_rows):
+    """Residual + LayerNorm in the GEMM epilogue (EPI_LNRES_IMG: each 256-column tile's row
+    partials exchanged between the row panel's column tiles inside the launch) against the
+    separate ln_res_img pass, on enough rows that every launch has more tiles than the chip has
+    workgroups (tiles claimed as workgroups free up; up to 3072 tiles per launch at 262144 rows,
+    the bench's chunk) and on many small launches: the same residual sum, statistics combined in another order —
+    scores within 1e-6 relative — and bitwise reproducible from call to call."""
+    from asr_rescoring_amd.scorer import PLLScorer
+    nb = D.synthetic_nbest(12, 50, seed=11, vocab=BERT_BASE.vocab, len_lo=4, len_hi=60)
+    s = PLLScorer(w_base, BERT_BASE, device=0, max_rows=max_rows, precision="fp16x3")
+    try:
+        monkeypatch.setenv("RS_LNFUSE", "1")
+        a = s.score(nb)
+        a2 = s.score(nb)
+        monkeypatch.setenv("RS_LNFUSE", "0")
+        b = s.score(nb)
+    finally:
+        s.close()
+    assert np.array_equal(a, a2)
+    assert not np.array_equal(a, b)          # the two paths really differ in the statistics' order
+    assert rel_err(a, b).max() < 1e-6, rel_err(a, b).max()
 
 
 def test_cls_golden(w_base, w_tiny, golden_dir):

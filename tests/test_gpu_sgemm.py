@@ -75,7 +75,7 @@ CASES = [("nt", 1037, 2304, 768), ("nt", 1037, 768, 3072), ("nt", 301, 21128, 76
 
 @pytest.mark.parametrize("form,M,N,K", CASES)
 @pytest.mark.parametrize("accum", [0, 1])
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6])
 def test_sgemm_forms_vs_float64(sgemm, form, M, N, K, accum, cfg):
     """Every tile configuration (k_sgemm.hip kSgCfg) on every form and edge."""
     g = torch.Generator(device="cuda").manual_seed(M * 7 + N + K)

@@ -1,0 +1,15 @@
+# fused residual + LayerNorm with gang scheduling: parity, then interleaved A/B
+set -o pipefail
+O=gpurun_out/r3k; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_gpu_bert.py -x -q --timeout 240 --timeout-method thread -k "lnfuse or fp16x3_golden or range_guard or dedup" > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
+tail -2 $O/tests.log
+run() {
+  local tag=$1; shift
+  env "$@" timeout -k 10 300 python -u bench.py --utts 100 --steps 2 --warmup 1 --cpu-seconds 0 --fp16-steps 0 > $O/$tag.json 2> $O/$tag.err || { tail -20 $O/$tag.err; return 1; }
+  python3 -c "import json; d=json.loads(open('$O/$tag.json').read().strip().splitlines()[-1]); print('$tag', d['value'], d['kinds_ms'])"
+}
+for r in 1 2; do
+  run off_r$r RS_LNFUSE=0 || exit 1
+  run on_r$r RS_LNFUSE=1 || exit 1
+  run nores_r$r RS_LNFUSE=1 RS_LNFUSE_DIAG=4 || exit 1
+done
