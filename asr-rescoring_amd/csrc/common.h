@@ -50,18 +50,18 @@ struct EpiArgs {
     const float2* res_stats0;
     const float* res_g0;
     const float* res_b0;
-    // EPI_LNRES_IMG: LN = (res_g, res_b, ln_eps) over nlog columns; lnx [M/256][N/256][256]
-    // per-tile row statistics (sum, M2), lncnt = lnres_words(M) words zeroed by the launch:
-    // [0] first-tile claims, [2] row-panel claims, [4 + p] arrivals at row panel p, [4 + P + p]
-    // the panel claimed after p (+1); lnerr (sticky, the caller's): set to 1 when a statistics
-    // wait timed out
-    float2* lnx;
+    // EPI_LNRES_IMG: LN = (res_g, res_b, ln_eps) over nlog columns; lnx: lnres_granules(M)
+    // 8-B granules [M/256][N/256][256][2] {ln_tag, sum | M2} (zeroed once by the owner); lncnt:
+    // 4 words, [0] the first-tile ticket (zeroed by the launch); lnerr (sticky, the caller's):
+    // set to 1 when a statistics wait timed out; ln_tag: set by the launch
+    void* lnx;
     unsigned* lncnt;
     unsigned* lnerr;
+    unsigned ln_tag;
     float ln_eps;
     int diag;              // EPI_LNRES_IMG timing diagnostics (RS_LNFUSE_DIAG; 0 in production)
 };
-inline size_t lnres_words(int m_pad) { return ((size_t)4 + 2 * (m_pad / 256) + 3) / 4 * 4; }
+inline size_t lnres_granules(int m_pad) { return (size_t)m_pad * 4 * 2; }     // <= 4 column tiles
 
 // fp16 operand image of an fp32 activation row with logical width K:
 //   kx == 1: [hi]                          (RS_PREC_FP16)

@@ -1153,11 +1153,11 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     typedef __attribute__((address_space(1))) unsigned gu32;
     typedef __attribute__((address_space(1))) unsigned long long gu64;
     if constexpr (LNR) {
-        // first tiles by ticket, in the order workgroups start (the grid is whole row panels and
-        // fits the chip at one per CU): each row panel's column tiles form a gang that stays
-        // together for the launch — after each statistics exchange the gang's last arriver claims
-        // the next row panel for all of them (lnres_epilogue).  A workgroup never holds a tile it
-        // has not started, so no wait can be on a tile whose owner is itself waiting.
+        // first tiles by ticket, in the order workgroups start: the grid is whole row panels and
+        // fits the chip at one workgroup per CU, so each row panel's column tiles form a gang of
+        // resident workgroups, and a gang walks the panels p, p + G, p + 2G, ... (G = gangs) with
+        // each member keeping its column: t += gridDim.x.  The statistics exchange
+        // (lnres_epilogue) is within a gang only, whose members all run the same panel sequence.
         if (tid == 0) {
             const unsigned c = __hip_atomic_fetch_add((gu32*)ep.lncnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             *(unsigned*)(slabs + 2048) = c;
@@ -1170,12 +1170,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
     }
     auto tile_of = [&](int tt, int& m0, int& n0) {
-        if constexpr (LNR) {                      // claim order: a row panel's column tiles in a row
-            m0 = (tt / n_tiles_n) * BM;
-            n0 = (tt - (tt / n_tiles_n) * n_tiles_n) * BM;
-            return;
-        }
-        if constexpr (LNR) {                      // claim order: a row panel's column tiles in a row
+        if constexpr (LNR) {                      // row panel t / ntn, column tile t % ntn
             m0 = (tt / n_tiles_n) * BM;
             n0 = (tt - (tt / n_tiles_n) * n_tiles_n) * BM;
             return;
@@ -1502,7 +1497,6 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                          : "memory");
         }
         // the next tile's stage 0 (into the buffer step nk-2 used) lands while this epilogue runs
-        // (LNR: once the claimed index has been shared, inside the epilogue)
         bool more = false;
         auto next_tile = [&](int tt) {
             t = tt;
@@ -1514,7 +1508,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 stage(last ^ 1, 0);
             }
         };
-        if constexpr (!LNR) next_tile(t + gridDim.x);
+        next_tile(t + gridDim.x);
         if constexpr (M16) {
             // bias (+ GELU) of row blocks [i0, i1)
             auto finish = [&](int i0, int i1) {
@@ -1531,32 +1525,36 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         }
             };
             // EPI_LNRES_IMG: h <- image(LN(acc + bias + h)) over whole rows.  This tile's 256
-            // columns give per-row partials (sum, M2 about the tile's own mean); the column tiles
-            // of a row panel hand them to each other through lnx with 8-B sc1 stores and loads
-            // (MI355X_MICROARCH inter-workgroup visibility, table row 1: every storing wave drains,
-            // one lane adds to the panel's arrival counter behind a barrier and polls it, the other
-            // waves load behind the barrier it then joins), and every tile combines the partials
-            // in column-tile order (Chan's pairwise form), so a row's tiles normalise with
-            // bit-identical statistics.  The poll is bounded: a timeout sets *lnerr (the host
-            // fails the call) instead of hanging the launch.
+            // columns give per-row partials (sum, M2 about the tile's own mean); the gang (the row
+            // panel's column tiles) hands them to each other as tagged 8-B granules {launch tag,
+            // value} written by single sc1 stores and polled with sc1 loads until every tag is
+            // this launch's (cdna_hip_programming §6 Guideline 16, R2: the data is the flag — no
+            // drain, counter or fence), and every tile combines the partials in column-tile order
+            // (Chan's pairwise form), so a row's tiles normalise with bit-identical statistics.
+            // The poll is bounded: a timeout sets *lnerr (the host fails the call) instead of
+            // hanging the launch.
             auto lnres_epilogue = [&]() {
                 const int H = ep.nlog, ldc = ep.ldc, ntn = n_tiles_n;
                 const int panel = cm0 / BM, tcol = cn0 / BM;
+                const unsigned long long tag = (unsigned long long)ep.ln_tag << 32;
                 const f16* img = (const f16*)ep.out;
                 const int c0 = cn0 + wn * WTN + 4 * q4;
                 // x = (acc + bias) + h, the residual image h = hi + lo/64 read in the accumulator
                 // layout, four row blocks at a time (as ln_res_img forms it)
+                // (loading it costs ~3 % of the step at C3 — 256 KB per tile at the ~50 GB/s one CU
+                // streams, RS_LNFUSE_DIAG=4 — and prefetching half of it beside the bias loads
+                // measured no better)
 #pragma unroll
                 for (int hh = 0; hh < 2; ++hh) {
-                    half4 rh[4][4], rl[4][4];
-                    const int rskip = (ep.diag & 4) ? 0 : 1;     // diag 4: residual rows of tile row 0
+                    half4 rh0[4][4], rl0[4][4];
+                    const int rskip = (ep.diag & 4) ? 0 : 1;     // diag 4 (timing only): the tile's first rows
 #pragma unroll
                     for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
                         for (int j = 0; j < 4; ++j) {
                             const f16* p = img + (size_t)(cm0 + rskip * (wm * WTM + 16 * (4 * hh + ii) + r16)) * ldc + c0 + 16 * j;
-                            rh[ii][j] = *(const half4*)p;
-                            rl[ii][j] = *(const half4*)(p + H);
+                            rh0[ii][j] = *(const half4*)p;
+                            rl0[ii][j] = *(const half4*)(p + H);
                         }
 #pragma unroll
                     for (int ii = 0; ii < 4; ++ii)
@@ -1565,13 +1563,13 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
 #pragma unroll
                             for (int e = 0; e < 4; ++e)
                                 acc16[4 * hh + ii][j][e] = (acc16[4 * hh + ii][j][e] + bq[j][e]) +
-                                                           ((float)rh[ii][j][e] + (float)rl[ii][j][e] * X3_DOWN);
+                                                           ((float)rh0[ii][j][e] + (float)rl0[ii][j][e] * X3_DOWN);
                 }
                 // row partials over the wave's 64 columns (lanes l, l^16, l^32, l^48 share a row),
                 // then over the four waves of the row half through their slabs
                 float* red = (float*)(slabs + wave * 4096);
                 auto slab_of = [&](int w2) { return (const float*)(slabs + (wm * WN + w2) * 4096); };
-                float tsum[8], tmean[8];
+                float tmean[8];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     float a = 0.f;
@@ -1579,11 +1577,11 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                     for (int j = 0; j < 4; ++j) a += (acc16[i][j][0] + acc16[i][j][1]) + (acc16[i][j][2] + acc16[i][j][3]);
                     a += __shfl_xor(a, 16);
                     a += __shfl_xor(a, 32);
-                    tsum[i] = a;
+                    tmean[i] = a;
                 }
                 if (q4 == 0) {
 #pragma unroll
-                    for (int i = 0; i < 8; ++i) red[16 * i + r16] = tsum[i];
+                    for (int i = 0; i < 8; ++i) red[16 * i + r16] = tmean[i];
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #pragma unroll
@@ -1591,10 +1589,8 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                     float a = 0.f;
 #pragma unroll
                     for (int w2 = 0; w2 < WN; ++w2) a += slab_of(w2)[16 * i + r16];
-                    tsum[i] = a;
                     tmean[i] = a * (1.f / BM);
                 }
-                float tm2[8];
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     float q = 0.f;
@@ -1607,116 +1603,86 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         }
                     q += __shfl_xor(q, 16);
                     q += __shfl_xor(q, 32);
-                    tm2[i] = q;
-                }
-                if (q4 == 0) {
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) red[128 + 16 * i + r16] = tm2[i];
+                    if (q4 == 0) red[128 + 16 * i + r16] = q;
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                // waves wn == 0: lane l owns rows l and l + 64 of the row half — its tile partials
+                // from the slabs (the same sums in the same order for every wave), published as
+                // granules, the peers' polled, the row statistics combined into the ring buffer
+                // this tile's last K-step read (free until the next tile's first barrier; the
+                // slabs are rewritten by the store pass)
+                float2* st2 = (float2*)(smem + last * STAGE) + wm * WTM;
+                if (wn == 0) {
+                    typedef unsigned long long u64;
+                    u64* gx = (u64*)ep.lnx + (size_t)panel * ntn * BM * 2 + wm * WTM * 2;   // [c][row][2]
+                    float os[2], oq[2];
 #pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    float a = 0.f;
+                    for (int k = 0; k < 2; ++k) {
+                        const int rr = lane + 64 * k;
+                        float a = 0.f, b = 0.f;
 #pragma unroll
-                    for (int w2 = 0; w2 < WN; ++w2) a += slab_of(w2)[128 + 16 * i + r16];
-                    tm2[i] = a;
-                }
-                // publish (sum, M2) of the tile's rows: waves wn == 0, one lane per row
-                float2* xt = ep.lnx + ((size_t)panel * ntn + tcol) * BM + wm * WTM;
-                if (wn == 0 && q4 == 0) {
-#pragma unroll
-                    for (int i = 0; i < 8; ++i) {
-                        const unsigned long long v = (unsigned long long)__float_as_uint(tsum[i]) |
-                                                     ((unsigned long long)__float_as_uint(tm2[i]) << 32);
-                        __hip_atomic_store((gu64*)(xt + 16 * i + r16), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        for (int w2 = 0; w2 < WN; ++w2) {
+                            a += slab_of(w2)[rr];
+                            b += slab_of(w2)[128 + rr];
+                        }
+                        os[k] = a;
+                        oq[k] = b;
+                        u64* g = gx + ((size_t)tcol * BM + rr) * 2;
+                        __hip_atomic_store((gu64*)g, tag | __float_as_uint(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store((gu64*)(g + 1), tag | __float_as_uint(b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
-                }
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // every storing wave drains
-                asm volatile("s_barrier" ::: "memory");
-                if (tid == 0) {
-                    // arrival; the panel's column tiles then move on together (a gang): the last
-                    // arriver claims the next panel for all of them and posts it, each takes the
-                    // column of its arrival rank — the gang's tiles start together, so they also
-                    // reach the next statistics exchange together
-                    const int npanels = n_tiles / ntn;
-                    gu32* pc = (gu32*)(ep.lncnt + 4 + panel);
-                    gu32* pn = (gu32*)(ep.lncnt + 4 + npanels + panel);
-                    const unsigned rank = __hip_atomic_fetch_add(pc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    unsigned np = 0;
-                    if (rank + 1 == (unsigned)ntn) {
-                        np = gridDim.x / ntn +
-                             __hip_atomic_fetch_add((gu32*)ep.lncnt + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        __hip_atomic_store(pn, np + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    } else {
-                        // the statistics first (the arrival counter: what orders the partials),
-                        // then the posted panel; diag 1 (timing only, wrong statistics): no wait
-                        unsigned spins = 0;
-                        for (int ph = 0; ph < 2; ++ph) {
-                            for (;;) {
-                                if (ph == 0 && (ep.diag & 1)) break;
-                                const unsigned v = __hip_atomic_load(ph ? pn : pc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                                if (ph ? v != 0u : v >= (unsigned)ntn) {
-                                    np = v - 1;
-                                    break;
-                                }
-                                if (ep.diag & 2) __builtin_amdgcn_s_sleep(16);
-                                else __builtin_amdgcn_s_sleep(1);
-                                if (++spins == (1u << 21)) {
-                                    __hip_atomic_store((gu32*)ep.lnerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                                    np = (unsigned)npanels;                // give up: leave the launch
-                                    break;
+                    float ps[2][4], pq[2][4];           // (diag 1: own partials only — no exchange)
+                    for (unsigned spins = 0;;) {
+                        bool ok = true;
+#pragma unroll
+                        for (int k = 0; k < 2; ++k)
+#pragma unroll
+                            for (int c = 0; c < 4; ++c) {
+                                ps[k][c] = os[k];
+                                pq[k][c] = oq[k];
+                                if (c < ntn && c != tcol && !(ep.diag & 1)) {
+                                    const u64* g = gx + ((size_t)c * BM + lane + 64 * k) * 2;
+                                    const u64 va = __hip_atomic_load((const gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                    const u64 vb = __hip_atomic_load((const gu64*)(g + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                    ok &= (va >> 32) == (tag >> 32) && (vb >> 32) == (tag >> 32);
+                                    ps[k][c] = __uint_as_float((unsigned)va);
+                                    pq[k][c] = __uint_as_float((unsigned)vb);
                                 }
                             }
-                            if (spins >= (1u << 21)) break;
+                        if (__all(ok)) break;
+                        __builtin_amdgcn_s_sleep(1);
+                        if (++spins == (1u << 20)) {
+                            if (lane == 0) __hip_atomic_store((gu32*)ep.lnerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            break;
                         }
                     }
-                    // to every wave through the ring buffer this tile's last K-step read (no DMA
-                    // enters it before the next tile's first barrier; the slabs are rewritten by
-                    // the store pass below)
-                    *(unsigned*)(smem + last * STAGE) = np * ntn + rank;
+#pragma unroll
+                    for (int k = 0; k < 2; ++k) {
+                        const int c_lo = (ep.diag & 1) ? tcol : 0, c_hi = (ep.diag & 1) ? tcol + 1 : ntn;
+                        const float inv_n = (ep.diag & 1) ? 1.f / BM : 1.f / H;
+                        float tot = 0.f;
+#pragma unroll
+                        for (int c = 0; c < 4; ++c)
+                            if (c >= c_lo && c < c_hi) tot += ps[k][c];
+                        const float mean = tot * inv_n;
+                        float m2 = 0.f;
+#pragma unroll
+                        for (int c = 0; c < 4; ++c) {
+                            if (c >= c_lo && c < c_hi) {
+                                const float d = ps[k][c] * (1.f / BM) - mean;
+                                m2 += __builtin_fmaf((float)BM * d, d, pq[k][c]);
+                            }
+                        }
+                        st2[lane + 64 * k] = make_float2(mean, 1.0f / sqrtf(__builtin_fmaf(m2, inv_n, ep.ln_eps)));
+                    }
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-                next_tile((int)*(const volatile unsigned*)(smem + last * STAGE));
-                // combine the panel's partials: lane l does rows l and l + 64 of the row half
-                float2* st2 = (float2*)(slabs + wave * 4096 + 1024);
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {
-                    const int rr = lane + 64 * k;
-                    // (diag 1: the tile's own partials only, as if the row were 256 wide)
-                    const int c_lo = (ep.diag & 1) ? tcol : 0, c_hi = (ep.diag & 1) ? tcol + 1 : ntn;
-                    const float inv_n = (ep.diag & 1) ? 1.f / BM : 1.f / H;
-                    float ts[4], tq[4], tot = 0.f;
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        ts[c] = 0.f;
-                        tq[c] = 0.f;
-                        if (c >= c_lo && c < c_hi) {
-                            const unsigned long long v = __hip_atomic_load(
-                                (gu64*)(ep.lnx + ((size_t)panel * ntn + c) * BM + wm * WTM + rr), __ATOMIC_RELAXED,
-                                __HIP_MEMORY_SCOPE_AGENT);
-                            ts[c] = __uint_as_float((unsigned)v);
-                            tq[c] = __uint_as_float((unsigned)(v >> 32));
-                            tot += ts[c];
-                        }
-                    }
-                    const float mean = tot * inv_n;
-                    float m2 = 0.f;
-#pragma unroll
-                    for (int c = 0; c < 4; ++c) {
-                        if (c >= c_lo && c < c_hi) {
-                            const float d = ts[c] * (1.f / BM) - mean;
-                            m2 += __builtin_fmaf((float)BM * d, d, tq[c]);
-                        }
-                    }
-                    st2[rr] = make_float2(mean, 1.0f / sqrtf(__builtin_fmaf(m2, inv_n, ep.ln_eps)));
-                }
                 f32x4 gq[4], bb[4];                      // LayerNorm weight / bias of the lane's columns
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     gq[j] = *(const f32x4*)(ep.res_g + c0 + 16 * j);
                     bb[j] = *(const f32x4*)(ep.res_b + c0 + 16 * j);
                 }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
                     const float2 st = st2[16 * i + r16];
@@ -1917,15 +1883,22 @@ hipError_t launch_x3s(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
         // tiles); the claim / arrival words start at zero every launch
         if (!ep.lnx || !ep.lncnt || !ep.lnerr || N_pad > 1024 || ep.nlog != N_pad || ep.ldc != 2 * N_pad)
             return hipErrorInvalidValue;
-        // whole row panels per round: the initial tiles form complete gangs (every workgroup
+        // whole row panels per round: the first tiles form complete gangs (every workgroup
         // resident at one per CU)
         grid = std::min(n_tiles, cus / ntn * ntn);
-        hipError_t e = hipMemsetAsync(ep.lncnt, 0, lnres_words(M_pad) * 4, st);
+        hipError_t e = hipMemsetAsync(ep.lncnt, 0, 16, st);          // the first-tile ticket
         if (e != hipSuccess) return e;
     }
     static const int gm_env = getenv("RS_GEMM_GROUP_M_X3S") ? atoi(getenv("RS_GEMM_GROUP_M_X3S")) : 0;
     EpiArgs e2 = ep;
     e2.group_m = gm_env > 0 ? gm_env : 8;
+    if constexpr (EPI == EPI_LNRES_IMG) {
+        // granule tag: this launch's sequence number (never 0: the granules start zeroed), so a
+        // granule left by an earlier launch never matches
+        static unsigned seq = 0;
+        if (++seq == 0) seq = 1;
+        e2.ln_tag = seq;
+    }
     hipLaunchKernelGGL((gemm_x3s_kernel<EPI, VAR>), dim3(grid), dim3(512), smem, st, A, W, K, ldw > 0 ? ldw : 2 * K,
                        ntn, n_tiles, e2);
     return hipGetLastError();

@@ -209,8 +209,9 @@ int reserve_impl(rs_model* m, int64_t max_rows) {
     const size_t kx = m->kx;
     HIPTRY(m->xst.ensure(M * sizeof(float2)));
     HIPTRY(m->xst1.ensure(M * sizeof(float2)));
-    HIPTRY(m->lnx.ensure(M * 4 * sizeof(float2)));            // <= 4 column tiles per row
-    HIPTRY(m->lncnt.ensure(lnres_words((int)M) * 4));
+    HIPTRY(m->lnx.ensure(lnres_granules((int)M) * 8));
+    HIPTRY(hipMemset(m->lnx.p, 0, m->lnx.bytes));               // granule tags start at 0 (never a launch's)
+    HIPTRY(m->lncnt.ensure(16));
     HIPTRY(m->lnerr.ensure(16));
     HIPTRY(hipMemset(m->lnerr.p, 0, 16));
     HIPTRY(m->h16.ensure(M * H * 2 * kx));
@@ -338,12 +339,12 @@ bool x3s_imgres_on() {
     const char* e = getenv("RS_X3S_IMGRES");
     return !(e && !strcmp(e, "0"));
 }
-// RS_LNFUSE=1 (image-held residual; default 0): the residual add + LayerNorm of both blocks run
-// in the O-projection / BertOutput GEMM epilogues (EPI_LNRES_IMG: full rows through an in-launch
-// exchange of row statistics) instead of as ln_res_img passes.  Read per call.
+// RS_LNFUSE (image-held residual; default 1): the residual add + LayerNorm of both blocks run in
+// the O-projection / BertOutput GEMM epilogues (EPI_LNRES_IMG: full rows through an in-launch
+// exchange of row statistics) instead of as ln_res_img passes (RS_LNFUSE=0).  Read per call.
 bool lnfuse_on(const rs_bert_cfg& cf) {
     const char* e = getenv("RS_LNFUSE");
-    return e && !strcmp(e, "1") && cf.hidden % 256 == 0 && cf.hidden <= 1024;
+    return !(e && !strcmp(e, "0")) && cf.hidden % 256 == 0 && cf.hidden <= 1024;
 }
 
 // Runs the encoder + head over sequences [c.s0, c.s1) (one chunk).
@@ -453,7 +454,7 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
             auto lnres_ep = [&](const float* bias, const float* g, const float* be) {
                 EpiArgs e{};
                 e.bias = bias; e.out = h16; e.ldc = 2 * H; e.nlog = H; e.res_g = g; e.res_b = be;
-                e.ln_eps = cf.ln_eps; e.lnx = m->lnx.as<float2>(); e.lncnt = m->lncnt.as<unsigned>();
+                e.ln_eps = cf.ln_eps; e.lnx = m->lnx.p; e.lncnt = m->lncnt.as<unsigned>();
                 e.lnerr = m->lnerr.as<unsigned>();
                 static const int diag = getenv("RS_LNFUSE_DIAG") ? atoi(getenv("RS_LNFUSE_DIAG")) : 0;
                 e.diag = diag;

@@ -1,6 +1,6 @@
 # fused residual + LayerNorm with gang scheduling: parity, then interleaved A/B
 set -o pipefail
-O=gpurun_out/r3k; mkdir -p $O
+O=gpurun_out/r3m; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests/test_gpu_bert.py -x -q --timeout 240 --timeout-method thread -k "lnfuse or fp16x3_golden or range_guard or dedup" > $O/tests.log 2>&1 || { tail -40 $O/tests.log; exit 1; }
 tail -2 $O/tests.log
 run() {
