@@ -180,6 +180,8 @@ def main():
             x3s = kx == 3 and os.environ.get("RS_X3S", "1") != "0"
             parts = 2 if x3s else kx
             out_b = (4 if dom != "ffn1" else 2 * parts) if kx == 3 else 2
+            if x3s and dom in ("oproj", "ffn2") and os.environ.get("RS_LNFUSE", "1") != "0":
+                out_b = 8      # residual + LayerNorm epilogue: the two-part residual image in, its update out
             alg_bytes = rows_per_launch * (parts * nk[1] * 2 + nk[0] * out_b) + parts * nk[0] * nk[1] * 2
         # the roofline figure is ALGORITHMIC: the reference's 2*M*N*K of the projection per launch
         #  / its HIP-event launch time, vs the dense fp16 MFMA peak; the MFMA work
