@@ -31,6 +31,7 @@
 // the buffer descriptor's extent, which the hardware returns as zeros.
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 #include "train.h"
@@ -336,6 +337,189 @@ sgemm_pipe_kernel(const float* __restrict__ A, int lda, const float* __restrict_
         }
 }
 
+// Stream-K form of the 128×128 kernel (the default): a persistent grid of G workgroups (two
+// per CU) first takes dp whole tiles each (round r: tile r·G + d), then splits the remaining
+// tiles' K-steps evenly — workgroup d takes iterations [d·I/G, (d+1)·I/G) of the flattened
+// (tile, K-step) space, so every CU ends with the same number of K-steps instead of a half-empty
+// last round or a split-K workspace pass.  A workgroup's first segment that starts inside a tile
+// is a partial: stored to ws[d] (sc1 write-through 16-B stores, every wave drained, then one
+// lane's sc1 flag store of this launch's epoch — MI355X_MICROARCH inter-workgroup visibility,
+// table row 1); the tile's owner (the workgroup holding its first K-step) polls the flags of the
+// workgroups after it and adds their partials (sc1 loads) in K order, so the sum order is fixed
+// by (shape, G) alone and a step stays bitwise reproducible.  Partials come first in every
+// workgroup's stream and owners wait only on later workgroups, so no wait chains; the grid fits
+// the chip at two per CU (every workgroup resident), and the poll is bounded (a timeout sets
+// flags[kSkTimeout]; the trainer step fails).
+constexpr int kSkMaxG = 512, kSkTimeout = 1023;    // flag words: [0, G) epochs, [1023] timeout
+
+template <bool AKC, bool BKC>
+__global__ void __launch_bounds__(256, 2)
+sgemm_sk_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb, float* __restrict__ C,
+                int ldc, int M, int N, int K, int accum, float* __restrict__ ws, unsigned* __restrict__ flags,
+                unsigned epoch, int dp, long long sk_iters, int sk_tile0) {
+    constexpr int BM = 128, BN = 128, TM = 64, BK = 32;
+    constexpr int WM = BM / TM, NW = 4, MT = TM / 32, HK = BK / 2;
+    constexpr int IMG_A = BM * BK * 4, STAGE = (BM + BN) * BK * 4;
+    using OA = SgOperand<AKC, BM, NW, BK>;
+    using OB = SgOperand<BKC, BN, NW, BK>;
+    typedef __attribute__((address_space(1))) unsigned gu32;
+    typedef int i4 __attribute__((ext_vector_type(4)));
+    __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int G = gridDim.x;
+    // XCD-contiguous workgroup index (blocks b and b + 8 share an XCD): neighbours d, d + 1 —
+    // a partial's producer and its owner — mostly share an L2
+    int d;
+    {
+        const int b = blockIdx.x, xcd = b & 7, pos = b >> 3, q = G >> 3, r = G & 7;
+        d = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + pos;
+    }
+    const int tiles_m = (M + BM - 1) / BM, tiles_n = (N + BN - 1) / BN;
+    const int steps = (K + BK - 1) / BK;
+    auto tile_rc = [&](int u, int& m0, int& n0) {            // groups of 8 row panels, column-walked
+        constexpr int GM = 8;
+        const int g = u / (GM * tiles_n), loc = u - g * GM * tiles_n;
+        const int gm = min(GM, tiles_m - g * GM);
+        const int tn = loc / gm;
+        m0 = (g * GM + (loc - tn * gm)) * BM;
+        n0 = tn * BN;
+    };
+    const int wm = (wave % WM) * TM, wn = (wave / WM) * 64;
+    const int h = lane >> 5, c = lane & 31;
+    const __amdgpu_buffer_rsrc_t wrs = sg_rsrc(ws, 0x7FFFFFF0u);
+    f32x16_t acc[MT][2];
+
+    // K-steps [s0, s1) of the tile at (m0, n0) into acc (zeroed first)
+    auto run = [&](int m0, int n0, int s0, int s1) {
+        OA oa;
+        OB ob;
+        oa.init(A, lda, M, m0, wave, lane);
+        ob.init(B, ldb, N, n0, wave, lane);
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        __syncthreads();                               // every wave done with the previous tile's LDS
+        oa.stage(smem, wave, s0 * BK, K);
+        ob.stage(smem + IMG_A, wave, s0 * BK, K);
+        int buf = 0;
+        for (int st = s0; st < s1; ++st) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            const char* sb = smem + buf * STAGE;
+            float fa[MT][HK], fb[2][HK];
+#pragma unroll
+            for (int i = 0; i < MT; ++i) OA::frag(sb, wm + 32 * i + c, h, fa[i]);
+#pragma unroll
+            for (int j = 0; j < 2; ++j) OB::frag(sb + IMG_A, wn + 32 * j + c, h, fb[j]);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if (st + 1 < s1) {
+                char* nx = smem + (buf ^ 1) * STAGE;
+                oa.stage(nx, wave, (st + 1) * BK, K);
+                ob.stage(nx + IMG_A, wave, (st + 1) * BK, K);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int kk = 0; kk < HK; ++kk)
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][kk], fb[j][kk], acc[i][j], 0, 0, 0);
+            buf ^= 1;
+        }
+    };
+    // D map of the 32x32 forms: column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+    auto store_c = [&](int m0, int n0) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+                const int col = n0 + wn + 32 * j + c;
+                if (col >= N) continue;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                    if (row >= M) continue;
+                    float* o = C + (size_t)row * ldc + col;
+                    *o = accum ? acc[i][j][r] + *o : acc[i][j][r];
+                }
+            }
+    };
+    // partial slot of workgroup w: [wave][i][j][lane][16] floats, 16-B pieces
+    auto part_off = [&](int w, int i, int j, int q) {
+        return (int)((((size_t)w * 16384 + wave * 4096 + ((i * 2 + j) * 64 + lane) * 16) + 4 * q) * 4);
+    };
+
+    for (int rr = 0; rr < dp; ++rr) {                  // data-parallel rounds: whole tiles
+        int m0, n0;
+        tile_rc(rr * G + d, m0, n0);
+        run(m0, n0, 0, steps);
+        store_c(m0, n0);
+    }
+    const long long b0 = (long long)d * sk_iters / G, b1 = (long long)(d + 1) * sk_iters / G;
+    for (long long it = b0; it < b1;) {
+        const int u = sk_tile0 + (int)(it / steps);
+        const int s0 = (int)(it % steps);
+        const long long tile_end = (long long)(u - sk_tile0 + 1) * steps;
+        const int s1 = (int)(min(tile_end, b1) - (long long)(u - sk_tile0) * steps);
+        int m0, n0;
+        tile_rc(u, m0, n0);
+        run(m0, n0, s0, s1);
+        if (s0 > 0) {
+            // a partial (this workgroup's first segment): publish it to the tile's owner
+#pragma unroll
+            for (int i = 0; i < MT; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const f32x4 v = {acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+                        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(i4, v), wrs, part_off(d, i, j, q), 0, 16);
+                    }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          // every storing wave drains
+            __syncthreads();
+            if (tid == 0) __hip_atomic_store((gu32*)(flags + d), epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            // the owner: the partials of the workgroups after it, in K order
+            long long cov = (long long)(u - sk_tile0) * steps + s1;     // covered up to (flat)
+            for (int w = d + 1; cov < tile_end && w < G; ++w) {
+                const long long wb0 = (long long)w * sk_iters / G, wb1 = (long long)(w + 1) * sk_iters / G;
+                if (wb0 == wb1) continue;                  // an empty range publishes nothing
+                if (tid == 0) {
+                    for (unsigned spins = 0; __hip_atomic_load((gu32*)(flags + w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != epoch;) {
+                        __builtin_amdgcn_s_sleep(2);
+                        if (++spins == (1u << 22)) {
+                            __hip_atomic_store((gu32*)(flags + kSkTimeout), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            break;
+                        }
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int i = 0; i < MT; ++i)
+#pragma unroll
+                    for (int j = 0; j < 2; ++j)
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(wrs, part_off(w, i, j, q), 0, 16));
+                            acc[i][j][4 * q] += v[0];
+                            acc[i][j][4 * q + 1] += v[1];
+                            acc[i][j][4 * q + 2] += v[2];
+                            acc[i][j][4 * q + 3] += v[3];
+                        }
+                cov = min(tile_end, wb1);
+            }
+            store_c(m0, n0);
+        }
+        it = min(tile_end, b1);
+    }
+}
+
 // C = sum over splits z = 0, 1, ... of ws[z] (+ C), in split order
 __global__ void __launch_bounds__(256)
 sgemm_splitk_sum_kernel(const float* __restrict__ ws, int splits, int M, int N, float* __restrict__ C, int ldc,
@@ -415,10 +599,60 @@ int sg_pick(int M, int N, int K) {
     return 0;
 }
 
+bool sk_enabled() {                                 // read per call (tests flip it in-process)
+    const char* e = getenv("RS_SGEMM_SK");
+    return e && !strcmp(e, "1");
+}
+
+int n_cus_sg() {
+    static int n = [] {
+        int dev = 0, v = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev);
+        return v > 0 ? v : 256;
+    }();
+    return n;
+}
+
+// Stream-K hand-off words of the current device: 1024 zeroed words (epoch tags [0, 512), the
+// timeout word), allocated on first use; the epoch counts launches (never 0, so a zeroed or
+// stale word never matches).  Single-threaded use, as the trainer's.
+struct SkFlags {
+    unsigned* p = nullptr;
+    unsigned epoch = 0;
+};
+SkFlags g_sk[16];
+
+hipError_t sk_flags(unsigned** f, unsigned* epoch) {
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev)) return e;
+    SkFlags& k = g_sk[dev & 15];
+    if (!k.p) {
+        if (hipError_t e = hipMalloc((void**)&k.p, 1024 * 4)) return e;
+        if (hipError_t e = hipMemset(k.p, 0, 1024 * 4)) return e;
+    }
+    if (++k.epoch == 0) k.epoch = 1;
+    *f = k.p;
+    *epoch = k.epoch;
+    return hipSuccess;
+}
+
 }  // namespace
 
+// 1 when a stream-K owner gave up waiting for a partial since the last call (cleared by it)
+int tr_sgemm_failed() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    SkFlags& k = g_sk[dev & 15];
+    if (!k.p) return 0;
+    unsigned v = 0;
+    if (hipMemcpy(&v, k.p + kSkTimeout, 4, hipMemcpyDeviceToHost) != hipSuccess) return 1;
+    if (v) (void)hipMemset(k.p + kSkTimeout, 0, 4);
+    return v != 0;
+}
+
 size_t tr_sgemm_ws_floats(int M, int N, int K) {
-    size_t w = 0;
+    size_t w = sk_enabled() ? (size_t)kSkMaxG * 16384 : 0;   // stream-K partial slots (128×128 each)
     for (int cfg = 0; cfg < kSgNCfg; ++cfg) {  // any configuration the picker or the knob may choose
         int kc = 0;
         const int s = sg_splits(cfg, M, N, K, &kc);
@@ -444,6 +678,31 @@ static hipError_t sg_run(int cfg, int M, int N, int K, const float* A, int lda, 
             if (e != hipSuccess) return e;
         }
         return hipSuccess;
+    }
+    // cfg 0 with RS_SGEMM_SK=1: the stream-K kernel instead of the split-K form (opt-in: its
+    // owner-side fix-up — poll, then 64 KB per partial read by one workgroup — cost more than
+    // the chip-wide workspace sum on all but one training shape, profiles/r3_sgemm_streamk.txt)
+    if (cfg == 0 && sk_enabled()) {
+        const int tiles = ((M + 127) / 128) * ((N + 127) / 128), steps = (K + 31) / 32;
+        const int G = std::min(std::min(kSkMaxG, 2 * n_cus_sg()), tiles * steps);
+        if (!ws || ws_floats < (size_t)G * 16384) return hipErrorInvalidValue;
+        unsigned* flags = nullptr;
+        unsigned epoch = 0;
+        if (hipError_t e = sk_flags(&flags, &epoch)) return e;
+        int dp = tiles / G;
+        const int rem = tiles - dp * G;
+        if (rem * 10 >= G * 9) ++dp;               // a nearly full last round: whole tiles, no partials
+        const int sk_tile0 = std::min(tiles, dp * G);
+        const long long sk_iters = (long long)(tiles - sk_tile0) * steps;
+#define SK_LAUNCH(AK, BK_)                                                                                      \
+    hipLaunchKernelGGL((sgemm_sk_kernel<AK, BK_>), dim3(G), dim3(256), 0, s, A, lda, B, ldb, C, ldc, M, N, K, accum, \
+                       ws, flags, epoch, dp, sk_iters, sk_tile0)
+        if (a_kc && b_kc) SK_LAUNCH(true, true);
+        else if (a_kc) SK_LAUNCH(true, false);
+        else if (b_kc) SK_LAUNCH(false, true);
+        else SK_LAUNCH(false, false);
+#undef SK_LAUNCH
+        return hipGetLastError();
     }
     int kc = 0;
     const int splits = sg_splits(cfg, M, N, K, &kc);

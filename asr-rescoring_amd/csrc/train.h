@@ -97,5 +97,6 @@ hipError_t tr_adamw(float* p, const float* g, float* m, float* v, long long n, f
 // or [K][ldb].  Few output tiles are split over K through ws (tr_sgemm_ws_floats floats),
 // summed in split order: deterministic.
 size_t tr_sgemm_ws_floats(int M, int N, int K);
+int tr_sgemm_failed();      // a stream-K hand-off timed out since the last call (synchronous check)
 hipError_t tr_sgemm(int M, int N, int K, const float* A, int lda, bool a_kc, const float* B, int ldb, bool b_kc,
                     float* C, int ldc, int accum, float* ws, size_t ws_floats, hipStream_t s);

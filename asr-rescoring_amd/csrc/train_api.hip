@@ -625,6 +625,7 @@ int rs_train_step_cls(rs_trainer* t, const int32_t* d_tok, const int32_t* h_hyp_
     if (int r = encoder_backward(c)) return r;
     if (int r = adamw(t, o, st)) return r;
     TRY_HIP(hipStreamSynchronize(st));        // the metadata upload read t->h_meta
+    if (tr_sgemm_failed()) return rs_fail(RS_EHIP, "a stream-K GEMM timed out waiting for a partial tile");
     return RS_OK;
 }
 
@@ -674,6 +675,7 @@ int rs_train_step_mlm(rs_trainer* t, const int32_t* d_ids, const int32_t* h_seq_
     if (int r = encoder_backward(c)) return r;
     if (int r = adamw(t, o, st)) return r;
     TRY_HIP(hipStreamSynchronize(st));
+    if (tr_sgemm_failed()) return rs_fail(RS_EHIP, "a stream-K GEMM timed out waiting for a partial tile");
     return RS_OK;
 }
 
