@@ -1,3 +1,4 @@
+#include <atomic>
 // fp16 MFMA GEMM for the BERT projections: C[M,N] = A[M,K] . W[N,K]^T (+ fused epilogue).
 //
 // Replaces the nn.Linear calls of transformers modeling_bert.py (Q/K/V :154-156 fused into
@@ -1863,18 +1864,25 @@ int n_cus() {
     return n;
 }
 
+// Raise a kernel's dynamic-LDS limit once per device (the attribute is per device; a process may
+// drive several).
+hipError_t smem_attr_once(const void* fn, int smem, std::atomic<unsigned>& devs) {
+    int dev = 0;
+    if (hipError_t e = hipGetDevice(&dev)) return e;
+    const unsigned bit = 1u << (dev & 31);
+    if (devs.load(std::memory_order_acquire) & bit) return hipSuccess;
+    if (hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, smem)) return e;
+    devs.fetch_or(bit, std::memory_order_release);
+    return hipSuccess;
+}
+
 template <int EPI, int VAR = 262144>
 hipError_t launch_x3s(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep, hipStream_t st,
                       int ldw = 0) {
     constexpr int smem = 2 * 65536;                  // ring (2 x 64 KiB); + 32 KiB static wave slabs
     if (K % 32 || K < 64 || M_pad % 256 || N_pad % 256) return hipErrorInvalidValue;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_x3s_kernel<EPI, VAR>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    static std::atomic<unsigned> attr_devs{0};      // devices whose LDS limit is raised
+    if (hipError_t e = smem_attr_once((const void*)gemm_x3s_kernel<EPI, VAR>, smem, attr_devs)) return e;
     const int ntn = N_pad / 256, n_tiles = (M_pad / 256) * ntn;
     const int cus = n_cus() / 8 * 8;
     int grid = n_tiles <= cus ? n_tiles : cus;
@@ -1910,13 +1918,8 @@ hipError_t launch_persist(const f16* A, const f16* W, int M_pad, int N_pad, int 
     // VAR 1048576: wave-private epilogue slabs in their own 32 KiB after the ring (160 KiB)
     constexpr int smem = 2 * 512 * 64 * 2 + ((VAR & 1048576) ? 8 * 32 * 128 : 0);
     if (K % 64 || M_pad % 256 || N_pad % 256) return hipErrorInvalidValue;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_persist_kernel<EPI, VAR>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    static std::atomic<unsigned> attr_devs{0};      // devices whose LDS limit is raised
+    if (hipError_t e = smem_attr_once((const void*)gemm_persist_kernel<EPI, VAR>, smem, attr_devs)) return e;
     const int ntn = N_pad / 256, n_tiles = (M_pad / 256) * ntn;
     const int cus = n_cus() / 8 * 8;
     const int grid = n_tiles <= cus ? n_tiles : cus;
@@ -1944,13 +1947,8 @@ hipError_t launch_t(const f16* A, const f16* W, int M_pad, int N_pad, int K, con
                     hipStream_t st) {
     constexpr int smem = NSTAGE * (BM + BN) * BK * 2;
     if (K % BK) return hipErrorInvalidValue;
-    static bool attr_set = false;
-    if (!attr_set) {
-        hipError_t e = hipFuncSetAttribute((const void*)gemm_f16_kernel<BM, BN, WM, WN, NSTAGE, BK, EPI, VAR>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-        if (e != hipSuccess) return e;
-        attr_set = true;
-    }
+    static std::atomic<unsigned> attr_devs{0};      // devices whose LDS limit is raised
+    if (hipError_t e = smem_attr_once((const void*)gemm_f16_kernel<BM, BN, WM, WN, NSTAGE, BK, EPI, VAR>, smem, attr_devs)) return e;
     const int ntn = N_pad / BN;
     const int grid = (M_pad / BM) * ntn;
     static const int gm_env = getenv("RS_GEMM_GROUP_M") ? atoi(getenv("RS_GEMM_GROUP_M")) : 0;
