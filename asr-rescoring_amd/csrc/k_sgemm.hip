@@ -546,10 +546,11 @@ sgemm_splitk_sum_kernel(const float* __restrict__ ws, int splits, int M, int N, 
 // resident at once), 2 = 256×128×32 (8 waves of 64×64, 1 per CU; half the operand bytes per
 // FLOP of a 128×128 tile on the A side).
 struct SgCfg { int bm, bn, bk, occ; };
-constexpr int kSgNCfg = 7;
+constexpr int kSgNCfg = 9;
 constexpr SgCfg kSgCfg[kSgNCfg] = {{128, 128, 32, 2}, {128, 128, 16, 4}, {256, 128, 32, 1},
                                    {128, 128, 16, 3}, {128, 128, 32, 1},    // 3, 4: sgemm_pipe_kernel
-                                   {128, 64, 32, 2},  {128, 64, 32, 3}};    // 5, 6: 4 waves of 32×64
+                                   {128, 64, 32, 2},  {128, 64, 32, 3},     // 5, 6: 4 waves of 32×64
+                                   {64, 64, 32, 4},   {64, 64, 32, 6}};     // 7, 8: 2 waves of 32×64
 
 int sg_splits(int cfg, int M, int N, int K, int* kc) {
     const SgCfg& g = kSgCfg[cfg];
@@ -729,7 +730,9 @@ static hipError_t sg_run(int cfg, int M, int N, int K, const float* A, int lda, 
     else if (cfg == 3) SG_FORMS(sgemm_pipe_kernel, 128, 128, 64, 16, 3);
     else if (cfg == 4) SG_FORMS(sgemm_pipe_kernel, 128, 128, 64, 32, 1);
     else if (cfg == 5) SG_FORMS(sgemm_dma_kernel, 128, 64, 32, 32, 2);
-    else SG_FORMS(sgemm_dma_kernel, 128, 64, 32, 32, 3);
+    else if (cfg == 6) SG_FORMS(sgemm_dma_kernel, 128, 64, 32, 32, 3);
+    else if (cfg == 7) SG_FORMS(sgemm_dma_kernel, 64, 64, 32, 32, 4);
+    else SG_FORMS(sgemm_dma_kernel, 64, 64, 32, 32, 6);
 #undef SG_FORMS
 #undef SG_LAUNCH
     hipError_t e = hipGetLastError();
