@@ -227,7 +227,7 @@ def main():
         threads = set_cpu_threads()
         model = TorchBert(weights, BERT_BASE)
         lm_np = lm.double().cpu().numpy()
-        rows_done, t_cpu, h, rel = 0, 0.0, 0, []
+        rows_done, t_cpu, h, rel, ref_lm = 0, 0.0, 0, [], []
         while t_cpu < args.cpu_seconds and h < nb.n_hyp:
             sub_off = nb.hyp_off[h:h + 2] - nb.hyp_off[h]
             toks = nb.tokens[nb.hyp_off[h]:nb.hyp_off[h + 1]]
@@ -235,14 +235,29 @@ def main():
             _, ref_pll = OB.pll_reference_pattern(model, toks, sub_off, batch_size=32, full_head=True)
             t_cpu += time.perf_counter() - t1
             rel.append(abs(lm_np[h] - ref_pll[0]) / abs(ref_pll[0]))
+            ref_lm.append(float(ref_pll[0]))
             rows_done += int(sub_off[-1]) - 2
             h += 1
+        # the rerank index from the CPU reference's own lm on the sampled utterances that were
+        # scored whole, against the HIP lm's (all 101 weights): a check of scoring + fusion
+        from oracle import rescore_ref as RR
+        Nb = args.nbest
+        uw = h // Nb
+        rerank_same = None
+        if uw > 0:
+            am_s = nb.am[:uw * Nb].reshape(uw, Nb)
+            hyps_s = [[nb.hyp_words(u * Nb + i) for i in range(Nb)] for u in range(uw)]
+            refs_s = nb.refs[:uw]
+            _, _, arg_ref = RR.find_best_weight(am_s, np.asarray(ref_lm[:uw * Nb]).reshape(uw, Nb), hyps_s, refs_s, Nb)
+            _, _, arg_hip = RR.find_best_weight(am_s, lm_np[:uw * Nb].reshape(uw, Nb), hyps_s, refs_s, Nb)
+            rerank_same = bool(np.array_equal(arg_ref, arg_hip))
         cpu = {"value": round(rows_done / t_cpu, 2), "unit": "masked fwd/s", "cores": threads,
                "cpu_model": _cpu_model(), "kind": "port",
                "sample": f"{h} hypotheses ({rows_done} masked forwards) of rank-0 step "
                f"input, reference work pattern (batch 32 padded rows, all-position logits + CE, "
                f"fp64 accumulation), torch {torch.__version__} CPU",
-               "pll_max_rel_err_vs_gpu": float(max(rel)) if rel else None}
+               "pll_max_rel_err_vs_gpu": float(max(rel)) if rel else None,
+               "rerank_argmax_equal_cpu_reference_lm": rerank_same, "rerank_check_utterances": uw}
 
     # ---- secondary leg: the reduced-precision fp16 mode on the same input (labelled) ------
     fp16 = None
