@@ -11,8 +11,8 @@
 //   dgrad    dX = dY · W    A = dY (KC)   B = W  (MC: W[n][k'] read with k' = output column)
 //   wgrad    dW = dYᵀ· X    A = dY (MC)   B = X  (MC)
 //
-// Tiles (by shape, sg_pick): 128×128 (4 waves of 64×64, two workgroups per CU), 256×128 (8
-// waves of 64×64) and 256×256 (8 waves of 128×64); BK = 32; two LDS stages filled by LDS-DMA
+// Tiles (by shape, sg_pick's time model): 128×128 (4 waves of 64×64) or 192×128 (4 waves of
+// 96×64), two workgroups per CU (other tiles are A/B knobs); BK = 32; two LDS stages filled by LDS-DMA
 // (buffer_load_dwordx4 … lds, 1 KiB per wave-instruction) with one barrier per K-step and two
 // waves per SIMD.  No register staging and no transposing LDS writes: the DMA writes each
 // operand's natural image —
@@ -546,37 +546,56 @@ sgemm_splitk_sum_kernel(const float* __restrict__ ws, int splits, int M, int N, 
 // resident at once), 2 = 256×128×32 (8 waves of 64×64, 1 per CU; half the operand bytes per
 // FLOP of a 128×128 tile on the A side).
 struct SgCfg { int bm, bn, bk, occ; };
-constexpr int kSgNCfg = 9;
+constexpr int kSgNCfg = 10;
 constexpr SgCfg kSgCfg[kSgNCfg] = {{128, 128, 32, 2}, {128, 128, 16, 4}, {256, 128, 32, 1},
                                    {128, 128, 16, 3}, {128, 128, 32, 1},    // 3, 4: sgemm_pipe_kernel
                                    {128, 64, 32, 2},  {128, 64, 32, 3},     // 5, 6: 4 waves of 32×64
-                                   {64, 64, 32, 4},   {64, 64, 32, 6}};     // 7, 8: 2 waves of 32×64
+                                   {64, 64, 32, 4},   {64, 64, 32, 6},      // 7, 8: 2 waves of 32×64
+                                   {192, 128, 32, 2}};                      // 9: 4 waves of 96×64
 
-int sg_splits(int cfg, int M, int N, int K, int* kc) {
+// Modelled time (µs) of one configuration at a split count: dispatch rounds × (K-steps per
+// workgroup × the time a CU takes per K-step with its resident workgroups + a per-round
+// prologue/epilogue), plus, split, the partials' round trip.  Fitted to the forced-split sweep of
+// the 128×128 tile (profiles/r3_sgemm_split_sweep.txt, 135 points, 5 % rms): 3.74 µs per K-step
+// with two workgroups on the CU, 2.14 alone (a grid of at most one workgroup per CU is spread
+// one per CU; a partial last round of a larger grid is packed two per CU and costs a whole
+// round), 5.4 µs per round, 4.2 µs + (2·splits + 1)·M·N·4 B at 7.9 TB/s for the partials; the
+// weight-gradient form (both operands output-contiguous, ds_read_b32 fragments) 10 % slower per
+// step.  192×128: 6.4 / 3.4 µs per K-step (profiles/r3u_sgemm_pick.txt).  Other tiles scale by
+// their K-step volume.
+double sg_model(int cfg, int M, int N, int K, int sp, bool mcmc = false) {
     const SgCfg& g = kSgCfg[cfg];
-    const int tiles = ((M + g.bm - 1) / g.bm) * ((N + g.bn - 1) / g.bn);
+    const long long tiles = (long long)((M + g.bm - 1) / g.bm) * ((N + g.bn - 1) / g.bn);
+    const int steps = (K + g.bk - 1) / g.bk, per = (steps + sp - 1) / sp, spr = (steps + per - 1) / per;
+    const double vol = (double)g.bm * g.bn * g.bk / (128.0 * 128.0 * 32.0);
+    double t_one = 2.14 * vol, t_full = 3.74 * vol * g.occ / 2.0;
+    if (cfg == 9) { t_one = 3.43; t_full = 6.4; }
+    else if (mcmc) { t_one *= 1.1; t_full *= 1.1; }
+    const long long wgs = tiles * spr, cus = 256;
+    double t = wgs <= cus ? per * t_one + 5.44
+                          : (double)((wgs + cus * g.occ - 1) / (cus * g.occ)) * (per * t_full + 5.44);
+    if (spr > 1) t += 4.24 + (2.0 * spr + 1.0) * M * N * 4.0 * 0.127e-6;
+    return t;
+}
+
+int sg_splits(int cfg, int M, int N, int K, int* kc, bool mcmc = false) {
+    const SgCfg& g = kSgCfg[cfg];
     const int steps = (K + g.bk - 1) / g.bk;
-    // Split K so the work list fills the chip in whole rounds: the occ workgroups a CU holds run
-    // in about the time of one (measured: a CU with two resident 128×128 tiles finishes them as
-    // fast as one alone), so the time is ~ rounds × K-steps per workgroup, rounds =
-    // ceil(tiles · splits / (CUs · occ)).  Each split also writes and re-reads an M·N partial:
-    // a quarter K-step per extra split breaks ties towards fewer.  RS_SGEMM_SPLITS forces a
-    // split count (A/B knob).
+    // the split count with the lowest modelled time (at least 4 K-steps per split).
+    // RS_SGEMM_SPLITS forces a split count (A/B knob).
     static const int forced = [] {
         const char* v = getenv("RS_SGEMM_SPLITS");
         return v ? std::max(1, atoi(v)) : 0;
     }();
-    const long long slots = 256ll * g.occ;
     int splits = 1;
     if (forced) {
         splits = std::min(forced, std::max(1, steps));
     } else {
         double best = 1e30;
         for (int sp = 1; sp <= 16 && sp <= std::max(1, steps / 4); ++sp) {
-            const long long rounds = ((long long)tiles * sp + slots - 1) / slots;
-            const double cost = (double)rounds * ((steps + sp - 1) / sp) + 0.25 * (sp - 1);
-            if (cost < best) {
-                best = cost;
+            const double t = sg_model(cfg, M, N, K, sp, mcmc);
+            if (t < best) {
+                best = t;
                 splits = sp;
             }
         }
@@ -586,18 +605,28 @@ int sg_splits(int cfg, int M, int N, int K, int* kc) {
     return (steps + per - 1) / per;
 }
 
-// RS_SGEMM_CFG=0..4 forces a tile configuration (A/B knob).  Default cfg 0 (128×128, BK 32,
-// two workgroups per CU): the lowest total over the trainer's shape set (tools/sgemm_bench.py);
-// the others win single shapes by 5–15%, not enough to justify a shape table whose choice
-// would also change the split-K order (and so the bits) from one batch shape to the next.
-int sg_pick(int M, int N, int K) {
+// The tile configuration: 128×128 (cfg 0) or 192×128 (cfg 9), whichever the model times lower
+// at its best split (192×128 wins where the 128×128 grid leaves a half-empty last round, e.g.
+// 5300 × 2304).  RS_SGEMM_CFG=0..9 forces a configuration (A/B knob).  The choice depends on
+// the shape only, so a shape's results stay bitwise reproducible.
+int sg_pick(int M, int N, int K, bool mcmc) {
     static const int forced = [] {
         const char* v = getenv("RS_SGEMM_CFG");
         return v ? atoi(v) : -1;
     }();
     if (forced >= 0 && forced < kSgNCfg) return forced;
-    (void)M; (void)N; (void)K;
-    return 0;
+    int best = 0;
+    double tb = 1e30;
+    for (int cfg : {0, 9}) {
+        int kc = 0;
+        const int sp = sg_splits(cfg, M, N, K, &kc, mcmc);
+        const double t = sg_model(cfg, M, N, K, sp, mcmc);
+        if (t < 0.97 * tb) {
+            tb = t;
+            best = cfg;
+        }
+    }
+    return best;
 }
 
 bool sk_enabled() {                                 // read per call (tests flip it in-process)
@@ -656,8 +685,10 @@ size_t tr_sgemm_ws_floats(int M, int N, int K) {
     size_t w = sk_enabled() ? (size_t)kSkMaxG * 16384 : 0;   // stream-K partial slots (128×128 each)
     for (int cfg = 0; cfg < kSgNCfg; ++cfg) {  // any configuration the picker or the knob may choose
         int kc = 0;
-        const int s = sg_splits(cfg, M, N, K, &kc);
-        if (s > 1) w = std::max(w, (size_t)s * M * N);
+        for (int mc = 0; mc < 2; ++mc) {
+            const int s = sg_splits(cfg, M, N, K, &kc, mc != 0);
+            if (s > 1) w = std::max(w, (size_t)s * M * N);
+        }
     }
     return w;
 }
@@ -706,7 +737,7 @@ static hipError_t sg_run(int cfg, int M, int N, int K, const float* A, int lda, 
         return hipGetLastError();
     }
     int kc = 0;
-    const int splits = sg_splits(cfg, M, N, K, &kc);
+    const int splits = sg_splits(cfg, M, N, K, &kc, !a_kc && !b_kc);
     float* P = nullptr;
     if (splits > 1) {
         if (!ws || ws_floats < (size_t)splits * M * N) return hipErrorInvalidValue;
@@ -732,7 +763,8 @@ static hipError_t sg_run(int cfg, int M, int N, int K, const float* A, int lda, 
     else if (cfg == 5) SG_FORMS(sgemm_dma_kernel, 128, 64, 32, 32, 2);
     else if (cfg == 6) SG_FORMS(sgemm_dma_kernel, 128, 64, 32, 32, 3);
     else if (cfg == 7) SG_FORMS(sgemm_dma_kernel, 64, 64, 32, 32, 4);
-    else SG_FORMS(sgemm_dma_kernel, 64, 64, 32, 32, 6);
+    else if (cfg == 8) SG_FORMS(sgemm_dma_kernel, 64, 64, 32, 32, 6);
+    else SG_FORMS(sgemm_dma_kernel, 192, 128, 96, 32, 2);
 #undef SG_FORMS
 #undef SG_LAUNCH
     hipError_t e = hipGetLastError();
@@ -745,7 +777,7 @@ static hipError_t sg_run(int cfg, int M, int N, int K, const float* A, int lda, 
 
 hipError_t tr_sgemm(int M, int N, int K, const float* A, int lda, bool a_kc, const float* B, int ldb, bool b_kc,
                     float* C, int ldc, int accum, float* ws, size_t ws_floats, hipStream_t s) {
-    return sg_run(sg_pick(M, N, K), M, N, K, A, lda, a_kc, B, ldb, b_kc, C, ldc, accum, ws, ws_floats, s);
+    return sg_run(sg_pick(M, N, K, !a_kc && !b_kc), M, N, K, A, lda, a_kc, B, ldb, b_kc, C, ldc, accum, ws, ws_floats, s);
 }
 
 // Test / timing entry (not part of the scoring path): one trainer GEMM in the given operand
@@ -766,7 +798,7 @@ extern "C" int rs_debug_sgemm_cfg(int cfg, int M, int N, int K, const float* A, 
         if (hipMalloc(&ws, wsf * 4) != hipSuccess) return -3;
         ws_cap = wsf;
     }
-    hipError_t e = sg_run(cfg < 0 ? sg_pick(M, N, K) : cfg, M, N, K, A, lda, a_kc != 0, B, ldb, b_kc != 0, C, ldc,
+    hipError_t e = sg_run(cfg < 0 ? sg_pick(M, N, K, a_kc == 0 && b_kc == 0) : cfg, M, N, K, A, lda, a_kc != 0, B, ldb, b_kc != 0, C, ldc,
                           accum, ws, ws_cap, (hipStream_t)stream);
     return e == hipSuccess ? 0 : -2;
 }

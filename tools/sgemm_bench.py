@@ -35,7 +35,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / reps
-    CFGS = (-1,) + tuple(int(c) for c in os.environ.get("SG_CFGS", "0,1,2,3,4,5,6,7,8").split(","))
+    CFGS = (-1,) + tuple(int(c) for c in os.environ.get("SG_CFGS", "0,1,2,3,4,5,6,7,8,9").split(","))
     tot = {c: 0.0 for c in CFGS}
     tot_ref = 0.0
     for T in (1100, 5300):
