@@ -11,8 +11,9 @@ this.  Restated functions (reference file:line):
 * ``rescore.py:55-58`` ``get_highest_score_hyp``: ``np.argmax(axis=-1)`` (first max).
 * ``rescore.py:25-45`` ``find_best_weight``: weights ``np.arange(0.0, 1.01, 0.01)``, corpus
   CER per weight, strict ``<`` keeps the first best weight.
-* ``jiwer.cer`` (third-party, absent, unpinned): sum of Levenshtein edits / sum of reference
-  lengths (see ``oracle/levenshtein.c``).
+* ``jiwer.cer`` (third-party, absent): sum of Levenshtein edits / sum of reference lengths
+  (see ``oracle/levenshtein.c``); pinned by the jiwer outputs the reference records in
+  ``Nbest_Align/cer.json`` (``tests/golden/jiwer_cer_pairs.json``: every value reproduced).
 * ``RMBR/mbr.py:5-28`` ``mbr_decode`` + ``RMBR/utility_functions.py:28-33``: ordered pairs
   (cand = hyp_i, ref = every other hyp_j of the top-k in list order), sim = 1 - cer(ref, cand)
   as Python float64, ``torch.tensor(float32)``, ``reshape(U, k, k-1).sum(-1)`` (torch-CPU

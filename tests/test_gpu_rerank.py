@@ -28,6 +28,26 @@ def test_ref_and_pairwise_edit_vs_oracle():
                 assert M[i, j] == R.levenshtein(nb.hyp_words(nb.utt_off[u] + i), nb.hyp_words(nb.utt_off[u] + j))
 
 
+def test_ref_edit_vs_jiwer_recorded_outputs(golden_dir):
+    """The CER kernel on the product's text path (data.from_texts -> rs_ref_edit) against
+    jiwer.cer outputs the reference recorded (Nbest_Align/cer.json, 1934 pairs): every
+    per-pair CER bit-exact, and the corpus CER kernel (rs_corpus_edits) gives Σ edits."""
+    from asr_rescoring_amd import rerank
+    pairs = json.load(open(os.path.join(golden_dir, "jiwer_cer_pairs.json"), encoding="utf-8"))["pairs"]
+    hyps = {f"u{i}": {"hyp_1": pred, "hyp_2": ref} for i, (ref, pred, _) in enumerate(pairs)}
+    refs = {f"u{i}": ref for i, (ref, _, _) in enumerate(pairs)}
+    nb = D.from_texts(hyps, refs)
+    ed = rerank.ref_edits(nb).cpu().numpy()
+    for i, (ref, _, cer) in enumerate(pairs):
+        n = len(ref.strip())
+        assert ed[2 * i] / n == cer, (ref, cer, ed[2 * i])
+        assert ed[2 * i + 1] == 0
+    import torch
+    arg = torch.zeros((1, nb.n_utt), dtype=torch.int32, device="cuda")     # hyp_1 everywhere
+    tot = int(rerank.corpus_edits(rerank.ref_edits(nb), nb.utt_off, arg).cpu()[0])
+    assert tot == sum(round(cer * len(ref.strip())) for ref, _, cer in pairs)
+
+
 def test_edit_long_strings_and_many_hypotheses():
     """Strings past one 64-bit word and past the old 1024-symbol DP (blocked Myers, exact up
     to 16384 symbols) and an utterance with 1500 hypotheses (ref_edit strides over them)."""

@@ -91,6 +91,24 @@ def test_cer_value_domain_matches_reference_data():
         R.corpus_cer([[]], [[1]])
 
 
+def test_cer_vs_jiwer_recorded_outputs(golden_dir):
+    """jiwer pinned: the reference holds jiwer.cer's outputs for 7176 (ref, pred)
+    pairs (Nbest_Align/cer.json; tests/golden/make_jiwer_fixture.py keeps the 1734 with a
+    non-zero CER and 200 zero ones).  The restatement (edits of ``strip()``-ed code points /
+    ref length, as Python float64) reproduces every recorded value bit for bit, and the corpus
+    form (Σ edits / Σ ref chars) the same sum."""
+    pairs = json.load(open(os.path.join(golden_dir, "jiwer_cer_pairs.json"), encoding="utf-8"))["pairs"]
+    assert len(pairs) == 1934
+    refs, hyps = [], []
+    for ref, pred, cer in pairs:
+        r, h = [ord(c) for c in ref.strip()], [ord(c) for c in pred.strip()]
+        assert R.levenshtein(r, h) / len(r) == cer, (ref, pred, cer)
+        refs.append(r)
+        hyps.append(h)
+    edits = sum(round(cer * len(ref.strip())) for ref, _, cer in pairs)
+    assert R.corpus_cer(refs, hyps) == edits / sum(len(r) for r in refs)
+
+
 @pytest.mark.parametrize("n", list(range(1, 100)))
 def test_torch_sum_order(n):
     x = torch.rand(64, n) * 0.3 + 0.7
