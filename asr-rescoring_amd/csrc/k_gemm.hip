@@ -1381,6 +1381,62 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         }
     };
 
+    // VAR 524288 (16x16 form): the younger wave half (waves 4-7) runs half a K-step behind the
+    // older half (MI355X_MICROARCH 'Two waves per SIMD' item 9).  After the barrier of step k it
+    // first runs the second row half (h = 1) of step k-1 from fragments it read into registers
+    // before that barrier (the DMA of step k+1 into that buffer is issued only after it, riding
+    // these MFMAs), then reads and runs (k, h = 0), and reads (k, h = 1) to carry across the
+    // next barrier.  So at each barrier only the older half opens with an LDS read burst while
+    // the younger half's MFMAs keep each SIMD's pipe busy.  Same fragments, same MFMAs in the
+    // same accumulator order: results bitwise equal to the unstaggered form.
+    constexpr bool STAG = M16 && (VAR & 524288) != 0;
+    auto read_w16 = [&](int buf, half8 (&wh)[4], half8 (&wl)[4], half8 (&wd)[4]) {
+        const char* sb = smem + buf * STAGE;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            wh[j] = *(const half8*)(sb + offW16 + j * 1024);
+            wl[j] = *(const half8*)(sb + offW16 + REG + j * 1024);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wd[j] = wh[j] * down;
+    };
+    auto read_a16 = [&](int buf, int h, half8 (&ah)[4], half8 (&al)[4]) {
+        const char* sb = smem + buf * STAGE;
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) {
+            ah[ii] = *(const half8*)(sb + offA16 + (4 * h + ii) * 1024);
+            al[ii] = *(const half8*)(sb + offA16 + REG + (4 * h + ii) * 1024);
+        }
+    };
+    // one row half's 48 MFMAs; the eight DMA pieces of (dbuf, k0n) ride its first 8 groups
+    auto mf_half16 = [&](auto hc, half8 (&wh)[4], half8 (&wl)[4], half8 (&wd)[4], half8 (&ah)[4], half8 (&al)[4],
+                         int dbuf, int k0n) {
+        constexpr int h = decltype(hc)::value;
+#pragma unroll
+        for (int pr = 0; pr < 3; ++pr) {
+            if (pr == 2) {
+#pragma unroll
+                for (int ii = 0; ii < 4; ++ii) ah[ii] *= down;
+            }
+#pragma unroll
+            for (int ii = 0; ii < 4; ++ii) {
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const half8 b = pr == 0 ? wh[j] : pr == 1 ? wd[j] : wl[j];
+                    const half8 a = pr == 1 ? al[ii] : ah[ii];
+                    acc16[4 * h + ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b, a, acc16[4 * h + ii][j], 0, 0, 0);
+                }
+                const int grp = 4 * pr + ii;
+                if (grp < 8 && k0n < (1 << 29)) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    piece(dbuf, k0n, grp);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        }
+    };
+    const bool young = STAG && wave >= NW / 2;
+
     int m0, n0;
     tile_of(t, m0, n0);
     set_src(m0, n0);
@@ -1401,6 +1457,9 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
 #pragma unroll
                 for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16)(0.f);
         }
+        // STAG: the fragments carried across a barrier (scoped to the tile, so none is live
+        // across the epilogue)
+        half8 cwh[4], cwl[4], cwd[4], cah[4], cal[4];
         for (int kt = 0; kt < nk; ++kt) {
             const int cur = (par + kt) & 1;
             // step kt landed for this wave (at a tile's first step the previous tile's stores
@@ -1411,6 +1470,34 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             } else if (kt == 0 && !first) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             asm volatile("s_barrier" ::: "memory");
+            if constexpr (STAG) {
+                // one code path for both halves (one register set): the younger half runs the
+                // (kt-1, h = 1) block first, the older half (kt, h = 1) last
+                using H0 = std::integral_constant<int, 0>;
+                using H1 = std::integral_constant<int, 1>;
+                const int k0n = kt + 1 < nk ? (kt + 1) * BK : (1 << 29);
+                __builtin_amdgcn_sched_barrier(0);
+                // VAR 2097152: the younger half's pieces ride its (kt, h = 0) block instead — the
+                // second half of the step, away from the older half's pieces
+                constexpr bool LATE_DMA = (VAR & 2097152) != 0;
+                if (young && kt > 0) mf_half16(H1(), cwh, cwl, cwd, cah, cal, cur ^ 1, LATE_DMA ? (1 << 29) : k0n);
+                read_w16(cur, cwh, cwl, cwd);
+                read_a16(cur, 0, cah, cal);
+                mf_half16(H0(), cwh, cwl, cwd, cah, cal, cur ^ 1, !young || kt == 0 || LATE_DMA ? k0n : (1 << 29));
+                read_a16(cur, 1, cah, cal);
+                if (!young) mf_half16(H1(), cwh, cwl, cwd, cah, cal, cur ^ 1, 1 << 29);
+                __builtin_amdgcn_sched_barrier(0);
+                continue;
+            }
+            if constexpr ((VAR & 8388608) != 0) {
+                // VAR 8388608 (diagnostic): the A slice of step kt + 2 touched into L2 by one
+                // plain 4-B load per lane (lane = (row, part)), so the A pieces' DMA hits L2
+                if (kt + 2 < nk) {
+                    const f16* pa = A + (size_t)(m0 + (tid & 255)) * ld2 + (tid >> 8) * K + (kt + 2) * BK;
+                    unsigned dummy;
+                    asm volatile("global_load_dword %0, %1, off" : "=v"(dummy) : "v"(pa) : "memory");
+                }
+            }
             if constexpr (M16) {
                 const bool st_ok = kt + 1 < nk;
                 if ((VAR & 4) == 0 && (VAR & 32768) == 0 && st_ok) stage(cur ^ 1, (kt + 1) * BK);
@@ -1467,6 +1554,9 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 mfma3(F);
                 __builtin_amdgcn_sched_barrier(0);
             }
+        }
+        if constexpr (STAG) {
+            if (young) mf_half16(std::integral_constant<int, 1>(), cwh, cwl, cwd, cah, cal, 0, 1 << 29);   // (nk-1, h = 1)
         }
         // ---- transition
         const int last = (par + nk - 1) & 1;                      // buffer of the last K-step
@@ -2189,6 +2279,22 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         else if (cfg == 30 && dbg == 19) e = launch_x3s<EPI_BIAS_F16, 262144 | 16 | 4>(a, w, M, N, K, ep, st);
         else if (cfg == 30 && dbg == 16) e = launch_x3s<EPI_BIAS_F16, 262144 | 16 | 4 | 128>(a, w, M, N, K, ep, st);
         else if (cfg == 32 && dbg == 15) e = launch_x3s<EPI_BIAS_F32, 262144>(a, w, M, N, K, ep, st);
+        // half-step stagger of the younger wave half (VAR 524288): 40 production + stagger,
+        // 41 without staging or epilogue, 42 without epilogue, 43 the unstaggered 'neither'
+        else if (cfg == 32 && dbg == 40) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 524288>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 41) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 524288 | 3>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 42) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 524288 | 2>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 43) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 3>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 44) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 524288 | 2097152>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 45) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 524288 | 2097152 | 2>(a, w, M, N, K, ep, st);
+        else if (cfg == 31 && dbg == 44) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 524288 | 2097152>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 46) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 2 | 8>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 47) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 524288 | 2 | 8>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 48) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 8388608>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 49) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 8388608 | 2>(a, w, M, N, K, ep, st);
+        else if (cfg == 31 && dbg == 48) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 8388608>(a, w, M, N, K, ep, st);
+        else if (cfg == 31 && dbg == 40) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 524288>(a, w, M, N, K, ep, st);
+        else if (cfg == 30 && dbg == 40) e = launch_x3s<EPI_BIAS_F16, 262144 | 16 | 4 | 128 | 512 | 524288>(a, w, M, N, K, ep, st);
         else {   // dbg 0: the production variant (launch_gemm_x3s)
             const int epi = cfg == 30 ? EPI_BIAS_F16 : cfg == 31 ? EPI_GELU_F16 : EPI_BIAS_F32;
             e = launch_gemm_x3s(epi, a, w, 2 * K, M, N, K, ep, st);

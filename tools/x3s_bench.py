@@ -95,6 +95,13 @@ def main():
         d16 = (h2.float() - out16.float()).abs()
         bound = out16.float().abs() * 2 ** -10 + 1e-5 * out16.float().abs().max()
         assert bool((d16 <= bound).all()), (d16 / bound).max().item()
+        # half-step stagger (dbg 40): bitwise equal to the production kernel on every output
+        for cfg_s, o_a in ((32, out32), (31, out_img), (30, out16)):
+            o_b = torch.empty_like(o_a)
+            for dbg_s in ((40, 44) if cfg_s != 30 else (40,)):
+                assert call(cfg_s, A2, W2, o_a, K, 0) == 0 and call(cfg_s, A2, W2, o_b, K, dbg_s) == 0
+                torch.cuda.synchronize()
+                assert torch.equal(o_a, o_b), f"stagger differs (cfg {cfg_s}, dbg {dbg_s})"
         # the K-concatenated form: K x 3 operand (values irrelevant to timing)
         A3 = torch.cat([A2, A2[:, :K]], dim=1).contiguous()
         W3 = torch.cat([W2, W2[:, :K]], dim=1).contiguous()
@@ -118,7 +125,16 @@ def main():
                     ("x3s16-f32-spread", 32, A2, W2, out32, K, 27), ("x3s16-f32-noprio", 32, A2, W2, out32, K, 28),
                     ("x3s16-gelu2-spread", 31, A2, W2, out_img, K, 27),
                     ("x3s16-f32-olddma", 32, A2, W2, out32, K, 29), ("x3s16-gelu2-olddma", 31, A2, W2, out_img, K, 29), ("x3s16-gelu2-noprio", 31, A2, W2, out_img, K, 28), ("x3s16-f32-direct", 32, A2, W2, out32, K, 21),
-                    ("x3s-gelu2", 31, A2, W2, out_img, K, 0), ("kcat-persist-f16", 9, A3, W3, out16, 3 * K, 0)]
+                    ("x3s-gelu2", 31, A2, W2, out_img, K, 0), ("kcat-persist-f16", 9, A3, W3, out16, 3 * K, 0),
+                    ("x3s16-f32-stag", 32, A2, W2, out32, K, 40), ("x3s16-f32-stag-neither", 32, A2, W2, out32, K, 41),
+                    ("x3s16-f32-stag-noepi", 32, A2, W2, out32, K, 42), ("x3s16-f32-prodV-neither", 32, A2, W2, out32, K, 43),
+                    ("x3s16-gelu2-stag", 31, A2, W2, out_img, K, 40), ("x3s16-f16-stag", 30, A2, W2, out16, K, 40),
+                    ("x3s16-f16-prod", 30, A2, W2, out16, K, 0),
+                    ("x3s16-f32-stagL", 32, A2, W2, out32, K, 44), ("x3s16-f32-stagL-noepi", 32, A2, W2, out32, K, 45),
+                    ("x3s16-gelu2-stagL", 31, A2, W2, out_img, K, 44),
+                    ("x3s16-f32-noepi-nowait", 32, A2, W2, out32, K, 46), ("x3s16-f32-stag-noepi-nowait", 32, A2, W2, out32, K, 47),
+                    ("x3s16-f32-pfA", 32, A2, W2, out32, K, 48), ("x3s16-f32-pfA-noepi", 32, A2, W2, out32, K, 49),
+                    ("x3s16-gelu2-pfA", 31, A2, W2, out_img, K, 48)]
         if os.environ.get("VARIANTS"):
             keep = os.environ["VARIANTS"].split(",")
             variants = [v for v in variants if v[0] in keep]
