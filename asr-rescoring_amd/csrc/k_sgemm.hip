@@ -546,12 +546,13 @@ sgemm_splitk_sum_kernel(const float* __restrict__ ws, int splits, int M, int N, 
 // resident at once), 2 = 256×128×32 (8 waves of 64×64, 1 per CU; half the operand bytes per
 // FLOP of a 128×128 tile on the A side).
 struct SgCfg { int bm, bn, bk, occ; };
-constexpr int kSgNCfg = 10;
+constexpr int kSgNCfg = 11;
 constexpr SgCfg kSgCfg[kSgNCfg] = {{128, 128, 32, 2}, {128, 128, 16, 4}, {256, 128, 32, 1},
                                    {128, 128, 16, 3}, {128, 128, 32, 1},    // 3, 4: sgemm_pipe_kernel
                                    {128, 64, 32, 2},  {128, 64, 32, 3},     // 5, 6: 4 waves of 32×64
                                    {64, 64, 32, 4},   {64, 64, 32, 6},      // 7, 8: 2 waves of 32×64
-                                   {192, 128, 32, 2}};                      // 9: 4 waves of 96×64
+                                   {192, 128, 32, 2},                       // 9: 4 waves of 96×64
+                                   {256, 256, 32, 1}};                      // 10: 8 waves of 128×64
 
 // Modelled time (µs) of one configuration at a split count: dispatch rounds × (K-steps per
 // workgroup × the time a CU takes per K-step with its resident workgroups + a per-round
@@ -764,7 +765,8 @@ static hipError_t sg_run(int cfg, int M, int N, int K, const float* A, int lda, 
     else if (cfg == 6) SG_FORMS(sgemm_dma_kernel, 128, 64, 32, 32, 3);
     else if (cfg == 7) SG_FORMS(sgemm_dma_kernel, 64, 64, 32, 32, 4);
     else if (cfg == 8) SG_FORMS(sgemm_dma_kernel, 64, 64, 32, 32, 6);
-    else SG_FORMS(sgemm_dma_kernel, 192, 128, 96, 32, 2);
+    else if (cfg == 9) SG_FORMS(sgemm_dma_kernel, 192, 128, 96, 32, 2);
+    else SG_FORMS(sgemm_dma_kernel, 256, 256, 128, 32, 1);
 #undef SG_FORMS
 #undef SG_LAUNCH
     hipError_t e = hipGetLastError();
