@@ -1140,6 +1140,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                   "x3s epilogues");
     constexpr bool LNR = EPI == EPI_LNRES_IMG;
     static_assert(!LNR || ((VAR & 128) != 0 && (VAR & 2) == 0), "the LayerNorm epilogue is written for the 16x16 form");
+    static_assert((VAR & 16777216) == 0 || (LNR && (VAR & 16) != 0), "the permuted-column layout is written for the LayerNorm epilogue");
     extern __shared__ __attribute__((aligned(16))) char smem[];        // the LDS-DMA ring (2 stages)
     // wave-private epilogue slabs: a separate LDS object, so the compiler can tell the slab
     // reads do not alias the LDS-DMA writes in flight (no vmcnt wait before them)
@@ -1202,12 +1203,21 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     // addresses): half the address data per DMA instruction
     __amdgpu_buffer_rsrc_t rsA, rsW;
     int voffA[4], voffW[4];                       // lane byte offsets: (p & 1) row half x (r & 1) hi / lo
+    // VAR 16777216 (16x16 form): output columns permuted inside each 32-column group so that a
+    // lane's two 16-column MFMA blocks 2m, 2m + 1 hold 8 CONSECUTIVE output columns (32 m + 8 q4
+    // .. + 7) instead of two runs of 4: W image row 32 m + 16 jj + 4 q + e is W row
+    // 32 m + 8 q + 4 jj + e.  The epilogue's per-lane loads (bias, residual image, LayerNorm
+    // weights) become 16-B loads, half as many instructions.
+    constexpr bool PERM = M16 && (VAR & 16777216) != 0;
+    auto wperm = [](int L) {
+        return PERM ? (L & ~31) | (((L >> 2) & 3) << 3) | (((L >> 4) & 1) << 2) | (L & 3) : L;
+    };
 #pragma unroll
     for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int l = 0; l < 2; ++l) {
             voffA[2 * h + l] = ((prow + 128 * h) * (int)ld2 + l * K + pswz) * 2;
-            voffW[2 * h + l] = ((prow + 128 * h) * ldw + l * K + pswz) * 2;
+            voffW[2 * h + l] = (wperm(prow + 128 * h) * ldw + l * K + pswz) * 2;
         }
     auto set_rsrc = [&](int m0, int n0) {
         rsA = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * ld2), (short)0, (int)(256 * ld2 * 2), 0x00020000);
@@ -1569,7 +1579,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             // columns 16 j + 4 (l >> 4) .. +3 of the wave's 64
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const float* bp = ep.bias + cn0 + wn * WTN + 16 * j + 4 * q4;
+                const float* bp = ep.bias + cn0 + wn * WTN + (PERM ? 32 * (j >> 1) + 8 * q4 + 4 * (j & 1) : 16 * j + 4 * q4);
                 asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bq[j]) : "v"(bp) : "memory");
             }
             asm volatile("s_waitcnt vmcnt(0)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]) : : "memory");
@@ -1634,19 +1644,35 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 // layout, four row blocks at a time (as ln_res_img forms it)
                 // (loading it costs ~3 % of the step at C3 — 256 KB per tile at the ~50 GB/s one CU
                 // streams, RS_LNFUSE_DIAG=4 — and prefetching half of it beside the bias loads
-                // measured no better)
+                // measured no better; the permuted-column layout (PERM) halves its load count:
+                // +1.1 % end to end)
 #pragma unroll
                 for (int hh = 0; hh < 2; ++hh) {
                     half4 rh0[4][4], rl0[4][4];
                     const int rskip = (ep.diag & 4) ? 0 : 1;     // diag 4 (timing only): the tile's first rows
 #pragma unroll
-                    for (int ii = 0; ii < 4; ++ii)
+                    for (int ii = 0; ii < 4; ++ii) {
+                        const f16* prow_img = img + (size_t)(cm0 + rskip * (wm * WTM + 16 * (4 * hh + ii) + r16)) * ldc;
+                        if constexpr (PERM) {
+                            // blocks 2m, 2m + 1: 8 consecutive columns, one 16-B load per image
 #pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            const f16* p = img + (size_t)(cm0 + rskip * (wm * WTM + 16 * (4 * hh + ii) + r16)) * ldc + c0 + 16 * j;
-                            rh0[ii][j] = *(const half4*)p;
-                            rl0[ii][j] = *(const half4*)(p + H);
+                            for (int m = 0; m < 2; ++m) {
+                                const f16* p = prow_img + cn0 + wn * WTN + 32 * m + 8 * q4;
+                                const half8 vh = *(const half8*)p, vl = *(const half8*)(p + H);
+                                rh0[ii][2 * m] = (half4){vh[0], vh[1], vh[2], vh[3]};
+                                rh0[ii][2 * m + 1] = (half4){vh[4], vh[5], vh[6], vh[7]};
+                                rl0[ii][2 * m] = (half4){vl[0], vl[1], vl[2], vl[3]};
+                                rl0[ii][2 * m + 1] = (half4){vl[4], vl[5], vl[6], vl[7]};
+                            }
+                        } else {
+#pragma unroll
+                            for (int j = 0; j < 4; ++j) {
+                                const f16* p = prow_img + c0 + 16 * j;
+                                rh0[ii][j] = *(const half4*)p;
+                                rl0[ii][j] = *(const half4*)(p + H);
+                            }
                         }
+                    }
 #pragma unroll
                     for (int ii = 0; ii < 4; ++ii)
 #pragma unroll
@@ -1771,8 +1797,9 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 f32x4 gq[4], bb[4];                      // LayerNorm weight / bias of the lane's columns
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    gq[j] = *(const f32x4*)(ep.res_g + c0 + 16 * j);
-                    bb[j] = *(const f32x4*)(ep.res_b + c0 + 16 * j);
+                    const int cj = PERM ? cn0 + wn * WTN + 32 * (j >> 1) + 8 * q4 + 4 * (j & 1) : c0 + 16 * j;
+                    gq[j] = *(const f32x4*)(ep.res_g + cj);
+                    bb[j] = *(const f32x4*)(ep.res_b + cj);
                 }
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
@@ -1850,7 +1877,8 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                                     const f16 hi = (f16)x;
                                     h[e] = img == 0 ? hi : x3_lo(x, hi);
                                 }
-                                const int row = 16 * a + r16, byte = 32 * j + 8 * q4;
+                                const int row = 16 * a + r16,
+                                          byte = PERM ? 64 * (j >> 1) + 16 * q4 + 8 * (j & 1) : 32 * j + 8 * q4;
                                 *(half4*)(slb + row * 128 + (((byte >> 4) ^ (row & 7)) << 4) + (byte & 8)) = h;
                             }
                         f16* ob = (f16*)ep.out + (size_t)(cm0 + wm * WTM + 32 * i2) * ep.ldc + img * ep.nlog + cn0 + wn * WTN + 8 * c16;
@@ -2179,8 +2207,13 @@ hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_p
         case EPI_BIAS_F16:
             return mf32 ? launch_x3s<EPI_BIAS_F16, V32>(A, W, M_pad, N_pad, K, ep, st, ldw)
                         : launch_x3s<EPI_BIAS_F16, V>(A, W, M_pad, N_pad, K, ep, st, ldw);
-        case EPI_LNRES_IMG:
-            return launch_x3s<EPI_LNRES_IMG, V>(A, W, M_pad, N_pad, K, ep, st, ldw);
+        case EPI_LNRES_IMG: {
+            // the permuted-column layout (16-B epilogue loads; VAR 16777216): +1.1 % end to end
+            // (profiles/r3p2_lnperm_ab.txt); RS_LNPERM=0 keeps the plain column order (A/B knob)
+            static const bool perm = !(getenv("RS_LNPERM") && !strcmp(getenv("RS_LNPERM"), "0"));
+            return perm ? launch_x3s<EPI_LNRES_IMG, V | 16777216>(A, W, M_pad, N_pad, K, ep, st, ldw)
+                        : launch_x3s<EPI_LNRES_IMG, V>(A, W, M_pad, N_pad, K, ep, st, ldw);
+        }
     }
     return hipErrorInvalidValue;
 }
