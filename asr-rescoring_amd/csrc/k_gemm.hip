@@ -1974,6 +1974,14 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     }
 }
 
+// Sequence number of a LayerNorm-epilogue launch (the granule tag), process-wide: never 0.
+unsigned ln_tag_next() {
+    static std::atomic<unsigned> seq{0};
+    unsigned v = seq.fetch_add(1, std::memory_order_relaxed) + 1;
+    while (v == 0) v = seq.fetch_add(1, std::memory_order_relaxed) + 1;
+    return v;
+}
+
 int n_cus() {
     static int n = [] {
         int dev = 0, v = 0;
@@ -2022,10 +2030,10 @@ hipError_t launch_x3s(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
     e2.group_m = gm_env > 0 ? gm_env : 8;
     if constexpr (EPI == EPI_LNRES_IMG) {
         // granule tag: this launch's sequence number (never 0: the granules start zeroed), so a
-        // granule left by an earlier launch never matches
-        static unsigned seq = 0;
-        if (++seq == 0) seq = 1;
-        e2.ln_tag = seq;
+        // granule left by an earlier launch never matches.  One counter for every instance of the
+        // kernel (ln_tag_next): the O-projection and BertOutput instances share the granule buffer,
+        // and per-instance counters would repeat each other's tags
+        e2.ln_tag = ln_tag_next();
     }
     hipLaunchKernelGGL((gemm_x3s_kernel<EPI, VAR>), dim3(grid), dim3(512), smem, st, A, W, K, ldw > 0 ? ldw : 2 * K,
                        ntn, n_tiles, e2);
@@ -2213,6 +2221,9 @@ hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_p
             // the permuted-column layout (16-B epilogue loads; VAR 16777216): +1.1 % end to end
             // (profiles/r3p2_lnperm_ab.txt); RS_LNPERM=0 keeps the plain column order (A/B knob)
             static const bool perm = !(getenv("RS_LNPERM") && !strcmp(getenv("RS_LNPERM"), "0"));
+            // VAR 67108864 is a name tag only (the BertOutput launch, K = 3072), so rocprofv3 reports
+            // the O-projection and BertOutput instances separately
+            if (perm && K > 1024) return launch_x3s<EPI_LNRES_IMG, V | 16777216 | 67108864>(A, W, M_pad, N_pad, K, ep, st, ldw);
             return perm ? launch_x3s<EPI_LNRES_IMG, V | 16777216>(A, W, M_pad, N_pad, K, ep, st, ldw)
                         : launch_x3s<EPI_LNRES_IMG, V>(A, W, M_pad, N_pad, K, ep, st, ldw);
         }

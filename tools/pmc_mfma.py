@@ -18,6 +18,12 @@ EPI = {0: "qkv", 1: "ffn1", 2: "head_transform", 3: "res_f32(last layer)", 4: "d
 
 
 def kname(n):
+    m = re.search(r"gemm_x3s_kernelILi(\d+)ELi(\d+)E", n)
+    if m:
+        epi, var = int(m.group(1)), int(m.group(2))
+        if epi == 7:
+            return "x3s:ffn2+LN" if var & 67108864 else "x3s:oproj+LN"
+        return "x3s:" + {5: "qkv(f32 out)", 1: "ffn1(GELU image)", 3: "f16 out"}.get(epi, str(epi))
     m = re.search(r"gemm_persist_kernelILi(\d+)ELi(\d+)E", n)
     if m and int(m.group(2)) & 65536:
         return "gemm_persist:oproj"
