@@ -1154,7 +1154,34 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     int t = blockIdx.x;
     typedef __attribute__((address_space(1))) unsigned gu32;
     typedef __attribute__((address_space(1))) unsigned long long gu64;
-    if constexpr (LNR) {
+    if constexpr (LNR && (VAR & 134217728) != 0) {
+        // VAR 134217728: gangs formed inside XCD groups (blocks b, b + 8, ... share an XCD as
+        // dispatched; a different placement changes only speed): the workgroups of group x = b & 7
+        // take gangs of n_tiles_n consecutive positions p = b >> 3; the few left over in each
+        // group form the last gangs across groups.  A gang's column tiles then read their shared
+        // A panel through one L2.  Every workgroup is resident (grid <= CUs at one per CU), as
+        // with the ticket form.
+        const int G = gridDim.x, ntn = n_tiles_n, x = blockIdx.x & 7, pp = blockIdx.x >> 3;
+        int loc_before = 0, left_before = 0, nloc = 0, nx = 0;
+        for (int y = 0; y < 8; ++y) {
+            const int ny = G > y ? (G - y + 7) / 8 : 0, ly = ny / ntn * ntn;
+            if (y < x) {
+                loc_before += ly;
+                left_before += ny - ly;
+            }
+            if (y == x) {
+                nx = ny;
+                nloc = ly;
+            }
+            (void)nx;
+        }
+        int total_loc = 0;
+        for (int y = 0; y < 8; ++y) {
+            const int ny = G > y ? (G - y + 7) / 8 : 0;
+            total_loc += ny / ntn * ntn;
+        }
+        t = pp < nloc ? loc_before + pp : total_loc + left_before + (pp - nloc);
+    } else if constexpr (LNR) {
         // first tiles by ticket, in the order workgroups start: the grid is whole row panels and
         // fits the chip at one workgroup per CU, so each row panel's column tiles form a gang of
         // resident workgroups, and a gang walks the panels p, p + G, p + 2G, ... (G = gangs) with
@@ -2223,6 +2250,14 @@ hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_p
             static const bool perm = !(getenv("RS_LNPERM") && !strcmp(getenv("RS_LNPERM"), "0"));
             // VAR 67108864 is a name tag only (the BertOutput launch, K = 3072), so rocprofv3 reports
             // the O-projection and BertOutput instances separately
+            // gangs formed inside XCD groups (VAR 134217728): BertOutput -4 %, fetch per row 26.4 ->
+            // 20.0 KB, +0.6-0.8 % end to end (profiles/r3g2_lngang_xcd.txt); RS_LNGANG_XCD=0: the
+            // start-order ticket (A/B knob)
+            static const bool gx = !(getenv("RS_LNGANG_XCD") && !strcmp(getenv("RS_LNGANG_XCD"), "0"));
+            if (gx && perm) {
+                if (K > 1024) return launch_x3s<EPI_LNRES_IMG, V | 16777216 | 67108864 | 134217728>(A, W, M_pad, N_pad, K, ep, st, ldw);
+                return launch_x3s<EPI_LNRES_IMG, V | 16777216 | 134217728>(A, W, M_pad, N_pad, K, ep, st, ldw);
+            }
             if (perm && K > 1024) return launch_x3s<EPI_LNRES_IMG, V | 16777216 | 67108864>(A, W, M_pad, N_pad, K, ep, st, ldw);
             return perm ? launch_x3s<EPI_LNRES_IMG, V | 16777216>(A, W, M_pad, N_pad, K, ep, st, ldw)
                         : launch_x3s<EPI_LNRES_IMG, V>(A, W, M_pad, N_pad, K, ep, st, ldw);
