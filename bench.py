@@ -227,34 +227,44 @@ def main():
         threads = set_cpu_threads()
         model = TorchBert(weights, BERT_BASE)
         lm_np = lm.double().cpu().numpy()
-        rows_done, t_cpu, h, rel, ref_lm = 0, 0.0, 0, [], []
-        while t_cpu < args.cpu_seconds and h < nb.n_hyp:
-            sub_off = nb.hyp_off[h:h + 2] - nb.hyp_off[h]
-            toks = nb.tokens[nb.hyp_off[h]:nb.hyp_off[h + 1]]
-            t1 = time.perf_counter()
-            _, ref_pll = OB.pll_reference_pattern(model, toks, sub_off, batch_size=32, full_head=True)
-            t_cpu += time.perf_counter() - t1
-            rel.append(abs(lm_np[h] - ref_pll[0]) / abs(ref_pll[0]))
-            ref_lm.append(float(ref_pll[0]))
-            rows_done += int(sub_off[-1]) - 2
-            h += 1
-        # the rerank index from the CPU reference's own lm on the sampled utterances that were
-        # scored whole, against the HIP lm's (all 101 weights): a check of scoring + fusion
-        from oracle import rescore_ref as RR
+        # whole utterances, cheapest (fewest masked forwards) first, until the time budget: the
+        # sample then covers several utterances for the rerank check below (short hypotheses
+        # cost the CPU less per forward, so this errs towards a faster CPU baseline)
         Nb = args.nbest
-        uw = h // Nb
+        T_h = np.diff(nb.hyp_off)
+        cost_u = np.add.reduceat(T_h - 2, nb.utt_off[:-1])
+        rows_done, t_cpu, rel, done_u, ref_lm = 0, 0.0, [], [], {}
+        for u in np.argsort(cost_u, kind="stable"):
+            if t_cpu >= args.cpu_seconds:
+                break
+            for hh in range(nb.utt_off[u], nb.utt_off[u + 1]):
+                sub_off = nb.hyp_off[hh:hh + 2] - nb.hyp_off[hh]
+                toks = nb.tokens[nb.hyp_off[hh]:nb.hyp_off[hh + 1]]
+                t1 = time.perf_counter()
+                _, ref_pll = OB.pll_reference_pattern(model, toks, sub_off, batch_size=32, full_head=True)
+                t_cpu += time.perf_counter() - t1
+                rel.append(abs(lm_np[hh] - ref_pll[0]) / abs(ref_pll[0]))
+                ref_lm[hh] = float(ref_pll[0])
+                rows_done += int(sub_off[-1]) - 2
+            done_u.append(int(u))
+        h = len(ref_lm)
+        # the rerank index from the CPU reference's own lm on the sampled utterances, against
+        # the HIP lm's (all 101 weights): a check of scoring + fusion
+        from oracle import rescore_ref as RR
+        uw = len(done_u)
         rerank_same = None
-        if uw > 0:
-            am_s = nb.am[:uw * Nb].reshape(uw, Nb)
-            hyps_s = [[nb.hyp_words(u * Nb + i) for i in range(Nb)] for u in range(uw)]
-            refs_s = nb.refs[:uw]
-            _, _, arg_ref = RR.find_best_weight(am_s, np.asarray(ref_lm[:uw * Nb]).reshape(uw, Nb), hyps_s, refs_s, Nb)
-            _, _, arg_hip = RR.find_best_weight(am_s, lm_np[:uw * Nb].reshape(uw, Nb), hyps_s, refs_s, Nb)
+        if uw > 0 and all(nb.utt_off[u + 1] - nb.utt_off[u] == Nb for u in done_u):
+            idx = [nb.utt_off[u] + i for u in done_u for i in range(Nb)]
+            am_s = nb.am[idx].reshape(uw, Nb)
+            hyps_s = [[nb.hyp_words(nb.utt_off[u] + i) for i in range(Nb)] for u in done_u]
+            refs_s = [nb.refs[u] for u in done_u]
+            _, _, arg_ref = RR.find_best_weight(am_s, np.asarray([ref_lm[i] for i in idx]).reshape(uw, Nb), hyps_s, refs_s, Nb)
+            _, _, arg_hip = RR.find_best_weight(am_s, lm_np[idx].reshape(uw, Nb), hyps_s, refs_s, Nb)
             rerank_same = bool(np.array_equal(arg_ref, arg_hip))
         cpu = {"value": round(rows_done / t_cpu, 2), "unit": "masked fwd/s", "cores": threads,
                "cpu_model": _cpu_model(), "kind": "port",
-               "sample": f"{h} hypotheses ({rows_done} masked forwards) of rank-0 step "
-               f"input, reference work pattern (batch 32 padded rows, all-position logits + CE, "
+               "sample": f"{uw} whole utterances, {h} hypotheses ({rows_done} masked forwards; the "
+               f"cheapest utterances of rank-0 step input), reference work pattern (batch 32 padded rows, all-position logits + CE, "
                f"fp64 accumulation), torch {torch.__version__} CPU",
                "pll_max_rel_err_vs_gpu": float(max(rel)) if rel else None,
                "rerank_argmax_equal_cpu_reference_lm": rerank_same, "rerank_check_utterances": uw}
