@@ -2049,8 +2049,10 @@ hipError_t launch_x3s(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
         // whole row panels per round: the first tiles form complete gangs (every workgroup
         // resident at one per CU)
         grid = std::min(n_tiles, cus / ntn * ntn);
-        hipError_t e = hipMemsetAsync(ep.lncnt, 0, 16, st);          // the first-tile ticket
-        if (e != hipSuccess) return e;
+        if constexpr ((VAR & 134217728) == 0) {                      // (the XCD-group form takes no ticket)
+            hipError_t e = hipMemsetAsync(ep.lncnt, 0, 16, st);      // the first-tile ticket
+            if (e != hipSuccess) return e;
+        }
     }
     static const int gm_env = getenv("RS_GEMM_GROUP_M_X3S") ? atoi(getenv("RS_GEMM_GROUP_M_X3S")) : 0;
     EpiArgs e2 = ep;
