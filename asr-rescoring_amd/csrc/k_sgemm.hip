@@ -809,3 +809,13 @@ extern "C" int rs_debug_sgemm(int M, int N, int K, const float* A, int lda, int 
                               float* C, int ldc, int accum, void* stream) {
     return rs_debug_sgemm_cfg(-1, M, N, K, A, lda, a_kc, B, ldb, b_kc, C, ldc, accum, stream);
 }
+
+// Test entry (host only, no GPU call): the tile configuration and split count the trainer's
+// picker chooses for a GEMM shape (100 · cfg + splits; mcmc = both operands output-contiguous,
+// the weight-gradient form).
+extern "C" int rs_debug_sgemm_pick(int M, int N, int K, int mcmc) {
+    const int cfg = sg_pick(M, N, K, mcmc != 0);
+    int kc = 0;
+    const int sp = sg_splits(cfg, M, N, K, &kc, mcmc != 0);
+    return 100 * cfg + sp;
+}

@@ -1,0 +1,38 @@
+"""Trainer GEMM picker (k_sgemm.hip sg_pick / sg_model), host only: the tile configuration and
+split-K count chosen for the bert-base training shapes are the measured-best ones
+(profiles/r3u_sgemm_pick.txt), the choice depends on the shape alone (bitwise-reproducible
+training), and the workspace the trainer allocates covers every split the picker can choose."""
+import ctypes
+
+import pytest
+
+from asr_rescoring_amd import _lib
+
+
+@pytest.fixture(scope="module")
+def pick():
+    lib = _lib.load()
+    fn = lib.rs_debug_sgemm_pick
+    fn.restype = ctypes.c_int
+    fn.argtypes = [ctypes.c_int] * 4
+    return lambda M, N, K, mcmc=0: divmod(fn(M, N, K, mcmc), 100)
+
+
+def test_192x128_where_the_128x128_grid_leaves_a_half_round(pick):
+    # 5300 x 2304 x 768 forward: 756 tiles of 128x128 = 1.48 rounds; 504 tiles of 192x128 = 1
+    assert pick(5300, 2304, 768) == (9, 1)
+    # 5300 x 3072 x 768: 1008 tiles of 128x128 = 2 full rounds -> 128x128, no split
+    assert pick(5300, 3072, 768) == (0, 1)
+
+
+def test_small_batches_split_k(pick):
+    cfg, sp = pick(1100, 768, 768)
+    assert cfg == 0 and 2 <= sp <= 8
+    cfg, sp = pick(768, 768, 5300, 1)           # weight gradient over 5.3k tokens
+    assert sp > 1
+
+
+def test_choice_is_a_function_of_the_shape(pick):
+    a = [pick(m, n, k, f) for m, n, k, f in [(1100, 2304, 768, 0), (2304, 768, 1100, 1), (5300, 768, 3072, 0)]]
+    b = [pick(m, n, k, f) for m, n, k, f in [(1100, 2304, 768, 0), (2304, 768, 1100, 1), (5300, 768, 3072, 0)]]
+    assert a == b
