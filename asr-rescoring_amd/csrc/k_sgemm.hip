@@ -564,6 +564,8 @@ constexpr SgCfg kSgCfg[kSgNCfg] = {{128, 128, 32, 2}, {128, 128, 16, 4}, {256, 1
 // weight-gradient form (both operands output-contiguous, ds_read_b32 fragments) 10 % slower per
 // step.  192×128: 6.4 / 3.4 µs per K-step (profiles/r3u_sgemm_pick.txt).  Other tiles scale by
 // their K-step volume.
+int n_cus_sg();
+
 double sg_model(int cfg, int M, int N, int K, int sp, bool mcmc = false) {
     const SgCfg& g = kSgCfg[cfg];
     const long long tiles = (long long)((M + g.bm - 1) / g.bm) * ((N + g.bn - 1) / g.bn);
@@ -572,7 +574,7 @@ double sg_model(int cfg, int M, int N, int K, int sp, bool mcmc = false) {
     double t_one = 2.14 * vol, t_full = 3.74 * vol * g.occ / 2.0;
     if (cfg == 9) { t_one = 3.43; t_full = 6.4; }
     else if (mcmc) { t_one *= 1.1; t_full *= 1.1; }
-    const long long wgs = tiles * spr, cus = 256;
+    const long long wgs = tiles * spr, cus = n_cus_sg();
     double t = wgs <= cus ? per * t_one + 5.44
                           : (double)((wgs + cus * g.occ - 1) / (cus * g.occ)) * (per * t_full + 5.44);
     if (spr > 1) t += 4.24 + (2.0 * spr + 1.0) * M * N * 4.0 * 0.127e-6;
