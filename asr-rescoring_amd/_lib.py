@@ -62,6 +62,8 @@ _SIGS = {
     "rs_profile_enable": (ctypes.c_int, [P, ctypes.c_int]),
     "rs_profile_read": (ctypes.c_int, [P, ctypes.c_int, ctypes.POINTER(ctypes.c_double),
                                        ctypes.POINTER(I64), ctypes.POINTER(ctypes.c_double)]),
+    "rs_model_set_sync_check": (ctypes.c_int, [P, ctypes.c_int]),
+    "rs_check": (ctypes.c_int, [P, P]),
     "rs_model_destroy": (None, [P]),
     "rs_pairwise_edit": (ctypes.c_int, [P, P, P, P, I32, I32, P, P]),
     "rs_mbr_scores": (ctypes.c_int, [P, P, P, P, I32, I32, P, P, P]),
@@ -77,7 +79,7 @@ _SIGS = {
     "rs_trainer_reset_optimizer": (ctypes.c_int, [P]),
     "rs_trainer_dropout_step": (I64, [P]),
     "rs_trainer_set_dropout_step": (ctypes.c_int, [P, I64]),
-    "rs_dropout_keep": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_float, I64, P, P]),
+    "rs_dropout_keep": (ctypes.c_int, [ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_float, I64, P, P]),
     "rs_trainer_destroy": (None, [P]),
     "rs_bertscore_recall": (ctypes.c_int, [P, P, P, P, I32, P, P, P]),
     "rs_align": (ctypes.c_int, [P, P, P, P, I32, P, P, P, P, P, P, P, I32, P]),

@@ -131,12 +131,12 @@ def _score_rows_sharded(scorer, rows, rank: int, world: int) -> Dict[str, Dict[s
             output_score[r["utt_id"]] = {}
         output_score[r["utt_id"]][r["hyp_id"]] = 0
     import torch
-    if world == 1:
+    import torch.distributed as dist
+    if world == 1 and not dist.is_initialized():
         allv = scorer.row_logprobs(rows).cpu().tolist() if rows else []
         for r, s in zip(rows, allv):
             output_score[r["utt_id"]][r["hyp_id"]] += s
         return output_score
-    import torch.distributed as dist
     # utterance runs of consecutive rows; cost = token rows
     starts = [i for i, r in enumerate(rows) if i == 0 or r["utt_id"] != rows[i - 1]["utt_id"]] + [len(rows)]
     costs = [sum(len(rows[i]["input_ids"]) for i in range(a, b)) for a, b in zip(starts, starts[1:])]
@@ -216,7 +216,7 @@ def mlm_finetune(cfg) -> Dict[str, object]:
     try:
         for ep in range(1, epochs + 1):
             tr.reset_optimizer()
-            tr.set_dropout_step(ep << 20)            # epoch-keyed masks: a resumed run draws the same
+            tr.set_dropout_step(ep << 32)            # epoch-keyed masks: a resumed run draws the same
             order = torch.randperm(len(train_d[0]), generator=gen).numpy() if shuffle else None
             train_rec[ep - 1] = mlm_epoch(tr, *train_d, bs, update=True, order=order)
             print("epoch ", ep, " train loss: ", train_rec[ep - 1])
@@ -330,7 +330,7 @@ def rescorebert_train(cfg) -> Dict[str, object]:
         for ep in range(int(start) if resume else 1, int(get(cfg, "epoch", 1)) + 1):
             print("Epoch {}/{}".format(ep, get(cfg, "epoch", 1)))
             tr.reset_optimizer()
-            tr.set_dropout_step(ep << 20)            # epoch-keyed masks: a resumed run draws the same
+            tr.set_dropout_step(ep << 32)            # epoch-keyed masks: a resumed run draws the same
             train_rec.append(epoch_pass(train_f, True))
             print("epoch ", ep, " train loss: ", train_rec[-1], "\n")
             if dev_f is not None and all(f in dev_f["features"] for f in need):

@@ -1188,13 +1188,14 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         // each member keeping its column: t += gridDim.x.  The statistics exchange
         // (lnres_epilogue) is within a gang only, whose members all run the same panel sequence.
         if (tid == 0) {
+            // a monotonic counter: this launch's tickets start at ep.ln_base (kept by the host)
             const unsigned c = __hip_atomic_fetch_add((gu32*)ep.lncnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            *(unsigned*)(slabs + 2048) = c;
+            *(unsigned*)(slabs + 2048) = c - ep.ln_base;
         }
         __syncthreads();
         t = (int)*(const unsigned*)(slabs + 2048);
     }
-    if (t >= n_tiles) return;
+    if ((unsigned)t >= (unsigned)n_tiles) return;
     if constexpr ((VAR & 262144) != 0) {
         if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
     }
@@ -1795,9 +1796,10 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                                     pq[k][c] = __uint_as_float((unsigned)vb);
                                 }
                             }
+                        if (ep.diag & 8) ok = false;        // diag 8 (tests): peers never arrive
                         if (__all(ok)) break;
                         __builtin_amdgcn_s_sleep(1);
-                        if (++spins == (1u << 20)) {
+                        if (++spins == ((ep.diag & 8) ? (1u << 8) : (1u << 20))) {
                             if (lane == 0) __hip_atomic_store((gu32*)ep.lnerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             break;
                         }
@@ -1856,6 +1858,9 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             }
             char* slb = slabs + wave * 4096;
             const int rr0 = lane >> 3, c16 = lane & 7;
+            // VAR 33554432 (timing diagnostic, wrong results): every tile stores onto the rows of
+            // row panel 0 (L2-resident lines), separating the store path from the HBM write burst
+            const int sm0 = (VAR & 33554432) ? 0 : cm0;
             if constexpr (EPI == EPI_BIAS_F32 && (VAR & 256) != 0) {
                 // VAR 256: direct 16-B stores from the accumulator layout (4 lanes cover 64
                 // contiguous bytes of a row), no slab pass
@@ -1879,7 +1884,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                                 const int row = 16 * a + r16, ch = 4 * b + q4;
                                 *(f32x4*)(slb + row * 128 + ((ch ^ (row & 7)) << 4)) = acc16[2 * i2 + a][2 * j2 + b];
                             }
-                        float* ob = (float*)ep.out + (size_t)(cm0 + wm * WTM + 32 * i2) * ep.ldc + cn0 + wn * WTN + 32 * j2 + 4 * c16;
+                        float* ob = (float*)ep.out + (size_t)(sm0 + wm * WTM + 32 * i2) * ep.ldc + cn0 + wn * WTN + 32 * j2 + 4 * c16;
                         uint4 v[4];
                         slab_read4(slb, rr0, c16, v);
 #pragma unroll
@@ -1910,7 +1915,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                                           byte = PERM ? 64 * (j >> 1) + 16 * q4 + 8 * (j & 1) : 32 * j + 8 * q4;
                                 *(half4*)(slb + row * 128 + (((byte >> 4) ^ (row & 7)) << 4) + (byte & 8)) = h;
                             }
-                        f16* ob = (f16*)ep.out + (size_t)(cm0 + wm * WTM + 32 * i2) * ep.ldc + img * ep.nlog + cn0 + wn * WTN + 8 * c16;
+                        f16* ob = (f16*)ep.out + (size_t)(sm0 + wm * WTM + 32 * i2) * ep.ldc + img * ep.nlog + cn0 + wn * WTN + 8 * c16;
                         uint4 v[4];
                         slab_read4(slb, rr0, c16, v);
 #pragma unroll
@@ -2033,7 +2038,7 @@ hipError_t smem_attr_once(const void* fn, int smem, std::atomic<unsigned>& devs)
 
 template <int EPI, int VAR = 262144>
 hipError_t launch_x3s(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep, hipStream_t st,
-                      int ldw = 0) {
+                      int ldw = 0, bool coop = false) {
     constexpr int smem = 2 * 65536;                  // ring (2 x 64 KiB); + 32 KiB static wave slabs
     if (K % 32 || K < 64 || M_pad % 256 || N_pad % 256) return hipErrorInvalidValue;
     static std::atomic<unsigned> attr_devs{0};      // devices whose LDS limit is raised
@@ -2049,10 +2054,6 @@ hipError_t launch_x3s(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
         // whole row panels per round: the first tiles form complete gangs (every workgroup
         // resident at one per CU)
         grid = std::min(n_tiles, cus / ntn * ntn);
-        if constexpr ((VAR & 134217728) == 0) {                      // (the XCD-group form takes no ticket)
-            hipError_t e = hipMemsetAsync(ep.lncnt, 0, 16, st);      // the first-tile ticket
-            if (e != hipSuccess) return e;
-        }
     }
     static const int gm_env = getenv("RS_GEMM_GROUP_M_X3S") ? atoi(getenv("RS_GEMM_GROUP_M_X3S")) : 0;
     EpiArgs e2 = ep;
@@ -2063,10 +2064,28 @@ hipError_t launch_x3s(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
         // kernel (ln_tag_next): the O-projection and BertOutput instances share the granule buffer,
         // and per-instance counters would repeat each other's tags
         e2.ln_tag = ln_tag_next();
+        // the ticket counter is never reset: every workgroup of every ticket launch on it takes
+        // exactly one ticket, so this launch's first ticket is the sum of the earlier grids
+        if constexpr ((VAR & 134217728) == 0) {
+            if (!ep.ln_next) return hipErrorInvalidValue;
+            e2.ln_base = *ep.ln_next;
+            *ep.ln_next += (unsigned)grid;
+        }
     }
-    hipLaunchKernelGGL((gemm_x3s_kernel<EPI, VAR>), dim3(grid), dim3(512), smem, st, A, W, K, ldw > 0 ? ldw : 2 * K,
-                       ntn, n_tiles, e2);
-    return hipGetLastError();
+    const int ldw2 = ldw > 0 ? ldw : 2 * K;
+    if (coop) {
+        // the XCD-group gangs (VAR 134217728) take their membership from blockIdx, so every
+        // workgroup of the grid must be resident at once: a cooperative launch makes the runtime
+        // check the grid against the kernel's occupancy up front (hipErrorCooperativeLaunchTooLarge)
+        void* args[] = {(void*)&A, (void*)&W, (void*)&K, (void*)&ldw2, (void*)&ntn, (void*)&n_tiles, (void*)&e2};
+        return hipLaunchCooperativeKernel((const void*)gemm_x3s_kernel<EPI, VAR>, dim3(grid), dim3(512), args, smem, st);
+    }
+    hipLaunchKernelGGL((gemm_x3s_kernel<EPI, VAR>), dim3(grid), dim3(512), smem, st, A, W, K, ldw2, ntn, n_tiles, e2);
+    const hipError_t e = hipGetLastError();
+    if constexpr (EPI == EPI_LNRES_IMG && (VAR & 134217728) == 0) {
+        if (e != hipSuccess) *ep.ln_next -= (unsigned)grid;     // no workgroup took a ticket
+    }
+    return e;
 }
 
 template <int EPI, int VAR = 0>
@@ -2225,6 +2244,15 @@ hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
 
 int gemm_row_align() { return 256; }
 
+// Workgroups of one fused residual + LayerNorm GEMM launch (EPI_LNRES_IMG): whole gangs of the
+// N_pad / 256 column tiles of a row panel, at one workgroup per CU.  A launch over P row panels
+// runs ceil(P / gangs) rounds of panels, so the host cuts its chunks at multiples of
+// 256 * gangs rows (run_all).
+int gemm_lnres_workgroups(int N_pad) {
+    const int ntn = N_pad / 256, cus = n_cus() / 8 * 8;
+    return ntn > 0 ? cus / ntn * ntn : 0;
+}
+
 // Production split-operand fp16x3 GEMM: LDS-DMA by buffer_load ... lds (VAR 16) spread over the
 // MFMAs (VAR 4), younger wave half at s_setprio 1 (VAR 262144); tools/x3s_bench.py.
 hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_pad, int N_pad, int K,
@@ -2247,22 +2275,27 @@ hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_p
             return mf32 ? launch_x3s<EPI_BIAS_F16, V32>(A, W, M_pad, N_pad, K, ep, st, ldw)
                         : launch_x3s<EPI_BIAS_F16, V>(A, W, M_pad, N_pad, K, ep, st, ldw);
         case EPI_LNRES_IMG: {
-            // the permuted-column layout (16-B epilogue loads; VAR 16777216): +1.1 % end to end
-            // (profiles/r3p2_lnperm_ab.txt); RS_LNPERM=0 keeps the plain column order (A/B knob)
-            static const bool perm = !(getenv("RS_LNPERM") && !strcmp(getenv("RS_LNPERM"), "0"));
-            // VAR 67108864 is a name tag only (the BertOutput launch, K = 3072), so rocprofv3 reports
-            // the O-projection and BertOutput instances separately
-            // gangs formed inside XCD groups (VAR 134217728): BertOutput -4 %, fetch per row 26.4 ->
-            // 20.0 KB, +0.6-0.8 % end to end (profiles/r3g2_lngang_xcd.txt); RS_LNGANG_XCD=0: the
-            // start-order ticket (A/B knob)
-            static const bool gx = !(getenv("RS_LNGANG_XCD") && !strcmp(getenv("RS_LNGANG_XCD"), "0"));
-            if (gx && perm) {
-                if (K > 1024) return launch_x3s<EPI_LNRES_IMG, V | 16777216 | 67108864 | 134217728>(A, W, M_pad, N_pad, K, ep, st, ldw);
-                return launch_x3s<EPI_LNRES_IMG, V | 16777216 | 134217728>(A, W, M_pad, N_pad, K, ep, st, ldw);
+            // Output columns permuted inside 32-column groups (VAR 16777216: 16-B epilogue loads,
+            // +1.1 % end to end, profiles/r3p2_lnperm_ab.txt); VAR 67108864 is a name tag only (the
+            // BertOutput launch, K = 3072), so rocprofv3 reports the two instances separately.
+            // Gang formation (RS_LNGANG, read per call):
+            //   "ticket" (default): gangs of consecutive start-order tickets.  Deadlock-free at ANY
+            //       residency (a gang's members have all started before the next gang forms; complete
+            //       gangs finish and free their CUs), so a GPU shared with other kernels or processes
+            //       only slows the launch down.
+            //   "xcd": gangs inside XCD groups from blockIdx (VAR 134217728; a panel's column tiles
+            //       share one L2: BertOutput fetch 26.4 -> 20.0 KB per row, profiles/r3g2_lngang_xcd.txt).
+            //       Needs the whole grid resident; launched cooperatively, so the runtime refuses a
+            //       grid the occupancy does not admit.
+            const char* g = getenv("RS_LNGANG");
+            const bool xcd = g && !strcmp(g, "xcd");
+            constexpr int VL = V | 16777216;
+            if (xcd) {
+                if (K > 1024) return launch_x3s<EPI_LNRES_IMG, VL | 67108864 | 134217728>(A, W, M_pad, N_pad, K, ep, st, ldw, true);
+                return launch_x3s<EPI_LNRES_IMG, VL | 134217728>(A, W, M_pad, N_pad, K, ep, st, ldw, true);
             }
-            if (perm && K > 1024) return launch_x3s<EPI_LNRES_IMG, V | 16777216 | 67108864>(A, W, M_pad, N_pad, K, ep, st, ldw);
-            return perm ? launch_x3s<EPI_LNRES_IMG, V | 16777216>(A, W, M_pad, N_pad, K, ep, st, ldw)
-                        : launch_x3s<EPI_LNRES_IMG, V>(A, W, M_pad, N_pad, K, ep, st, ldw);
+            if (K > 1024) return launch_x3s<EPI_LNRES_IMG, VL | 67108864>(A, W, M_pad, N_pad, K, ep, st, ldw);
+            return launch_x3s<EPI_LNRES_IMG, VL>(A, W, M_pad, N_pad, K, ep, st, ldw);
         }
     }
     return hipErrorInvalidValue;
@@ -2378,6 +2411,16 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         else if (cfg == 31 && dbg == 48) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 8388608>(a, w, M, N, K, ep, st);
         else if (cfg == 31 && dbg == 40) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 524288>(a, w, M, N, K, ep, st);
         else if (cfg == 30 && dbg == 40) e = launch_x3s<EPI_BIAS_F16, 262144 | 16 | 4 | 128 | 512 | 524288>(a, w, M, N, K, ep, st);
+        // round 4 epilogue probes: 50 production + DMA never waited for (so the next tile's K loop
+        // never waits for this tile's stores), 51 stores aliased onto panel 0 (no HBM write burst),
+        // 52 production without the epilogue (GELU image)
+        else if (cfg == 32 && dbg == 50) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 8>(a, w, M, N, K, ep, st);
+        else if (cfg == 31 && dbg == 50) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 8>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 51) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 33554432>(a, w, M, N, K, ep, st);
+        else if (cfg == 31 && dbg == 51) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 33554432>(a, w, M, N, K, ep, st);
+        else if (cfg == 31 && dbg == 52) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 2>(a, w, M, N, K, ep, st);
+        else if (cfg == 32 && dbg == 53) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 8 | 33554432>(a, w, M, N, K, ep, st);
+        else if (cfg == 31 && dbg == 53) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 8 | 33554432>(a, w, M, N, K, ep, st);
         else {   // dbg 0: the production variant (launch_gemm_x3s)
             const int epi = cfg == 30 ? EPI_BIAS_F16 : cfg == 31 ? EPI_GELU_F16 : EPI_BIAS_F32;
             e = launch_gemm_x3s(epi, a, w, 2 * K, M, N, K, ep, st);
@@ -2466,4 +2509,32 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
 #undef RS_DBG
 #undef RS_DBG16
     return e == hipSuccess ? 0 : -2;
+}
+
+// Test utility (not part of the scoring path): keeps `blocks` workgroups resident for `usec`
+// microseconds, one per CU (each declares the whole 160 KiB of LDS), on `stream` — a kernel of
+// another stream (or process) holding CUs while the scorer runs.  Bounded by the constant-rate
+// s_memrealtime clock (100 MHz): every wave exits once the time is up.
+namespace {
+__global__ void __launch_bounds__(64) occupy_kernel(long long ticks, int* out) {
+    extern __shared__ int lds_hold[];
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    int spins = 0;
+    while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
+        __builtin_amdgcn_s_sleep(8);
+        ++spins;
+    }
+    lds_hold[threadIdx.x] = spins;
+    __syncthreads();
+    if (threadIdx.x == 0 && out) out[blockIdx.x] = lds_hold[0];     // vector store
+}
+}  // namespace
+
+extern "C" int rs_debug_occupy(int blocks, int usec, int* d_out, void* stream) {
+    if (blocks <= 0 || blocks > 4096 || usec <= 0 || usec > 2000000) return -1;
+    constexpr int smem = 160 * 1024;
+    static std::atomic<unsigned> attr_devs{0};
+    if (smem_attr_once((const void*)occupy_kernel, smem, attr_devs) != hipSuccess) return -2;
+    hipLaunchKernelGGL(occupy_kernel, dim3(blocks), dim3(64), smem, (hipStream_t)stream, (long long)usec * 100, d_out);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
 }

@@ -566,7 +566,9 @@ constexpr SgCfg kSgCfg[kSgNCfg] = {{128, 128, 32, 2}, {128, 128, 16, 4}, {256, 1
 // their K-step volume.
 int n_cus_sg();
 
-double sg_model(int cfg, int M, int N, int K, int sp, bool mcmc = false) {
+// `cus`: the device's CU count (n_cus_sg() on the trainer's path; an explicit value in the host-only
+// picker test), so the pick is a function of the shape and the CU count
+double sg_model(int cfg, int M, int N, int K, int sp, bool mcmc, int cus_) {
     const SgCfg& g = kSgCfg[cfg];
     const long long tiles = (long long)((M + g.bm - 1) / g.bm) * ((N + g.bn - 1) / g.bn);
     const int steps = (K + g.bk - 1) / g.bk, per = (steps + sp - 1) / sp, spr = (steps + per - 1) / per;
@@ -574,14 +576,14 @@ double sg_model(int cfg, int M, int N, int K, int sp, bool mcmc = false) {
     double t_one = 2.14 * vol, t_full = 3.74 * vol * g.occ / 2.0;
     if (cfg == 9) { t_one = 3.43; t_full = 6.4; }
     else if (mcmc) { t_one *= 1.1; t_full *= 1.1; }
-    const long long wgs = tiles * spr, cus = n_cus_sg();
+    const long long wgs = tiles * spr, cus = cus_;
     double t = wgs <= cus ? per * t_one + 5.44
                           : (double)((wgs + cus * g.occ - 1) / (cus * g.occ)) * (per * t_full + 5.44);
     if (spr > 1) t += 4.24 + (2.0 * spr + 1.0) * M * N * 4.0 * 0.127e-6;
     return t;
 }
 
-int sg_splits(int cfg, int M, int N, int K, int* kc, bool mcmc = false) {
+int sg_splits(int cfg, int M, int N, int K, int* kc, bool mcmc, int cus) {
     const SgCfg& g = kSgCfg[cfg];
     const int steps = (K + g.bk - 1) / g.bk;
     // the split count with the lowest modelled time (at least 4 K-steps per split).
@@ -596,7 +598,7 @@ int sg_splits(int cfg, int M, int N, int K, int* kc, bool mcmc = false) {
     } else {
         double best = 1e30;
         for (int sp = 1; sp <= 16 && sp <= std::max(1, steps / 4); ++sp) {
-            const double t = sg_model(cfg, M, N, K, sp, mcmc);
+            const double t = sg_model(cfg, M, N, K, sp, mcmc, cus);
             if (t < best) {
                 best = t;
                 splits = sp;
@@ -611,8 +613,9 @@ int sg_splits(int cfg, int M, int N, int K, int* kc, bool mcmc = false) {
 // The tile configuration: 128×128 (cfg 0) or 192×128 (cfg 9), whichever the model times lower
 // at its best split (192×128 wins where the 128×128 grid leaves a half-empty last round, e.g.
 // 5300 × 2304).  RS_SGEMM_CFG=0..9 forces a configuration (A/B knob).  The choice depends on
-// the shape only, so a shape's results stay bitwise reproducible.
-int sg_pick(int M, int N, int K, bool mcmc) {
+// the shape and the device's CU count only, so a shape's results stay bitwise reproducible on a
+// given device model.
+int sg_pick(int M, int N, int K, bool mcmc, int cus) {
     static const int forced = [] {
         const char* v = getenv("RS_SGEMM_CFG");
         return v ? atoi(v) : -1;
@@ -622,8 +625,8 @@ int sg_pick(int M, int N, int K, bool mcmc) {
     double tb = 1e30;
     for (int cfg : {0, 9}) {
         int kc = 0;
-        const int sp = sg_splits(cfg, M, N, K, &kc, mcmc);
-        const double t = sg_model(cfg, M, N, K, sp, mcmc);
+        const int sp = sg_splits(cfg, M, N, K, &kc, mcmc, cus);
+        const double t = sg_model(cfg, M, N, K, sp, mcmc, cus);
         if (t < 0.97 * tb) {
             tb = t;
             best = cfg;
@@ -689,7 +692,7 @@ size_t tr_sgemm_ws_floats(int M, int N, int K) {
     for (int cfg = 0; cfg < kSgNCfg; ++cfg) {  // any configuration the picker or the knob may choose
         int kc = 0;
         for (int mc = 0; mc < 2; ++mc) {
-            const int s = sg_splits(cfg, M, N, K, &kc, mc != 0);
+            const int s = sg_splits(cfg, M, N, K, &kc, mc != 0, n_cus_sg());
             if (s > 1) w = std::max(w, (size_t)s * M * N);
         }
     }
@@ -740,7 +743,7 @@ static hipError_t sg_run(int cfg, int M, int N, int K, const float* A, int lda, 
         return hipGetLastError();
     }
     int kc = 0;
-    const int splits = sg_splits(cfg, M, N, K, &kc, !a_kc && !b_kc);
+    const int splits = sg_splits(cfg, M, N, K, &kc, !a_kc && !b_kc, n_cus_sg());
     float* P = nullptr;
     if (splits > 1) {
         if (!ws || ws_floats < (size_t)splits * M * N) return hipErrorInvalidValue;
@@ -781,7 +784,7 @@ static hipError_t sg_run(int cfg, int M, int N, int K, const float* A, int lda, 
 
 hipError_t tr_sgemm(int M, int N, int K, const float* A, int lda, bool a_kc, const float* B, int ldb, bool b_kc,
                     float* C, int ldc, int accum, float* ws, size_t ws_floats, hipStream_t s) {
-    return sg_run(sg_pick(M, N, K, !a_kc && !b_kc), M, N, K, A, lda, a_kc, B, ldb, b_kc, C, ldc, accum, ws, ws_floats, s);
+    return sg_run(sg_pick(M, N, K, !a_kc && !b_kc, n_cus_sg()), M, N, K, A, lda, a_kc, B, ldb, b_kc, C, ldc, accum, ws, ws_floats, s);
 }
 
 // Test / timing entry (not part of the scoring path): one trainer GEMM in the given operand
@@ -802,7 +805,7 @@ extern "C" int rs_debug_sgemm_cfg(int cfg, int M, int N, int K, const float* A, 
         if (hipMalloc(&ws, wsf * 4) != hipSuccess) return -3;
         ws_cap = wsf;
     }
-    hipError_t e = sg_run(cfg < 0 ? sg_pick(M, N, K, a_kc == 0 && b_kc == 0) : cfg, M, N, K, A, lda, a_kc != 0, B, ldb, b_kc != 0, C, ldc,
+    hipError_t e = sg_run(cfg < 0 ? sg_pick(M, N, K, a_kc == 0 && b_kc == 0, n_cus_sg()) : cfg, M, N, K, A, lda, a_kc != 0, B, ldb, b_kc != 0, C, ldc,
                           accum, ws, ws_cap, (hipStream_t)stream);
     return e == hipSuccess ? 0 : -2;
 }
@@ -813,11 +816,12 @@ extern "C" int rs_debug_sgemm(int M, int N, int K, const float* A, int lda, int 
 }
 
 // Test entry (host only, no GPU call): the tile configuration and split count the trainer's
-// picker chooses for a GEMM shape (100 · cfg + splits; mcmc = both operands output-contiguous,
-// the weight-gradient form).
-extern "C" int rs_debug_sgemm_pick(int M, int N, int K, int mcmc) {
-    const int cfg = sg_pick(M, N, K, mcmc != 0);
+// picker chooses for a GEMM shape on a device of `cus` CUs (100 · cfg + splits; mcmc = both
+// operands output-contiguous, the weight-gradient form).
+extern "C" int rs_debug_sgemm_pick(int M, int N, int K, int mcmc, int cus) {
+    if (cus <= 0) return -1;
+    const int cfg = sg_pick(M, N, K, mcmc != 0, cus);
     int kc = 0;
-    const int sp = sg_splits(cfg, M, N, K, &kc, mcmc != 0);
+    const int sp = sg_splits(cfg, M, N, K, &kc, mcmc != 0, cus);
     return 100 * cfg + sp;
 }

@@ -83,13 +83,15 @@ struct rs_model {
     int kx = 1;                 // fp16 operand image width (1: fp16, 3: fp16x3)
     DevBuf xst, h16, t32, qkv, ctx, inter;   // xst: (mean, rstd) of the pre-LN rows in t32
     DevBuf xst1;                // statistics of the post-attention stream (deferred residual)
-    DevBuf lnx, lncnt, lnerr;   // EPI_LNRES_IMG: per-tile row statistics, claim / arrival words,
-                                // sticky statistics-wait timeout flag
+    DevBuf lnx, lncnt, lnerr;   // EPI_LNRES_IMG: per-tile row statistics, the monotonic ticket
+                                // counter, sticky statistics-wait timeout flag
+    unsigned ln_next = 0;       // first ticket of the next ticket-gang launch (host copy of lncnt[0])
     DevBuf ctxq, resq, tq32, hq32, hq16, interq, lab, llog, part, rowlp_tmp;
     DevBuf meta, hypoff;
     f16* emb_dst = nullptr;     // MODE_EMB output (rs_token_embed / rs_bertscore_recall)
     DevBuf emb, plan;           // rs_bertscore_recall: token embeddings, work-item plan
-    DevBuf flag;                // non-finite-output flag of the last scoring call (range guard)
+    DevBuf flag;                // non-finite-output flag of the last scoring call(s) (range guard)
+    bool sync_check = true;     // scoring calls synchronise and report their flags (rs_model_set_sync_check)
     int* pinned_flag = nullptr;
     int* pinned_plan = nullptr;
     size_t pinned_plan_cap = 0;
@@ -170,28 +172,53 @@ __global__ void __launch_bounds__(256) nonfinite_kernel(const T* __restrict__ v,
     if (bad) flag[0] = 1;          // plain vector store; every writer stores the same value
 }
 
-template <class T>
-int check_finite(rs_model* m, hipStream_t st, const T* p, size_t n, const char* what) {
-    if (n == 0) return RS_OK;
-    HIPTRY(m->flag.ensure(4));
+// Reads the flags (non-finite output, statistics-wait timeout) after synchronising the stream,
+// clears them and turns them into the call's error.
+int report_flags(rs_model* m, hipStream_t st, const char* what) {
     if (!m->pinned_flag) HIPTRY(hipHostMalloc((void**)&m->pinned_flag, 8, hipHostMallocDefault));
-    HIPTRY(hipMemsetAsync(m->flag.p, 0, 4, st));
-    const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 2048);
-    hipLaunchKernelGGL(nonfinite_kernel<T>, dim3(blocks), dim3(256), 0, st, p, n, m->flag.as<int>());
-    HIPTRY(hipGetLastError());
-    HIPTRY(hipMemcpyAsync(m->pinned_flag, m->flag.p, 4, hipMemcpyDeviceToHost, st));
+    m->pinned_flag[0] = 0;
     m->pinned_flag[1] = 0;
+    if (m->flag.p) HIPTRY(hipMemcpyAsync(m->pinned_flag, m->flag.p, 4, hipMemcpyDeviceToHost, st));
     if (m->lnerr.p) HIPTRY(hipMemcpyAsync(m->pinned_flag + 1, m->lnerr.p, 4, hipMemcpyDeviceToHost, st));
     HIPTRY(hipStreamSynchronize(st));
-    if (m->pinned_flag[1]) {
+    const int bad = m->pinned_flag[0], lnto = m->pinned_flag[1];
+    if (bad && m->flag.p) HIPTRY(hipMemset(m->flag.p, 0, 4));
+    if (lnto) {
         HIPTRY(hipMemset(m->lnerr.p, 0, 4));
         return fail(RS_EHIP, "a residual-LayerNorm GEMM timed out waiting for its row statistics "
-                                  "(set RS_LNFUSE=0 to use the separate LayerNorm pass)");
+                             "(set RS_LNFUSE=0 to use the separate LayerNorm pass)");
     }
-    if (*m->pinned_flag)
+    if (bad)
         return fail(RS_EUNSUP, std::string("non-finite ") + what +
                                    ": an activation left the fp16 range of the operand images (|x| > 65504); "
                                    "the fp32 reference stays finite here");
+    return RS_OK;
+}
+
+// End of every scoring call: one pass over its outputs sets the non-finite flag.  Synchronous
+// mode (default): the call waits for its stream and reports the flags.  Deferred mode
+// (rs_model_set_sync_check(m, 0)): the pass is only enqueued, the flags accumulate on the device
+// and rs_check reports them, so pipelined callers keep their stream asynchronous.
+template <class T>
+int check_finite(rs_model* m, hipStream_t st, const T* p, size_t n, const char* what) {
+    if (!m->flag.p) {
+        HIPTRY(m->flag.ensure(4));
+        HIPTRY(hipMemset(m->flag.p, 0, 4));
+    }
+    if (n > 0) {
+        const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 2048);
+        hipLaunchKernelGGL(nonfinite_kernel<T>, dim3(blocks), dim3(256), 0, st, p, n, m->flag.as<int>());
+        HIPTRY(hipGetLastError());
+    }
+    if (!m->sync_check) return RS_OK;
+    return report_flags(m, st, what);
+}
+
+// Start of every scoring call in synchronous mode: a timeout flag left by an earlier call that
+// failed before its report is dropped (each call reports only its own).
+int begin_call(rs_model* m, hipStream_t st) {
+    if (m->sync_check && m->lnerr.p) HIPTRY(hipMemsetAsync(m->lnerr.p, 0, 4, st));
+    if (m->sync_check && m->flag.p) HIPTRY(hipMemsetAsync(m->flag.p, 0, 4, st));
     return RS_OK;
 }
 
@@ -211,7 +238,11 @@ int reserve_impl(rs_model* m, int64_t max_rows) {
     HIPTRY(m->xst1.ensure(M * sizeof(float2)));
     HIPTRY(m->lnx.ensure(lnres_granules((int)M) * 8));
     HIPTRY(hipMemset(m->lnx.p, 0, m->lnx.bytes));               // granule tags start at 0 (never a launch's)
-    HIPTRY(m->lncnt.ensure(16));
+    if (!m->lncnt.p) {
+        HIPTRY(m->lncnt.ensure(16));
+        HIPTRY(hipMemset(m->lncnt.p, 0, 16));
+        m->ln_next = 0;
+    }
     HIPTRY(m->lnerr.ensure(16));
     HIPTRY(hipMemset(m->lnerr.p, 0, 16));
     HIPTRY(m->h16.ensure(M * H * 2 * kx));
@@ -455,9 +486,11 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
                 EpiArgs e{};
                 e.bias = bias; e.out = h16; e.ldc = 2 * H; e.nlog = H; e.res_g = g; e.res_b = be;
                 e.ln_eps = cf.ln_eps; e.lnx = m->lnx.p; e.lncnt = m->lncnt.as<unsigned>();
+                e.ln_next = &m->ln_next;
                 e.lnerr = m->lnerr.as<unsigned>();
-                static const int diag = getenv("RS_LNFUSE_DIAG") ? atoi(getenv("RS_LNFUSE_DIAG")) : 0;
-                e.diag = diag;
+                // RS_LNFUSE_DIAG (tests / timing only; read per call): 8 = the statistics wait
+                // times out at once (the RS_EHIP path)
+                e.diag = getenv("RS_LNFUSE_DIAG") ? atoi(getenv("RS_LNFUSE_DIAG")) : 0;
                 return e;
             };
             if (lnfuse) {
@@ -624,15 +657,31 @@ int run_all(rs_model* m, hipStream_t st, const int* d_tok, SeqList& sl, int mode
     if (m->max_rows == 0)
         if (int r = reserve_impl(m, 65536)) return r;
     HIPTRY(hipSetDevice(m->device));
+    if (int r = begin_call(m, st)) return r;
     const size_t S = sl.size();
     std::vector<Chunk> chunks;
+    // Chunk rows: with the fused residual + LayerNorm GEMMs (lnfuse), a chunk of P row panels runs
+    // ceil(P / G) rounds of whole panels on G = gemm_lnres_workgroups / (H / 256) gangs, so the
+    // chunks are cut at a multiple of 256 * G rows (bert-base on 256 CUs: 85 gangs, 21760 rows;
+    // 262144 -> 261120 rows = 12 full rounds instead of 12 + a 4-panel 13th).  RS_CHUNK_ALIGN=0
+    // keeps max_rows (read per call).
+    int64_t cap = m->max_rows;
+    {
+        const char* ca = getenv("RS_CHUNK_ALIGN");
+        const bool lnf = m->kx == 3 && x3s_on(m->cfg) && x3s_imgres_on() && lnfuse_on(m->cfg);
+        const int ntn = m->cfg.hidden / 256;
+        if (lnf && !(ca && !strcmp(ca, "0")) && ntn > 0) {
+            const int64_t unit = (int64_t)256 * (gemm_lnres_workgroups(m->cfg.hidden) / ntn);
+            if (unit > 0 && cap >= unit) cap = cap / unit * unit;
+        }
+    }
     int rows = 0, s0 = 0, max_len = 0;
     for (size_t s = 0; s < S; ++s) {
         const int T = sl.len[s];
         if (T > m->cfg.max_pos) return fail(RS_EUNSUP, "sequence longer than max_position_embeddings");
         if (T < 1) return fail(RS_EARG, "empty sequence");
         if (T > m->max_rows) return fail(RS_EARG, "sequence longer than the reserved rows");
-        if (rows + T > m->max_rows || (int)s - s0 >= m->s_cap) {
+        if (rows + T > cap || (int)s - s0 >= m->s_cap) {
             chunks.push_back({s0, (int)s, rows, 0, max_len});
             s0 = (int)s;
             rows = 0;
@@ -996,6 +1045,18 @@ int rs_bertscore_recall(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_
     HIPTRY(launch_bertscore_recall(m->emb.as<f16>(), H, d + w_items + w_moff, d + w_items + w_moff + n_hyp + 1,
                                    (const long long*)(d + w_items), (const int4*)d, n_items, d_rmat, d_rmat0, st, two));
     return RS_OK;
+}
+
+int rs_model_set_sync_check(rs_model* m, int on) {
+    if (!m) return fail(RS_EARG, "null model");
+    m->sync_check = on != 0;
+    return RS_OK;
+}
+
+int rs_check(rs_model* m, void* stream) {
+    if (!m) return fail(RS_EARG, "null model");
+    HIPTRY(hipSetDevice(m->device));
+    return report_flags(m, (hipStream_t)stream, "scores");
 }
 
 int rs_profile_enable(rs_model* m, int on) {

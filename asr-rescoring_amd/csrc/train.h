@@ -18,14 +18,16 @@
 // the attention-probability dropout, BertSelfOutput / BertOutput dropout on the dense output
 // before the residual add), inverted scaling x * 1/(1-p) on kept elements.  The keep bit of
 // element e of site `site` in dropout step `step` is a counter-based draw,
-//   keep = Philox4x32-10(counter = (e_lo, e_hi, site, 0), key = (seed, step)).word0 >= thresh,
+//   keep = Philox4x32-10(counter = (e_lo, e_hi, site, step_hi), key = (seed, step_lo)).word0 >= thresh,
 //   thresh = p * 2^32,
+// with the 64-bit dropout step split into its words (the CLI keys epoch k's steps from k << 32, so
+// every epoch has 2^32 steps of its own; steps below 2^32 have step_hi = 0, the round-3 masks),
 // so no mask is stored: the backward recomputes the same bits, and a step is bitwise
 // reproducible.  Sites: 0 = embeddings; layer l: 1 + 3l attention probabilities (element =
 // its index in the saved-P layout), 2 + 3l self-output, 3 + 3l output (element = row * H + c).
 // thresh == 0: off (p = 0, the fixture-pinned mode).
 struct TrDrop {
-    uint32_t seed = 0, step = 0, site = 0, thresh = 0;
+    uint32_t seed = 0, step = 0, site = 0, thresh = 0, step_hi = 0;
     float scale = 1.f;
 };
 
@@ -46,7 +48,7 @@ __host__ __device__ inline uint32_t tr_philox_w0(uint32_t c0, uint32_t c1, uint3
 }
 
 __host__ __device__ inline bool tr_keep(const TrDrop& d, unsigned long long e) {
-    return tr_philox_w0((uint32_t)e, (uint32_t)(e >> 32), d.site, 0u, d.seed, d.step) >= d.thresh;
+    return tr_philox_w0((uint32_t)e, (uint32_t)(e >> 32), d.site, d.step_hi, d.seed, d.step) >= d.thresh;
 }
 
 __host__ __device__ inline float tr_drop(const TrDrop& d, unsigned long long e, float x) {

@@ -84,7 +84,7 @@ struct rs_trainer {
     Buf P, G, M1, V1;       // parameters, gradients, Adam moments
     Buf act, grad, meta, small, ws;   // ws: split-K partials of tr_sgemm
     long long step = 0;
-    uint32_t drop_step = 0;         // dropout-step counter (key of the next dropout-active step)
+    uint64_t drop_step = 0;         // dropout-step counter (key of the next dropout-active step)
     std::vector<int> h_tok, h_meta;
 };
 
@@ -320,12 +320,14 @@ struct StepCtx {
     float *tpre = nullptr, *tx = nullptr, *th = nullptr, *logits = nullptr;
     float2* tst = nullptr;
     // dropout of this step (train mode: update >= 0 and p > 0)
-    uint32_t seed = 0, dstep = 0, th_hidden = 0, th_attn = 0;
+    uint32_t seed = 0, th_hidden = 0, th_attn = 0;
+    uint64_t dstep = 0;
     float sc_hidden = 1.f, sc_attn = 1.f;
     TrDrop drop(uint32_t site, bool attn) const {
         TrDrop d;
         d.seed = seed;
-        d.step = dstep;
+        d.step = (uint32_t)dstep;
+        d.step_hi = (uint32_t)(dstep >> 32);
         d.site = site;
         d.thresh = attn ? th_attn : th_hidden;
         d.scale = attn ? sc_attn : sc_hidden;
@@ -693,17 +695,18 @@ int rs_trainer_reset_optimizer(rs_trainer* t) {
 int64_t rs_trainer_dropout_step(const rs_trainer* t) { return t ? (int64_t)t->drop_step : -1; }
 
 int rs_trainer_set_dropout_step(rs_trainer* t, int64_t step) {
-    if (!t || step < 0 || step > 0xFFFFFFFFll) return rs_fail(RS_EARG, "bad argument");
-    t->drop_step = (uint32_t)step;
+    if (!t || step < 0) return rs_fail(RS_EARG, "bad argument");
+    t->drop_step = (uint64_t)step;
     return RS_OK;
 }
 
-int rs_dropout_keep(uint32_t seed, uint32_t step, uint32_t site, float p, int64_t n, uint8_t* d_keep, void* stream) {
+int rs_dropout_keep(uint32_t seed, uint64_t step, uint32_t site, float p, int64_t n, uint8_t* d_keep, void* stream) {
     if (n < 0 || (n > 0 && !d_keep)) return rs_fail(RS_EARG, "null argument");
     if (!(p >= 0.f && p < 1.f)) return rs_fail(RS_EARG, "p must be in [0, 1)");
     TrDrop d;
     d.seed = seed;
-    d.step = step;
+    d.step = (uint32_t)step;
+    d.step_hi = (uint32_t)(step >> 32);
     d.site = site;
     d.thresh = drop_thresh(p);
     TRY_HIP(tr_dropout_keep(d_keep, (long long)n, d, (hipStream_t)stream));

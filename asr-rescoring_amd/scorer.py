@@ -82,6 +82,17 @@ class BertEngine:
         except Exception:
             pass
 
+    # ---- deferred range / timeout check (rs_model_set_sync_check, rs_check) -------------
+    def set_sync_check(self, on: bool = True):
+        """False: scoring calls stay asynchronous on the current stream and their non-finite /
+        statistics-timeout flags accumulate until ``check()``; True (default): every call
+        synchronises and raises on its own flags."""
+        _lib.check(self.lib.rs_model_set_sync_check(self.handle, int(on)))
+
+    def check(self):
+        """Synchronise the current stream and raise if any deferred call flagged an error."""
+        _lib.check(self.lib.rs_check(self.handle, _lib.stream_ptr(self.device)))
+
     # ---- profiling (HIP events per kernel kind) ----------------------------------------
     def profile(self, on: bool = True):
         _lib.check(self.lib.rs_profile_enable(self.handle, int(on)))

@@ -59,16 +59,23 @@ def gather_scores(local: torch.Tensor, counts: Sequence[int], group=None) -> tor
     return torch.cat([out[r, :, :counts[r]] for r in range(world)], dim=1)
 
 
-def init_from_env(device_index: int | None = None):
+def init_from_env(device_index: int | None = None, force: bool = False):
     """torchrun / torch.distributed.run launch: (rank, world, local_rank).  Initialises the
-    default process group once (backend "nccl" = RCCL when a GPU is visible, else "gloo")."""
+    default process group once (backend "nccl" = RCCL when a GPU is visible, else "gloo") when
+    WORLD_SIZE > 1, or at any world size with ``force`` (a one-rank group: the exchange code
+    path runs unchanged on one GPU; MASTER_ADDR / MASTER_PORT default to 127.0.0.1:29512)."""
     import os
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0")) if device_index is None else device_index
     # RS_DIST_BACKEND=gloo: CPU exchange (e.g. several ranks sharing one GPU in a test)
     backend = os.environ.get("RS_DIST_BACKEND", "nccl" if torch.cuda.is_available() else "gloo")
-    if world > 1 and not dist.is_initialized():
+    if force and world == 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29512")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
+    if (world > 1 or force) and not dist.is_initialized():
         if backend == "nccl":
             torch.cuda.set_device(local)
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -102,18 +109,19 @@ def score_sharded(nb: NBest, score_fn, mode: str = "pll", device=None, group=Non
     scorer in the product; any callable in tests).  Returns the (am, lm) float64 block
     [2, H] of EVERY hypothesis, in global order, on every rank.  A rank may own no
     utterance (fewer utterances than ranks, or a few costly ones taking the prefix sum)."""
-    world = dist.get_world_size(group) if dist.is_initialized() else 1
-    rank = dist.get_rank(group) if dist.is_initialized() else 0
+    distributed = dist.is_initialized()
+    world = dist.get_world_size(group) if distributed else 1
+    rank = dist.get_rank(group) if distributed else 0
     parts = plan_shards(utterance_costs(nb, mode), world)
     u0, u1 = parts[rank]
     sub = nb.slice_utts(u0, u1)
     h0, h1 = int(nb.utt_off[u0]), int(nb.utt_off[u1])
     lm = score_fn(sub) if h1 > h0 else torch.zeros(0, dtype=torch.float64)
     lm = torch.as_tensor(lm).to(torch.float64)
-    dev = exchange_device(dist.get_backend(group) if world > 1 else None, lm.device, device)
+    dev = exchange_device(dist.get_backend(group) if distributed else None, lm.device, device)
     am = torch.from_numpy(np.ascontiguousarray(nb.am[h0:h1], np.float64)).to(dev)
     local = torch.stack([am, lm.to(dev)])
-    if world == 1:
+    if not distributed:            # with a process group (also of one rank) the exchange runs
         return local
     counts = [int(nb.utt_off[b] - nb.utt_off[a]) for a, b in parts]
     if max(counts) == 0:

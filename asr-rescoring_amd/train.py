@@ -297,6 +297,44 @@ def dropout_keep(seed: int, step: int, site: int, p: float, n: int, device=0) ->
     lib = _lib.load()
     dev = torch.device("cuda", device if isinstance(device, int) else torch.device(device).index)
     out = torch.empty(max(int(n), 1), dtype=torch.uint8, device=dev)
-    _lib.check(lib.rs_dropout_keep(int(seed) & 0xFFFFFFFF, int(step) & 0xFFFFFFFF, int(site), float(p), int(n),
+    _lib.check(lib.rs_dropout_keep(int(seed) & 0xFFFFFFFF, int(step) & 0xFFFFFFFFFFFFFFFF, int(site), float(p), int(n),
                                    _lib.ptr(out), _lib.stream_ptr(dev)))
     return out[:int(n)].cpu().numpy()
+
+
+def finetune_mlm_on_texts(weights: Dict[str, np.ndarray], sentences: Sequence[Sequence[int]],
+                          shape: BertShape = BERT_BASE, steps: int = 300, batch_size: int = 64,
+                          lr: float = 1e-4, seed: int = 0, device=0, dropout: float = 0.0,
+                          log_every: int = 0) -> Tuple[Dict[str, np.ndarray], List[float]]:
+    """MLM fine-tuning on in-domain text, then scoring with the result: the reference's
+    pipeline (MLM_PLL/main.py:117-161 mlm_finetune_bert -> :184-186 scoring with that checkpoint ->
+    rescore.py:25-45 fusion).  ``sentences`` are word-id lists (no [CLS]/[SEP]); their do_job rows
+    (MLM_PLL/preprocess.py:9-30) are visited in a seeded permutation per epoch, ``batch_size``
+    padded rows per step (collate, MLM_PLL/main.py:28-54), for ``steps`` AdamW steps.
+    Deterministic (native trainer, bitwise reproducible; dropout off by default).  Returns the
+    HF-keyed state dict (loadable by the scorers) and the per-step losses."""
+    seqs, labels = [], []
+    for s in sentences:
+        h = [shape.cls_id] + [int(x) for x in s] + [shape.sep_id]
+        for p in range(1, len(h) - 1):
+            row = list(h)
+            row[p] = shape.mask_id
+            seqs.append(row)
+            labels.append(h)
+    tr = MLMTrainer(weights, shape, device=device, lr=lr, hidden_dropout=dropout, attn_dropout=dropout,
+                    dropout_seed=seed)
+    try:
+        rng = np.random.Generator(np.random.PCG64(seed))
+        order = np.empty(0, np.int64)
+        losses: List[float] = []
+        for it in range(steps):
+            if len(order) < batch_size:
+                order = np.concatenate([order, rng.permutation(len(seqs))])
+            sel, order = order[:batch_size], order[batch_size:]
+            ids, off, lab, klen = pad_rows([seqs[i] for i in sel], [labels[i] for i in sel])
+            losses.append(tr.step(ids, off, lab, klen))
+            if log_every and (it + 1) % log_every == 0:
+                print(f"finetune step {it + 1}/{steps} loss {losses[-1]:.4f}", flush=True)
+        return tr.state_dict(), losses
+    finally:
+        tr.close()

@@ -76,6 +76,12 @@ def main():
                          "in fp32); fp16: fp16 operands (reduced precision, reported as a secondary field)")
     ap.add_argument("--fp16-steps", type=int, default=2,
                     help="secondary leg: steps of the reduced-precision fp16 mode (0 = skip)")
+    ap.add_argument("--force-gather", action="store_true",
+                    help="at one rank too: a one-rank nccl (RCCL) group and the all_gather inside every step")
+    ap.add_argument("--finetune-steps", type=int, default=300,
+                    help="MLM fine-tuning steps on the synthetic set's reference sentences before scoring "
+                         "(the reference's mlm_finetune_bert -> scoring -> fusion pipeline; 0 = random-init LM)")
+    ap.add_argument("--finetune-lr", type=float, default=1e-4)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -83,12 +89,13 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+    from asr_rescoring_amd import shard
+    if world > 1 or args.force_gather:
+        shard.init_from_env(local, force=args.force_gather)
+    gather = dist.is_initialized()
 
     from asr_rescoring_amd.scorer import PLLScorer
     weights = make_weights(BERT_BASE, seed=1234)
-    scorer = PLLScorer(weights, BERT_BASE, device=local, max_rows=args.max_rows, precision=args.precision)
     kx = 3 if args.precision == "fp16x3" else 1
 
     # ONE global synthetic set of utts x world utterances, split by the product's sharding
@@ -96,10 +103,26 @@ def main():
     # contiguous utterance range, the (am, lm) blocks meet in one all-gather (RCCL), rank 0
     # runs the 101-weight fusion sweep over the whole set.  The global set grows with the
     # rank count (weak scaling: per-rank work ~ utts utterances).
-    from asr_rescoring_amd import shard
     # hard: hypotheses permuted and AM scores unsorted, so the fused argmax moves with the weight
     # and the rerank check below is not the trivial AM-only case (same token counts)
     nb_all = D.synthetic_nbest(args.utts * world, args.nbest, seed=1, hard=True)
+
+    # The reference's pipeline: fine-tune BertForMaskedLM on in-domain text (MLM_PLL/main.py:117-161),
+    # score with that checkpoint (:184-186), fuse (rescore.py:25-45).  Here the in-domain text is the
+    # synthetic set's reference sentences, so the LM learns to prefer the correct hypotheses and the
+    # fused argmax depends on the LM.  Native trainer, deterministic; outside the timed region.
+    ft = None
+    if args.finetune_steps > 0:
+        from asr_rescoring_amd.train import finetune_mlm_on_texts
+        t_ft = time.perf_counter()
+        weights, losses = finetune_mlm_on_texts(weights, nb_all.refs, BERT_BASE, steps=args.finetune_steps,
+                                                lr=args.finetune_lr, seed=0, device=local)
+        torch.cuda.synchronize()
+        ft = {"steps": args.finetune_steps, "lr": args.finetune_lr, "batch_rows": 64,
+              "first_loss": round(losses[0], 4), "final_loss": round(losses[-1], 4),
+              "seconds": round(time.perf_counter() - t_ft, 2),
+              "text": "the synthetic set's reference sentences (do_job rows, dropout off)"}
+    scorer = PLLScorer(weights, BERT_BASE, device=local, max_rows=args.max_rows, precision=args.precision)
     parts = shard.plan_shards(shard.utterance_costs(nb_all), world)
     u0, u1 = parts[rank]
     nb = nb_all.slice_utts(u0, u1)
@@ -116,7 +139,7 @@ def main():
     def step():
         lm = scorer.score_nbest(d_tok, nb.hyp_off)               # float64 [H_local]
         pair = torch.stack([am_d, lm])                           # (am, lm) [2, H_local]
-        out = shard.gather_scores(pair, counts) if world > 1 else pair
+        out = shard.gather_scores(pair, counts) if gather else pair
         if rank == 0:
             rerank.fuse_rerank(out[0], out[1], hyp_len_all, nb_all.utt_off, grid, "norm", args.nbest, local)
         return out[1]
@@ -125,19 +148,19 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
+    if gather:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         lm = step()
     torch.cuda.synchronize()
-    if world > 1:
+    if gather:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     t = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
+    if gather:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
     total_fwd = n_fwd_all * args.steps
@@ -227,14 +250,15 @@ def main():
         threads = set_cpu_threads()
         model = TorchBert(weights, BERT_BASE)
         lm_np = lm.double().cpu().numpy()
-        # whole utterances, cheapest (fewest masked forwards) first, until the time budget: the
-        # sample then covers several utterances for the rerank check below (short hypotheses
-        # cost the CPU less per forward, so this errs towards a faster CPU baseline)
+        # whole utterances nearest the step's median utterance cost (sum_h L_h (L_h + 2), the cost
+        # the sharding plan balances) first, until the time budget: a sample at the step's length
+        # distribution (its mean T is reported next to config.mean_T), covering several
+        # utterances for the rerank check below
         Nb = args.nbest
         T_h = np.diff(nb.hyp_off)
-        cost_u = np.add.reduceat(T_h - 2, nb.utt_off[:-1])
+        cost_u = shard.utterance_costs(nb).astype(np.float64)
         rows_done, t_cpu, rel, done_u, ref_lm = 0, 0.0, [], [], {}
-        for u in np.argsort(cost_u, kind="stable"):
+        for u in np.argsort(np.abs(cost_u - np.median(cost_u)), kind="stable"):
             if t_cpu >= args.cpu_seconds:
                 break
             for hh in range(nb.utt_off[u], nb.utt_off[u + 1]):
@@ -261,11 +285,17 @@ def main():
             _, _, arg_ref = RR.find_best_weight(am_s, np.asarray([ref_lm[i] for i in idx]).reshape(uw, Nb), hyps_s, refs_s, Nb)
             _, _, arg_hip = RR.find_best_weight(am_s, lm_np[idx].reshape(uw, Nb), hyps_s, refs_s, Nb)
             rerank_same = bool(np.array_equal(arg_ref, arg_hip))
+        hs = np.asarray(sorted(ref_lm), np.int64)
+        Ls = T_h[hs] - 2
+        mean_T_sample = float(np.average(T_h[hs], weights=Ls)) if len(hs) else None
         cpu = {"value": round(rows_done / t_cpu, 2), "unit": "masked fwd/s", "cores": threads,
                "cpu_model": _cpu_model(), "kind": "port",
-               "sample": f"{uw} whole utterances, {h} hypotheses ({rows_done} masked forwards; the "
-               f"cheapest utterances of rank-0 step input), reference work pattern (batch 32 padded rows, all-position logits + CE, "
+               "sample": f"{uw} whole utterances, {h} hypotheses ({rows_done} masked forwards, mean T "
+               f"{mean_T_sample:.2f} per forward; the utterances nearest the median utterance cost of the "
+               f"rank-0 step input), reference work pattern (batch 32 padded rows, all-position logits + CE, "
                f"fp64 accumulation), torch {torch.__version__} CPU",
+               "sample_mean_T": round(mean_T_sample, 2) if mean_T_sample else None,
+               "seconds": round(t_cpu, 2),
                "pll_max_rel_err_vs_gpu": float(max(rel)) if rel else None,
                "rerank_argmax_equal_cpu_reference_lm": rerank_same, "rerank_check_utterances": uw}
 
@@ -296,14 +326,16 @@ def main():
                "config": {"workload": "C3 MLM_PLL full PLL", "model": "bert-base-chinese shape (12L/768/12H/3072/V21128)",
                           "utts_per_rank": args.utts, "n_best": args.nbest, "utts_total": nb_all.n_utt,
                           "forwards_per_step": n_fwd_all, "forwards_rank0_step": n_fwd,
-                          "mean_T": round(mean_T, 2), "parallelism": f"dp{world} (cost-balanced utterance shards of one global set + one RCCL all_gather)"},
+                          "mean_T": round(mean_T, 2),
+                          "parallelism": f"dp{world} (cost-balanced utterance shards of one global set + one RCCL all_gather"
+                                         + (" in every step" if gather else "; none at one rank") + ")"},
                "achieved_tflops_canonical": round(flops_step * args.steps / dt / 1e12, 2),
-               "roofline": roof, "cpu_baseline": cpu, "rerank": rr, "fp16_secondary": fp16,
+               "roofline": roof, "cpu_baseline": cpu, "rerank": rr, "lm_finetune": ft, "fp16_secondary": fp16,
                "kinds_ms": {k: round(v[0], 3) for k, v in kinds.items()}}
         print(json.dumps(rec))
     scorer.close()
     del lm
-    if world > 1:
+    if gather:
         dist.destroy_process_group()
 
 

@@ -102,8 +102,18 @@ int rs_model_reserve(rs_model* m, int64_t max_rows);
  * for non-finite values (an operand image that overflowed fp16 turns every dependent score
  * into inf / NaN), synchronises `stream` and returns RS_EUNSUP with a message instead of
  * handing back non-finite scores.  These calls therefore return with their work complete.
+ * The same report carries RS_EHIP when a fused residual-LayerNorm GEMM timed out waiting for
+ * its row statistics (each call reports only its own).
  *
- * MLM_PLL scoring (MLM_PLL/preprocess.py:9-30 + MLM_PLL/main.py:83-107):
+ * rs_model_set_sync_check(m, 0) defers that report: the calls only enqueue the check (they stay
+ * asynchronous on `stream`), the flags accumulate on the device, and rs_check(m, stream)
+ * synchronises `stream`, reports (RS_EUNSUP / RS_EHIP) and clears them.  on = 1 restores the
+ * default; call rs_check first so nothing pending is dropped.  No reference counterpart (the
+ * reference's forward is synchronous PyTorch-CPU, MLM_PLL/main.py:83-107). */
+int rs_model_set_sync_check(rs_model* m, int on);
+int rs_check(rs_model* m, void* stream);
+
+/* MLM_PLL scoring (MLM_PLL/preprocess.py:9-30 + MLM_PLL/main.py:83-107):
  *   d_tok      int32 [h_hyp_off[n_hyp]]  hypotheses as [CLS] w_1..w_L [SEP]
  *   h_hyp_off  int32 [n_hyp + 1]         host offsets into d_tok (T_h = L_h + 2 >= 3)
  *   d_pll      float64 [n_hyp]           sum_p log p(w_p | w_{\p}) accumulated in row
@@ -267,14 +277,16 @@ int rs_train_step_mlm(rs_trainer* t, const int32_t* d_ids, const int32_t* h_seq_
                       float* d_loss, void* stream);
 /* The dropout-step counter: the key the next dropout-active step uses (then incremented). */
 int64_t rs_trainer_dropout_step(const rs_trainer* t);
-/* Sets it (0 .. 2^32-1): part of the resume state — the CLI keys each epoch's first step by
- * the epoch number, so a run resumed at epoch k draws the masks of the straight run. */
+/* Sets it (0 .. 2^63-1; a 64-bit counter whose high word is a Philox counter word and low word
+ * the second key word): part of the resume state — the CLI starts epoch k at k << 32, so every
+ * epoch has 2^32 dropout steps of its own and a run resumed at epoch k draws the masks of the
+ * straight run. */
 int rs_trainer_set_dropout_step(rs_trainer* t, int64_t step);
 /* d_keep uint8 [n]: the keep bit the trainer's kernels use for element e of dropout site
  * `site` (0 = embeddings; layer l: 1 + 3l attention probabilities in the saved-P layout,
  * 2 + 3l self-output, 3 + 3l output, element = row * hidden + column) in dropout step `step`
  * with probability p.  Test / export entry (masks fed to the CPU oracle). */
-int rs_dropout_keep(uint32_t seed, uint32_t step, uint32_t site, float p, int64_t n, uint8_t* d_keep, void* stream);
+int rs_dropout_keep(uint32_t seed, uint64_t step, uint32_t site, float p, int64_t n, uint8_t* d_keep, void* stream);
 /* Synchronous copies of one parameter / its last gradient (numel must match). */
 int rs_trainer_get_tensor(rs_trainer* t, const char* hf_key, void* host_out, int64_t numel);
 int rs_trainer_get_grad(rs_trainer* t, const char* hf_key, void* host_out, int64_t numel);

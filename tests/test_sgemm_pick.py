@@ -1,7 +1,8 @@
 """Trainer GEMM picker (k_sgemm.hip sg_pick / sg_model), host only: the tile configuration and
-split-K count chosen for the bert-base training shapes are the measured-best ones
-(profiles/r3u_sgemm_pick.txt), the choice depends on the shape alone (bitwise-reproducible
-training), and the workspace the trainer allocates covers every split the picker can choose."""
+split-K count chosen for the bert-base training shapes on MI355X's 256 CUs are the measured-best
+ones (profiles/r3u_sgemm_pick.txt), and the choice is a function of the shape and the CU count
+(bitwise-reproducible training on a given device model).  The CU count is passed explicitly, so
+these tests make no GPU call."""
 import ctypes
 
 import pytest
@@ -14,8 +15,8 @@ def pick():
     lib = _lib.load()
     fn = lib.rs_debug_sgemm_pick
     fn.restype = ctypes.c_int
-    fn.argtypes = [ctypes.c_int] * 4
-    return lambda M, N, K, mcmc=0: divmod(fn(M, N, K, mcmc), 100)
+    fn.argtypes = [ctypes.c_int] * 5
+    return lambda M, N, K, mcmc=0, cus=256: divmod(fn(M, N, K, mcmc, cus), 100)
 
 
 def test_192x128_where_the_128x128_grid_leaves_a_half_round(pick):
@@ -32,7 +33,12 @@ def test_small_batches_split_k(pick):
     assert sp > 1
 
 
-def test_choice_is_a_function_of_the_shape(pick):
-    a = [pick(m, n, k, f) for m, n, k, f in [(1100, 2304, 768, 0), (2304, 768, 1100, 1), (5300, 768, 3072, 0)]]
-    b = [pick(m, n, k, f) for m, n, k, f in [(1100, 2304, 768, 0), (2304, 768, 1100, 1), (5300, 768, 3072, 0)]]
+def test_choice_is_a_function_of_shape_and_cus(pick):
+    shapes = [(1100, 2304, 768, 0), (2304, 768, 1100, 1), (5300, 768, 3072, 0)]
+    a = [pick(m, n, k, f) for m, n, k, f in shapes]
+    b = [pick(m, n, k, f) for m, n, k, f in shapes]
     assert a == b
+    # a device with fewer CUs rounds differently: 756 tiles of 128x128 on 128 CUs x 2 = 2.95
+    # rounds, against 1.48 on 256 CUs where the 192x128 tile's single round wins
+    assert pick(5300, 2304, 768, 0, 256) == (9, 1)
+    assert pick(5300, 2304, 768, 0, 0) == (-1, 99)        # rejected
