@@ -1,0 +1,68 @@
+// Device helpers shared by the GEMM kernels (k_gemm.hip, k_gemm_pp.hip).
+#pragma once
+#include "common.h"
+
+namespace {
+
+// Packed GELU for the epilogues: two values per v_pk_* instruction, one transcendental per
+// value.  GELU(x) = relu(x) - |x|/2 * erfc(|x|/sqrt2), erfc(z) = 2^P(z) with z clamped to
+// 5.7 (erfc(5.7) < 2e-15) and P the degree-6 fit of log2(erfc) from tools/fit_gelu.py:
+// |GELU error| <= 2.7e-7 over all x in fp32 (the previous A&S 7.1.26 form: 4.7e-7, with a
+// reciprocal and an exponential per value — 15 % of the FFN1 GEMM's time).
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f32x2 gelu2(f32x2 x) {
+    const f32x2 ax = __builtin_elementwise_abs(x);
+    const f32x2 z = __builtin_elementwise_min(ax * 0.70710678118654752f, (f32x2)(5.7f));
+    f32x2 q = __builtin_elementwise_fma(z, (f32x2)(2.758793125e-04f), (f32x2)(-4.419489298e-03f));
+    q = __builtin_elementwise_fma(q, z, (f32x2)(3.247941285e-02f));
+    q = __builtin_elementwise_fma(q, z, (f32x2)(-1.512418836e-01f));
+    q = __builtin_elementwise_fma(q, z, (f32x2)(-9.174530506e-01f));
+    q = __builtin_elementwise_fma(q, z, (f32x2)(-1.628065586e+00f));
+    q = __builtin_elementwise_fma(q, z, (f32x2)(8.448299013e-06f));
+    const f32x2 e = {__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
+    const f32x2 r = __builtin_elementwise_max(x, (f32x2)(0.f));
+    return __builtin_elementwise_fma(-(ax * 0.5f), e, r);
+}
+
+// 16-byte epilogue store; VAR&64: non-temporal (streamed past L2, keeps the A panels there)
+template <int VAR>
+__device__ __forceinline__ void st16(uint4* p, uint4 v) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    if constexpr (VAR & 64) __builtin_nontemporal_store((u32x4){v.x, v.y, v.z, v.w}, (u32x4*)p);
+    else *p = v;
+}
+
+// Chunk swizzle of the split-operand kernel's 64-B LDS rows for 16x16x32 fragment reads: lane
+// l reads row r = l & 15 of a 16-aligned block at chunk l >> 4, the ds_read_b128 lane groups
+// are {0-3,12-15,20-27}, {4-11,16-19,28-31} and the same + 32; the bank quad of (r, chunk c)
+// is 4 (r & 3) + (c ^ g16(r >> 2)), and g16 = [0, 2, 3, 1] makes each group's 16 quads
+// distinct (the 32x32 swizzle c ^ ((r >> 2) & 3) collides rows 0-3 with rows 4-7 there).
+__device__ __forceinline__ int g16(int rb) { return (0x78 >> (2 * (rb & 3))) & 3; }
+
+// Four 16-B reads of rows rr0 + 8 it (it = 0..3), chunk c16 of a 32 x 128-B epilogue slab whose
+// chunks are XOR-swizzled by (row & 7), as inline asm: the compiler treats every LDS read after an
+// LDS-DMA issue as a possible alias of the DMA and waits vmcnt(0) first, which would hold each
+// epilogue back until the next tile's stage 0 has landed.  The slab is written by this wave's
+// own ds_writes just before (LDS ops of a wave execute in order); one lgkmcnt(0) covers the four.
+__device__ __forceinline__ void slab_read4(const char* slb, int rr0, int c16, uint4 (&v)[4]) {
+    const uint32_t base = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)slb;
+    uint32_t a[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+        const int rr = it * 8 + rr0;
+        a[it] = base + rr * 128 + ((c16 ^ (rr & 7)) << 4);
+    }
+    uint4 v0, v1, v2, v3;
+    asm volatile(
+        "ds_read_b128 %0, %4\n\t"
+        "ds_read_b128 %1, %5\n\t"
+        "ds_read_b128 %2, %6\n\t"
+        "ds_read_b128 %3, %7\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3)
+        : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3])
+        : "memory");
+    v[0] = v0; v[1] = v1; v[2] = v2; v[3] = v3;
+}
+
+}  // namespace

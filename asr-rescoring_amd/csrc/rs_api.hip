@@ -373,6 +373,13 @@ bool x3s_imgres_on() {
 // RS_LNFUSE (image-held residual; default 1): the residual add + LayerNorm of both blocks run in
 // the O-projection / BertOutput GEMM epilogues (EPI_LNRES_IMG: full rows through an in-launch
 // exchange of row statistics) instead of as ln_res_img passes (RS_LNFUSE=0).  Read per call.
+// RS_PP (split-operand layers; read per call): 1 = the QKV and BertIntermediate projections on
+// the ping-pong kernel (k_gemm_pp.hip: the epilogue of one half of the workgroup overlapped by
+// the other half's K loop), 0 = gemm_x3s_kernel.  Bitwise equal results.
+bool pp_on() {
+    const char* e = getenv("RS_PP");
+    return e && !strcmp(e, "1");
+}
 bool lnfuse_on(const rs_bert_cfg& cf) {
     const char* e = getenv("RS_LNFUSE");
     return !(e && !strcmp(e, "0")) && cf.hidden % 256 == 0 && cf.hidden <= 1024;
@@ -418,7 +425,11 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
         const int al = gemm_row_align();
         e.m_valid = m_valid;
         ProfScope ps(m, st, kind, 2.0 * m_valid * (double)n_flop_cols * 3.0 * K);
-        HIPTRY(launch_gemm_x3s(epi, A, W, ldw, (m_valid + al - 1) / al * al, N, K, e, st));
+        const int M_pad = (m_valid + al - 1) / al * al;
+        if ((epi == EPI_BIAS_F32 || epi == EPI_GELU_F16) && K % 64 == 0 && pp_on())
+            HIPTRY(launch_gemm_pp(epi, A, W, ldw, M_pad, N, K, e, st));
+        else
+            HIPTRY(launch_gemm_x3s(epi, A, W, ldw, M_pad, N, K, e, st));
         return RS_OK;
     };
     auto gelu_ep = [&](const float* bias, f16* out) {

@@ -102,3 +102,28 @@ def test_x3s_vs_torch_fp32(gemm, name, N, K, gelu, dbg, M):
             gl = torch.nn.functional.gelu(ref)
             err = (o[:, :N].float() + o[:, N:].float() / 64.0 - gl).abs().max() / gl.abs().max()
         assert err < 1e-5, (cfg, float(err))
+
+
+@pytest.mark.parametrize("M", [256, 768, 40960, 262144])
+@pytest.mark.parametrize("name,N,K,gelu", SHAPES)
+def test_pp_bitwise_equals_x3s(gemm, name, N, K, gelu, M):
+    """The ping-pong split-operand kernel (k_gemm_pp.hip: two phase-shifted 4-wave halves, 128 x 256
+    tiles, W fragments straight to registers) issues the same MFMAs in the same order per
+    accumulator as gemm_x3s_kernel (rs_debug_gemm dbg 60 vs 0): bitwise equal fp32 outputs and
+    GELU images.  M = 256 / 768: fewer tiles than workgroup halves (halves with no tile, a
+    half 1 with fewer tiles than half 0); 262144: the bench chunk, many tiles per half."""
+    g = torch.Generator(device="cuda").manual_seed(5)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    W = torch.randn(N, K, device="cuda", generator=g) * 0.05
+    b = torch.randn(N, device="cuda", generator=g) * 0.1
+    A2, W2 = _split2(A), _split2(W)
+    lib = _lib.load()
+    st = torch.cuda.current_stream().cuda_stream
+    for cfg, mk in ((32, lambda: torch.full((M, N), float("nan"), device="cuda")),
+                    (31, lambda: torch.full((M, 2 * N), float("nan"), device="cuda", dtype=torch.float16))):
+        o0, o1 = mk(), mk()
+        assert lib.rs_debug_gemm(cfg, 0, A2.data_ptr(), W2.data_ptr(), b.data_ptr(), o0.data_ptr(), M, N, K, st) == 0
+        assert lib.rs_debug_gemm(cfg, 60, A2.data_ptr(), W2.data_ptr(), b.data_ptr(), o1.data_ptr(), M, N, K, st) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(o0.view(torch.int32) if cfg == 32 else o0.view(torch.int16),
+                           o1.view(torch.int32) if cfg == 32 else o1.view(torch.int16)), (name, cfg, M)

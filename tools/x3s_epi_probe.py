@@ -39,8 +39,15 @@ def main():
         out32 = torch.empty(M, N, device=dev)
         img = torch.empty(M, 2 * N, device=dev, dtype=torch.float16)
         fl = 3 * 2.0 * M * N * K
-        var = {"f32": (32, out32, {"prod": 0, "nowait": 50, "alias": 51, "nw+al": 53, "noepi": 20}),
-               "gelu2": (31, img, {"prod": 0, "nowait": 50, "alias": 51, "nw+al": 53, "noepi": 52})}
+        var = {"f32": (32, out32, {"prod": 0, "pp": 60, "nowait": 50, "alias": 51, "nw+al": 53, "noepi": 20}),
+               "gelu2": (31, img, {"prod": 0, "pp": 60, "nowait": 50, "alias": 51, "nw+al": 53, "noepi": 52})}
+        # the ping-pong kernel is bitwise equal to the production kernel (same MFMA order)
+        for cfg, o in ((32, out32), (31, img)):
+            o2 = torch.empty_like(o)
+            assert fn(cfg, 0, A2.data_ptr(), W2.data_ptr(), b.data_ptr(), o.data_ptr(), M, N, K, st) == 0
+            assert fn(cfg, 60, A2.data_ptr(), W2.data_ptr(), b.data_ptr(), o2.data_ptr(), M, N, K, st) == 0
+            torch.cuda.synchronize()
+            print(f"pp == prod (cfg {cfg}, N={N}, K={K}): {torch.equal(o, o2)}", flush=True)
         times = {}
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for _ in range(rounds):
