@@ -54,13 +54,10 @@ __device__ __forceinline__ typename AccT<MS>::type mfma_f16(half8 a, half8 b, ty
 template <int MS>
 __device__ __forceinline__ int qcol(int g, int lane) { return MS == 32 ? 8 * g + 4 * (lane >> 5) : 4 * (lane >> 4); }
 
-// VAR = variant bits.  Production: 128 (K loop software-pipelined by sched_group_barrier)
-// and 64 (non-temporal epilogue stores).  Alternatives kept for timing: 256 (front-loaded
-// read schedule), 32 (direct permlane epilogue, no LDS pass).  Timing experiments only
-// (rs_debug_gemm): bit0 = no K-loop staging (MFMA + LDS reads on stale tiles), bit1 = no
-// epilogue (accumulators kept alive, nothing stored), bit2 = staging interleaved with the
-// MFMAs, bit3 = stores aliased onto rows 0..255 (L2-resident), bit4 = no global stores,
-// bit9 = K-loop DMA never waited for (isolates its latency from its bandwidth cost).
+// VAR bits: 128 (K loop software-pipelined by sched_group_barrier), 64 (non-temporal epilogue
+// stores), 8192 (v_mfma_f32_16x16x32_f16).  (The measured-slower alternatives of rounds 1-3 —
+// front-loaded reads, the direct permlane epilogue, the ping-pong wave rows, the two-buffer
+// cross-step pipeline — are recorded in profiles/r1_*; their code was removed in round 4.)
 template <int BM, int BN, int WM, int WN, int NSTAGE, int BK, int EPI, int VAR = 0>
 __global__ void __launch_bounds__(WM * WN * 64)
 gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int n_tiles_n,
@@ -73,8 +70,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     constexpr int KPS = 512 / MS, CPS = KPS / 8, NQ = MS * MS / 256;
     typedef typename AccT<MS>::type accT;
     constexpr int TM = WTM / MS, TN = WTN / MS;
-    static_assert(MS == 32 || (!(VAR & (4 | 32 | 256 | 1024 | 2048)) && EPI != EPI_LSE && BK / KPS >= 2),
-                  "16x16x32 MFMA: default K loop and the LDS epilogue only");
+    static_assert(MS == 32 || (EPI != EPI_LSE && BK / KPS >= 2), "16x16x32 MFMA: not the logsumexp epilogue");
     constexpr int RB = BK * 2;            // LDS row bytes
     constexpr int CPR = BK / 8;           // 16-byte chunks per row
     constexpr int RPP = 1024 / RB;        // rows per 1 KiB LDS-DMA piece
@@ -105,10 +101,6 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
-    if constexpr ((VAR & 262144) != 0) {      // younger wave half at s_setprio 1 (as the persistent kernel)
-        if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
-    }
-
     // per-lane global source pointers of the pieces this wave stages (k0 = 0)
     const f16* src[PPW];
     int ldsoff[PPW];
@@ -200,167 +192,22 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         if (s < nk) stage(s, s * BK);
 
     const int frow = lane % MS, fh = lane / MS;
-    if constexpr (NSTAGE == 2 && WM == 2 && BK == 64 && (VAR & 2048)) {
-        // Ping-pong: the two wave rows (grp = wm; every SIMD holds one wave of each) run one
-        // barrier apart, so while one issues its MFMA cluster the other reads its next
-        // fragments / issues DMA, and the MFMA pipe never waits on LDS latency.
-        // Phase p = one k16 substep (K-step u = p/4, s = p%4):
-        //   load segment:  6 ds_read_b128 of substep s (+ DMA issue / wait, below); s_barrier
-        //   MFMA segment:  lgkmcnt(0); 8 MFMAs;                                   s_barrier
-        // Group 1 starts with one extra barrier (pairs with group 0's first load barrier) and
-        // group 0 ends with one.  Barrier B_j (B_0 = prologue): group 0 load(p) = [B_2p,
-        // B_2p+1), MFMA(p) = [B_2p+1, B_2p+2); group 1 is one barrier later.  Buffer of step
-        // u-1 is free after B_8u+1 (group 1's last reads retire in its MFMA(4u-1)), so the
-        // DMA of step u+1 is issued in group 1's load(4u) / group 0's load(4u+1), and each
-        // wave waits vmcnt(0) in load(4u+3): every piece has landed before B_8u+8, where
-        // group 0 starts reading step u+1.
-        constexpr int NSUB = BK / 16;
-        static_assert(NSUB == 4, "ping-pong schedule assumes BK = 64");
-        const int grp = wm;
-        const int offA = (wm * WTM + frow) * RB + (swz<BK>(wm * WTM + frow, fh) << 4);
-        const int offB = A_BYTES + (wn * WTN + frow) * RB + (swz<BK>(wn * WTN + frow, fh) << 4);
-        half8 af[TM], bf[TN];
-        if (nk > 1 && !(VAR & 1)) stage(1, BK);
-        if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_barrier" ::: "memory");                                   // B_0
-        if (grp == 1) asm volatile("s_barrier" ::: "memory");
-        for (int u = 0; u < nk; ++u) {
-            const char* sbase = smem + (u & 1) * STAGE;
-#pragma unroll
-            for (int s = 0; s < NSUB; ++s) {
-                // ---- load segment
-                __builtin_amdgcn_sched_barrier(0);
-                const int xa = offA ^ (s << 5), xb = offB ^ (s << 5);
-#pragma unroll
-                for (int j = 0; j < TN; ++j) bf[j] = *(const half8*)(sbase + xb + j * 32 * RB);
-#pragma unroll
-                for (int i = 0; i < TM; ++i) af[i] = *(const half8*)(sbase + xa + i * 32 * RB);
-                if (s == 1 - grp && u >= 1 && u + 1 < nk && !(VAR & 1)) stage((u + 1) & 1, (u + 1) * BK);
-                if (s == 3 && !(VAR & 512)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);
-                asm volatile("s_barrier" ::: "memory");
-                // ---- MFMA segment
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_sched_barrier(0);
-                if constexpr (VAR & 4096) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-                for (int i = 0; i < TM; ++i)
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
-                if constexpr (VAR & 4096) __builtin_amdgcn_s_setprio(0);
-                __builtin_amdgcn_sched_barrier(0);
-                asm volatile("s_barrier" ::: "memory");
-            }
-        }
-        if (grp == 0) asm volatile("s_barrier" ::: "memory");
-    } else if constexpr (NSTAGE == 2 && (VAR & 1024)) {
-        // Two-buffer ring pipelined across K-steps.  One barrier per K-step, placed after
-        // this wave's reads of the step's last substep have landed and its own DMA pieces
-        // of the next step have arrived: past it, (a) every wave is done reading buffer
-        // `cur`, which is refilled with step kt+2, and (b) step kt+1 is complete, so its
-        // substep-0 fragments are read while the last substep's MFMAs issue.  Inside a
-        // step, substep s+1's reads interleave with substep s's MFMAs (MFMA first, so the
-        // compiler's lgkmcnt wait before it covers only the older reads).
-        constexpr int NSUB = BK / 16, NR = TM + TN, NM = TM * TN;
-        static_assert(NSUB % 2 == 0 && NM >= NR, "pipeline shape");
-        // Fragment addresses: swz(row, 2s + fh) = swz(row, fh) ^ 2s, and fragments 32 rows
-        // apart share the swizzle, so substep s is one XOR of bits 5-6 of a per-lane base and
-        // the fragment/buffer offsets are immediates (no per-substep address registers).
-        const int offA = (wm * WTM + frow) * RB + (swz<BK>(wm * WTM + frow, fh) << 4);
-        const int offB = A_BYTES + (wn * WTN + frow) * RB + (swz<BK>(wn * WTN + frow, fh) << 4);
-        auto load_frags = [&](const char* sbase, int s, half8 (&af)[TM], half8 (&bf)[TN]) {
-            const int xa = offA ^ (s << 5), xb = offB ^ (s << 5);
-#pragma unroll
-            for (int j = 0; j < TN; ++j) bf[j] = *(const half8*)(sbase + xb + j * 32 * RB);
-#pragma unroll
-            for (int i = 0; i < TM; ++i) af[i] = *(const half8*)(sbase + xa + i * 32 * RB);
-        };
-        auto mfmas = [&](const half8 (&af)[TM], const half8 (&bf)[TN]) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_f16(bf[j], af[i], acc[i][j], 0, 0, 0);
-        };
-        auto pattern = [&]() {
-#pragma unroll
-            for (int r = 0; r < NR; ++r) {
-                __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
-        };
-        half8 af0[TM], bf0[TN], af1[TM], bf1[TN];
-        if (nk > 1 && !(VAR & 1)) stage(1, BK);
-        if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        asm volatile("s_barrier" ::: "memory");
-        load_frags(smem, 0, af0, bf0);
-        for (int kt = 0; kt < nk; ++kt) {
-            const int cur = kt & 1;
-            const char* sbase = smem + cur * STAGE;
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int s = 0; s + 1 < NSUB; s += 2) {
-                load_frags(sbase, s + 1, af1, bf1);
-                mfmas(af0, bf0);
-                pattern();
-                __builtin_amdgcn_sched_barrier(0);
-                if (s + 2 < NSUB) {
-                    load_frags(sbase, s + 2, af0, bf0);
-                    mfmas(af1, bf1);
-                    pattern();
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            // last substep (fragments in af1/bf1)
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (kt + 1 < nk) {
-                if (!(VAR & 512)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                asm volatile("s_barrier" ::: "memory");
-                if (kt + 2 < nk && !(VAR & 1)) stage(cur, (kt + 2) * BK);
-                load_frags(smem + (cur ^ 1) * STAGE, 0, af0, bf0);
-            }
-            mfmas(af1, bf1);
-        }
-    } else {
     int buf = 0;
     for (int kt = 0; kt < nk; ++kt) {
         // tile kt landed for this wave: all later-issued stages may stay in flight
         {
             const int ahead = min(NSTAGE - 2, nk - 1 - kt);   // stages issued after tile kt
-            if (VAR & 512) {   // diagnostic: DMA issued but never waited for (latency cost)
-            } else if (NSTAGE >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
+            if (NSTAGE >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PPW) : "memory");
             else if (NSTAGE >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PPW) : "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
         // every wave's part of tile kt landed; every wave finished reading tile kt-1
         asm volatile("s_barrier" ::: "memory");
-        const bool do_stage = !(VAR & 1) && kt + NSTAGE - 1 < nk;
         int nb = buf + NSTAGE - 1;
         if (nb >= NSTAGE) nb -= NSTAGE;
-        const int knext = (kt + NSTAGE - 1) * BK;
-        if constexpr (!(VAR & 4)) {
-            if (do_stage) stage(nb, knext);
-        }
-        if constexpr (VAR & 384) __builtin_amdgcn_sched_barrier(0);
-        // VAR&4: the next stage's LDS-DMA pieces are spread over the MFMA clusters
+        if (kt + NSTAGE - 1 < nk) stage(nb, (kt + NSTAGE - 1) * BK);
+        if constexpr (VAR & 128) __builtin_amdgcn_sched_barrier(0);
         constexpr int NSUB = BK / KPS;         // k-substeps per stage
-        auto stage_part = [&](int q) {
-            if constexpr (VAR & 4) {
-                __builtin_amdgcn_sched_barrier(0);
-                if (do_stage) {
-#pragma unroll
-                    for (int p = (q * PPW) / NSUB; p < ((q + 1) * PPW) / NSUB; ++p)
-                        __builtin_amdgcn_global_load_lds(
-                            (const void*)(src[p] + knext),
-                            (__attribute__((address_space(3))) void*)(smem + nb * STAGE + ldsoff[p]), 16, 0, 0);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        };
         const char* sA = smem + buf * STAGE;
         const char* sB = sA + A_BYTES;
         // fragments of k-substep s+1 are read while the MFMAs of substep s issue
@@ -389,34 +236,14 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         load_frags(0, af0, bf0);
         load_frags(1, af1, bf1);
         mfmas(af0, bf0);
-        stage_part(0);
         if constexpr (NSUB == 4) {
             load_frags(2, af0, bf0);
             mfmas(af1, bf1);
-            stage_part(1);
             load_frags(3, af1, bf1);
             mfmas(af0, bf0);
-            stage_part(2);
         }
         mfmas(af1, bf1);
-        stage_part(NSUB - 1);
-        if constexpr ((VAR & 256) && !(VAR & 4)) {
-            // variant: substep s+1's reads front-loaded, two per MFMA, so the last one has
-            // NM - NR/2 MFMAs to land before the (conservative) lgkmcnt(0)
-            constexpr int NR = TM + TN, NM = TM * TN;
-            static_assert(NR % 2 == 0 && NM >= NR / 2, "two reads per MFMA slot");
-            __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
-#pragma unroll
-            for (int s = 0; s < NSUB - 1; ++s) {
-#pragma unroll
-                for (int r = 0; r < NR / 2; ++r) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-                }
-                __builtin_amdgcn_sched_group_barrier(0x008, NM - NR / 2, 0);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
-        } else if constexpr ((VAR & 128) && !(VAR & 4)) {
+        if constexpr ((VAR & 128) != 0) {
             // Software pipeline the scheduler will not find by itself (it serialises the
             // fragment reads and the MFMAs that consume them, exposing LDS latency per
             // substep): substep 0's reads, then substep s+1's reads one per MFMA of substep s.
@@ -435,19 +262,6 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
         }
         buf = buf + 1 == NSTAGE ? 0 : buf + 1;
-    }
-    }
-
-    if constexpr (VAR & 2) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-#if defined(__HIP_DEVICE_COMPILE__)
-                asm volatile("" ::"v"(acc[i][j]));
-#endif
-            }
-        return;
     }
     // ---------------- epilogue.  acc[i][j][4g + e] = C[row][col + e],
     //   row = m0 + wm*WTM + 32i + (lane&31),  col = n0 + wn*WTN + 32j + 8g + 4(lane>>5)
@@ -487,79 +301,6 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             if (fh == 0 && row < ep.m_valid)
                 ep.lse_part[(size_t)row * ep.n_parts + slab] = make_float2(mx, sm);
         }
-    } else if constexpr ((VAR & 32) != 0) {
-        // Straight from the accumulators.  fp16 outputs: lane l holds cols 8g..8g+3 and lane
-        // l+32 cols 8g+4..8g+7 of the same row; one v_permlane32_swap per dword pair (g, g+1)
-        // gives lanes 0-31 cols 8g..8g+7 and lanes 32-63 cols 8g+8..8g+15 -> 16-B stores.
-        // fp32 outputs: the lane's 4 columns are already one 16-B store.
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            const int row = rbase + i * 32;
-            const bool ok = row < ep.m_valid;
-#pragma unroll
-            for (int j = 0; j < TN; ++j) {
-                if constexpr (EPI == EPI_BIAS_F16 || EPI == EPI_GELU_F16) {
-#pragma unroll
-                    for (int gp = 0; gp < 2; ++gp) {
-                        float x[8];
-#pragma unroll
-                        for (int e = 0; e < 8; ++e) x[e] = acc[i][j][8 * gp + e];
-                        if constexpr (EPI == EPI_GELU_F16) {
-#pragma unroll
-                            for (int e = 0; e < 8; e += 2) {
-                                const f32x2 gv = gelu2((f32x2){x[e], x[e + 1]});
-                                x[e] = gv.x;
-                                x[e + 1] = gv.y;
-                            }
-                        }
-                        half8 h;
-#pragma unroll
-                        for (int e = 0; e < 8; ++e) h[e] = (f16)x[e];
-                        uint4 hv = __builtin_bit_cast(uint4, h);     // .xy group 2gp, .zw group 2gp+1
-                        auto s0 = __builtin_amdgcn_permlane32_swap(hv.x, hv.z, false, false);
-                        auto s1 = __builtin_amdgcn_permlane32_swap(hv.y, hv.w, false, false);
-                        const uint4 sv = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-                        const int col = n0 + wn * WTN + 32 * j + 16 * gp + 8 * fh;
-                        f16* orow = (f16*)ep.out + (size_t)((VAR & 8) ? (row & 255) : row) * ep.ldc;
-                        if (ok) st16<VAR>((uint4*)(orow + col), sv);
-                        if constexpr (EPI == EPI_GELU_F16) {
-                            if (ep.kx == 3) {
-                                half8 l, md;
-#pragma unroll
-                                for (int e = 0; e < 8; ++e) {
-                                    l[e] = x3_lo(x[e], h[e]);
-                                    md[e] = x3_mid(h[e]);
-                                }
-                                uint4 lv = __builtin_bit_cast(uint4, l), mv = __builtin_bit_cast(uint4, md);
-                                auto t0 = __builtin_amdgcn_permlane32_swap(lv.x, lv.z, false, false);
-                                auto t1 = __builtin_amdgcn_permlane32_swap(lv.y, lv.w, false, false);
-                                auto u0 = __builtin_amdgcn_permlane32_swap(mv.x, mv.z, false, false);
-                                auto u1 = __builtin_amdgcn_permlane32_swap(mv.y, mv.w, false, false);
-                                if (ok) {
-                                    st16<VAR>((uint4*)(orow + ep.nlog + col), make_uint4(u0[0], u1[0], u0[1], u1[1]));
-                                    st16<VAR>((uint4*)(orow + 2 * ep.nlog + col), make_uint4(t0[0], t1[0], t0[1], t1[1]));
-                                }
-                            }
-                        }
-                    }
-                } else {  // EPI_BIAS_F32, EPI_GELU_F32, EPI_RES_F32, EPI_RESLN_F32
-#pragma unroll
-                    for (int g = 0; g < 4; ++g) {
-                        float x[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-                        if constexpr (EPI == EPI_GELU_F32) {
-#pragma unroll
-                            for (int e = 0; e < 4; e += 2) {
-                                const f32x2 gv = gelu2((f32x2){x[e], x[e + 1]});
-                                x[e] = gv.x;
-                                x[e + 1] = gv.y;
-                            }
-                        }
-                        const size_t o = (size_t)((VAR & 8) ? (row & 255) : row) * ep.ldc + cbase + 32 * j + 8 * g;
-                        if (ok) st16<VAR>((uint4*)((float*)ep.out + o), __builtin_bit_cast(uint4, make_float4(x[0], x[1], x[2], x[3])));
-                    }
-                }
-            }
-        }
     } else {
         // Through LDS: each wave parks one 32-row slice of its accumulators (fp32, row
         // stride WTN+4 floats: conflict-free b128 writes) in a private region, then reads it
@@ -591,13 +332,8 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 const float4 u0 = *(const float4*)(lw + rr * LDW + cc);
                 const float4 u1 = *(const float4*)(lw + rr * LDW + cc + 4);
                 float x[8] = {u0.x, u0.y, u0.z, u0.w, u1.x, u1.y, u1.z, u1.w};
-                if constexpr (VAR & 16) {       // diagnostic: LDS pass + conversion, no store
-                    asm volatile("" ::"v"(x[0]), "v"(x[3]), "v"(x[7]));
-                    continue;
-                }
                 if (row < ep.m_valid) {
-                    // VAR&8 (diagnostic): every tile stores into rows 0..255 (L2-resident)
-                    const size_t o = (size_t)((VAR & 8) ? (row & 255) : row) * ep.ldc + col;
+                    const size_t o = (size_t)row * ep.ldc + col;
                     if constexpr (EPI == EPI_GELU_F16 || EPI == EPI_GELU_F32) {
 #pragma unroll
                         for (int e = 0; e < 8; e += 2) {
@@ -655,21 +391,20 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
     constexpr int BM = 256, BN = 256, WN = 4, BK = 64, NW = 8;
     constexpr int A_BYTES = BM * BK * 2, STAGE = (BM + BN) * BK * 2;
     constexpr int WTM = 128, WTN = 64;
-    constexpr int MS = (VAR & 8192) ? 16 : 32;    // MFMA shape (VAR bit 8192: 16x16x32)
+    constexpr int MS = 32;                        // v_mfma_f32_32x32x16_f16 (16x16: +7 % QKV time)
     constexpr int KPS = 512 / MS, CPS = KPS / 8, NQ = MS * MS / 256;
     typedef typename AccT<MS>::type accT;
     constexpr int TM = WTM / MS, TN = WTN / MS, NBQ = TN * NQ;   // NBQ: bias quads per lane
     constexpr int RB = BK * 2, CPR = BK / 8, RPP = 1024 / RB;
     constexpr int A_PIECES = BM / RPP, PIECES = (BM + BN) / RPP, PPW = PIECES / NW;
-    constexpr int LDH = WTN + 8;                  // epilogue slab row, halfs (16-B aligned rows)
     constexpr int NSTORE = (WTM / 32) * 4;        // 16-B stores per wave per tile
     constexpr int NSUB = BK / KPS, NR = TM + TN, NM = TM * TN;
     static_assert(EPI == EPI_BIAS_F16 || EPI == EPI_GELU_F16, "fp16-output epilogues only");
     // VAR 4194304: fp16x3 precision mode (kx = 3) — the GELU output is written as the
     // three-part operand image [hi | hi/64 | lo·64] of the next GEMM (ep.nlog columns apart)
     constexpr bool X3 = (VAR & 4194304) != 0;
-    static_assert(!X3 || (EPI == EPI_GELU_F16 && MS == 32 && !(VAR & 32768)), "x3 image: GELU, 32x32 slab path");
-    static_assert(NW * 32 * LDH * 2 <= STAGE, "epilogue slab fits in one buffer");
+    static_assert(!X3 || EPI == EPI_GELU_F16, "x3 image: GELU");
+    static_assert(NW * 32 * 128 <= STAGE, "epilogue slab fits in one buffer");
     extern __shared__ __attribute__((aligned(16))) char smem[];
 
     const int tid = threadIdx.x, lane = tid & 63;
@@ -792,40 +527,6 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
                         acc[i][j] = mfma_f16<MS>(bf[j], af[i], acc[i][j]);
             };
             static_assert(NSUB == 2 || NSUB == 4, "substeps per K-step");
-            if constexpr (MS == 16 && (VAR & 16384)) {
-                // Rolling fragments (16x16x32, NSUB = 2): the B fragments are double-buffered,
-                // the A fragment i of substep 1 is read into af0[i] right after the MFMAs
-                // reading it retire from issue: 128 accumulator + 64 fragment registers.
-                static_assert(NSUB == 2, "rolling schedule: two substeps per K-step");
-                const int xa1 = offA ^ (CPS << 4), xb1 = offB ^ (CPS << 4);
-                load_frags(0, af0, bf0);
-#pragma unroll
-                for (int i = 0; i < TM; ++i) {
-#pragma unroll
-                    for (int j = 0; j < TN; ++j) acc[i][j] = mfma_f16<MS>(bf0[j], af0[i], acc[i][j]);
-                    if (i == 0) {
-#pragma unroll
-                        for (int j = 0; j < TN; ++j) bf1[j] = *(const half8*)(sb + xb1 + j * MS * RB);
-                    }
-                    af0[i] = *(const half8*)(sb + xa1 + i * MS * RB);
-                }
-                mfmas(af0, bf1);
-                __builtin_amdgcn_sched_group_barrier(0x100, NR, 0);
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                }
-#pragma unroll
-                for (int i = 1; i < TM; ++i) {
-                    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                    __builtin_amdgcn_sched_group_barrier(0x008, TN - 1, 0);
-                }
-                __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-                __builtin_amdgcn_sched_group_barrier(0x008, NM, 0);
-                continue;
-            }
             if constexpr (NSUB == 4 && STAG) {
                 {
                     // Stagger (MI355X_MICROARCH 'Two waves per SIMD' item 9): the younger wave
@@ -906,12 +607,9 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
         // every wave is done reading the ring (the slab lives in buffer 1).  VAR 1048576: the
         // slabs have their own LDS, and with an even K-step count the next tile's stage 0
         // (buffer 0) was last read before the final K-step's barrier, so no wave waits here
-        if (!((VAR & 1048576) && MS == 32) || (nk & 1)) asm volatile("s_barrier" ::: "memory");
-        // VAR 2097152 (with the private slabs): the next tile's stage 0 and bias are issued
-        // before this tile's epilogue math instead of after it (more time to land)
+        if (!(VAR & 1048576) || (nk & 1)) asm volatile("s_barrier" ::: "memory");
         const int cm0 = m0, cn0 = n0;
         bool more = false;
-        constexpr bool EARLY = (VAR & 2097152) && (VAR & 1048576) && MS == 32;
         auto issue_next = [&]() {
             t += gridDim.x;
             more = t < n_tiles;
@@ -922,19 +620,17 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
                 load_bias(n0);
             }
         };
-        if constexpr (EARLY) issue_next();
         // epilogue part 1: bias/GELU, fp16, transposed through the wave's slab (buffer 1) into
         // whole-row registers; no LDS access follows the next tile's DMA issue below
-        f16* slab = (f16*)(smem + STAGE) + wave * 32 * LDH;
         const int rr0 = lane >> 3, cc = (lane & 7) * 8;
         uint4 ov[WTM / 32][4];
         f16* obase = (f16*)ep.out + (size_t)(cm0 + wm * WTM + rr0) * ep.ldc + cn0 + wn * WTN + cc;
-        if constexpr (MS == 32 && !(VAR & 32768)) {
+        {
             // 32x32x16 accumulators: v_permlane32_swap packs 8 consecutive columns per lane
             // (lanes 0-31 the low, 32-63 the high 8 of each 16-column pair), stored as one
             // ds_write_b128 into 128-B slab rows with the 16-B chunk XOR-swizzled by (row & 7):
             // the 8-lane write groups (8 rows, one chunk) and the 16-lane read groups (two rows,
-            // all chunks) are both conflict-free (the padded layout below: 2-way on both)
+            // all chunks) are both conflict-free (a padded layout measured 2-way on both, round 1)
             static_assert(WTN == 64, "slab rows of 8 chunks");
             char* slb = smem + ((VAR & 1048576) ? 2 * STAGE : STAGE) + wave * 32 * 128;
             if constexpr (X3) {
@@ -1011,30 +707,9 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
             } else {
                 build_img(0, std::false_type{});
             }
-        } else
-#pragma unroll
-        for (int i32 = 0; i32 < WTM / 32; ++i32) {     // 32-row slices of the wave tile
-#pragma unroll
-            for (int sub = 0; sub < 32 / MS; ++sub) {
-                const int i = i32 * (32 / MS) + sub;
-#pragma unroll
-                for (int j = 0; j < TN; ++j)
-#pragma unroll
-                    for (int g = 0; g < NQ; ++g) {
-                        float x[4] = {acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-                        if constexpr (EPI == EPI_GELU_F16) {
-                            const f32x2 a = gelu2((f32x2){x[0], x[1]}), b = gelu2((f32x2){x[2], x[3]});
-                            x[0] = a.x; x[1] = a.y; x[2] = b.x; x[3] = b.y;
-                        }
-                        const half4 h = {(f16)x[0], (f16)x[1], (f16)x[2], (f16)x[3]};
-                        *(half4*)(slab + (sub * MS + frow) * LDH + MS * j + qcol<MS>(g, lane)) = h;
-                    }
-            }
-#pragma unroll
-            for (int it = 0; it < 4; ++it) ov[i32][it] = *(const uint4*)(slab + (it * 8 + rr0) * LDH + cc);
         }
         // part 2: the next tile's stage 0 (buffer 0) and bias
-        if constexpr (!EARLY) issue_next();
+        issue_next();
         // part 3: this tile's stores (whole 128-B row segments, non-temporal)
 #pragma unroll
         for (int i = 0; i < WTM / 32; ++i)
@@ -1074,17 +749,15 @@ template <int EPI, int VAR>
 __global__ void __launch_bounds__(512)
 gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int ldw, int n_tiles_n, int n_tiles,
                 EpiArgs ep) {
-    constexpr int BM = 256, BK = 32, NW = 8, WN = 4, WTM = 128, WTN = 64, MS = 32;
-    constexpr int TM = WTM / MS, TN = WTN / MS;
+    constexpr int BM = 256, BK = 32, NW = 8, WN = 4, WTM = 128, WTN = 64;
     constexpr int RB = BK * 2;                   // 64-byte LDS rows
     constexpr int REG = BM * RB;                 // one 256-row region: 16 KiB
     constexpr int STAGE = 4 * REG;               // A_hi | A_lo | W_hi | W_lo
-    constexpr int NSTORE = EPI == EPI_BIAS_F16 ? 16 : 32;
-    static_assert(EPI == EPI_BIAS_F32 || EPI == EPI_GELU_F16 || EPI == EPI_BIAS_F16 || EPI == EPI_LNRES_IMG,
-                  "x3s epilogues");
+    constexpr int NSTORE = 32;                   // epilogue stores per wave per tile
+    static_assert(EPI == EPI_BIAS_F32 || EPI == EPI_GELU_F16 || EPI == EPI_LNRES_IMG, "x3s epilogues");
     constexpr bool LNR = EPI == EPI_LNRES_IMG;
-    static_assert(!LNR || ((VAR & 128) != 0 && (VAR & 2) == 0), "the LayerNorm epilogue is written for the 16x16 form");
-    static_assert((VAR & 16777216) == 0 || (LNR && (VAR & 16) != 0), "the permuted-column layout is written for the LayerNorm epilogue");
+    static_assert(!LNR || (VAR & 2) == 0, "the LayerNorm epilogue has no no-store diagnostic");
+    static_assert((VAR & 16777216) == 0 || LNR, "the permuted-column layout is written for the LayerNorm epilogue");
     extern __shared__ __attribute__((aligned(16))) char smem[];        // the LDS-DMA ring (2 stages)
     // wave-private epilogue slabs: a separate LDS object, so the compiler can tell the slab
     // reads do not alias the LDS-DMA writes in flight (no vmcnt wait before them)
@@ -1093,7 +766,6 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int wm = wave / WN, wn = wave % WN;
-    const int frow = lane & 31, fh = lane >> 5;
     const int nk = K / BK;
     int t = blockIdx.x;
     typedef __attribute__((address_space(1))) unsigned gu32;
@@ -1103,34 +775,25 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         // dispatched; a different placement changes only speed): the workgroups of group x = b & 7
         // take gangs of n_tiles_n consecutive positions p = b >> 3; the few left over in each
         // group form the last gangs across groups.  A gang's column tiles then read their shared
-        // A panel through one L2.  Every workgroup is resident (grid <= CUs at one per CU), as
-        // with the ticket form.
+        // A panel through one L2.  Needs every workgroup resident: cooperative launch (RS_LNGANG=xcd).
         const int G = gridDim.x, ntn = n_tiles_n, x = blockIdx.x & 7, pp = blockIdx.x >> 3;
-        int loc_before = 0, left_before = 0, nloc = 0, nx = 0;
+        int loc_before = 0, left_before = 0, nloc = 0, total_loc = 0;
         for (int y = 0; y < 8; ++y) {
             const int ny = G > y ? (G - y + 7) / 8 : 0, ly = ny / ntn * ntn;
             if (y < x) {
                 loc_before += ly;
                 left_before += ny - ly;
             }
-            if (y == x) {
-                nx = ny;
-                nloc = ly;
-            }
-            (void)nx;
-        }
-        int total_loc = 0;
-        for (int y = 0; y < 8; ++y) {
-            const int ny = G > y ? (G - y + 7) / 8 : 0;
-            total_loc += ny / ntn * ntn;
+            if (y == x) nloc = ly;
+            total_loc += ly;
         }
         t = pp < nloc ? loc_before + pp : total_loc + left_before + (pp - nloc);
     } else if constexpr (LNR) {
-        // first tiles by ticket, in the order workgroups start: the grid is whole row panels and
-        // fits the chip at one workgroup per CU, so each row panel's column tiles form a gang of
-        // resident workgroups, and a gang walks the panels p, p + G, p + 2G, ... (G = gangs) with
-        // each member keeping its column: t += gridDim.x.  The statistics exchange
-        // (lnres_epilogue) is within a gang only, whose members all run the same panel sequence.
+        // first tiles by ticket, in the order workgroups start: each row panel's column tiles
+        // form a gang of workgroups that have all started (so the statistics exchange cannot
+        // wait on a workgroup that is not resident, at any residency), and a gang walks the
+        // panels p, p + G, p + 2G, ... (G = gangs) with each member keeping its column:
+        // t += gridDim.x.  The exchange (lnres_epilogue) is within a gang only.
         if (tid == 0) {
             // a monotonic counter: this launch's tickets start at ep.ln_base (kept by the host)
             const unsigned c = __hip_atomic_fetch_add((gu32*)ep.lncnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1140,9 +803,9 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         t = (int)*(const unsigned*)(slabs + 2048);
     }
     if ((unsigned)t >= (unsigned)n_tiles) return;
-    if constexpr ((VAR & 262144) != 0) {
-        if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
-    }
+    // the younger wave half (waves 4-7, one per SIMD beside an older partner) at s_setprio 1
+    // (MI355X_MICROARCH 'Two waves per SIMD' item 4)
+    if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
     auto tile_of = [&](int tt, int& m0, int& n0) {
         if constexpr (LNR) {                      // row panel t / ntn, column tile t % ntn
             m0 = (tt / n_tiles_n) * BM;
@@ -1158,29 +821,20 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         m0 = (g * GM + (loc - tn * gm)) * BM;
         n0 = tn * BM;
     };
-    // LDS-DMA: 1 KiB pieces of 16 rows x 64 B; wave w stages pieces p = 0..7 of region p >> 1,
-    // rows (p & 1) * 128 + w * 16 + lane / 4 (16-B chunk lane & 3, source-swizzled)
-    constexpr bool M16 = (VAR & 128) != 0;
+    // LDS-DMA: buffer_load_dwordx4 ... lds (32-bit lane offsets into a per-tile panel buffer
+    // descriptor, k0 in the scalar offset), 1 KiB pieces of 16 rows x 64 B; wave w stages pieces
+    // p = 0..7 of region p >> 1, rows (p & 1) * 128 + w * 16 + lane / 4 (16-B chunk lane & 3,
+    // g16-swizzled on the source address)
     const int prow = wave * 16 + (lane >> 2);
-    const int pswz = (M16 ? (lane & 3) ^ g16(prow >> 2) : swz<32>(prow, lane & 3)) * 8;
+    const int pswz = ((lane & 3) ^ g16(prow >> 2)) * 8;
     const size_t ld2 = (size_t)2 * K;
-    const f16* srcA;
-    const f16* srcW;
-    auto set_src = [&](int m0, int n0) {
-        srcA = A + (size_t)(m0 + prow) * ld2 + pswz;
-        srcW = W + (size_t)(n0 + prow) * ldw + pswz;
-    };
-    // VAR 16: the pieces as buffer_load_dwordx4 ... lds (32-bit lane offsets into a per-tile
-    // panel descriptor, k0 in the scalar offset) instead of global_load_lds (64-bit lane
-    // addresses): half the address data per DMA instruction
     __amdgpu_buffer_rsrc_t rsA, rsW;
     int voffA[4], voffW[4];                       // lane byte offsets: (p & 1) row half x (r & 1) hi / lo
-    // VAR 16777216 (16x16 form): output columns permuted inside each 32-column group so that a
-    // lane's two 16-column MFMA blocks 2m, 2m + 1 hold 8 CONSECUTIVE output columns (32 m + 8 q4
-    // .. + 7) instead of two runs of 4: W image row 32 m + 16 jj + 4 q + e is W row
-    // 32 m + 8 q + 4 jj + e.  The epilogue's per-lane loads (bias, residual image, LayerNorm
-    // weights) become 16-B loads, half as many instructions.
-    constexpr bool PERM = M16 && (VAR & 16777216) != 0;
+    // VAR 16777216: output columns permuted inside each 32-column group so that a lane's two
+    // 16-column MFMA blocks 2m, 2m + 1 hold 8 CONSECUTIVE output columns (32 m + 8 q4 .. + 7)
+    // instead of two runs of 4: W image row 32 m + 16 jj + 4 q + e is W row 32 m + 8 q + 4 jj + e.
+    // The epilogue's per-lane loads (bias, residual image, LayerNorm weights) become 16-B loads.
+    constexpr bool PERM = (VAR & 16777216) != 0;
     auto wperm = [](int L) {
         return PERM ? (L & ~31) | (((L >> 2) & 3) << 3) | (((L >> 4) & 1) << 2) | (L & 3) : L;
     };
@@ -1197,116 +851,30 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     };
     auto piece = [&](int buf, int k0, int p) {
         if constexpr ((VAR & 1) != 0) return;     // diagnostic: no K-loop staging (stale tiles)
-        if constexpr ((VAR & 1024) != 0) {        // diagnostic: the W half of the staging only
-            if (p < 4) return;
-        }
-        if constexpr ((VAR & 2048) != 0) {        // diagnostic: the A half of the staging only
-            if (p >= 4) return;
-        }
         const int r = p >> 1;
-        if constexpr ((VAR & 16) != 0) {
-            // VAR 4096 (diagnostic): 4-byte pieces — the same instruction count, a quarter of
-            // the bytes (separates the DMA's issue cost from its bandwidth)
-            auto* dst = (__attribute__((address_space(3))) void*)(smem + buf * STAGE + r * REG + ((p & 1) * 8 + wave) * 1024);
-            const int vo = (r < 2 ? voffA : voffW)[2 * (p & 1) + (r & 1)];
-            if constexpr ((VAR & 4096) != 0) __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 4, vo, k0 * 2, 0, 0);
-            else __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 16, vo, k0 * 2, 0, 0);
-            return;
-        }
-        if (k0 >= K) return;                      // (flat-address form: no past-the-panel dummy step)
-        const f16* g = r < 2 ? srcA + (size_t)(p & 1) * 128 * ld2 + (r & 1) * K + k0
-                             : srcW + (size_t)(p & 1) * 128 * ldw + (r & 1) * K + k0;
-        __builtin_amdgcn_global_load_lds((const void*)g,
-                                         (__attribute__((address_space(3))) void*)(smem + buf * STAGE + r * REG +
-                                                                                    ((p & 1) * 8 + wave) * 1024),
-                                         16, 0, 0);
+        auto* dst = (__attribute__((address_space(3))) void*)(smem + buf * STAGE + r * REG + ((p & 1) * 8 + wave) * 1024);
+        const int vo = (r < 2 ? voffA : voffW)[2 * (p & 1) + (r & 1)];
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 16, vo, k0 * 2, 0, 0);
     };
     auto stage = [&](int buf, int k0) {
 #pragma unroll
         for (int p = 0; p < 8; ++p) piece(buf, k0, p);
     };
-    // VAR 32768 (with 16): piece p of this wave (partner 0) or of wave + 4 (partner 1): the K
-    // loop's staging is issued by the older wave half alone, so the younger wave of each SIMD
-    // (at s_setprio 1) keeps the MFMA pipe busy while its partner pays the DMA issue cost
-    auto piece2 = [&](int buf, int k0, int p, int partner) {
-        const int r = p >> 1;
-        auto* dst = (__attribute__((address_space(3))) void*)(smem + buf * STAGE + r * REG +
-                                                               ((p & 1) * 8 + wave + 4 * partner) * 1024);
-        const int vo = (r < 2 ? voffA : voffW)[2 * (p & 1) + (r & 1)] +
-                       partner * (r < 2 ? 128 * (int)ld2 : 128 * ldw);     // rows + 64
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 16, vo, k0 * 2, 0, 0);
-    };
-    // fragment addresses: row R, logical chunk 2s + fh -> position (fh ^ ((R >> 2) & 3)) ^ 2s;
-    // rows 32 apart share the swizzle, so fragment / region offsets are immediates
-    const int offA = (wm * WTM + frow) * RB + ((fh ^ (((wm * WTM + frow) >> 2) & 3)) << 4);
-    const int offW = 2 * REG + (wn * WTN + frow) * RB + ((fh ^ (((wn * WTN + frow) >> 2) & 3)) << 4);
-    struct Frags { half8 ah[TM], al[TM], wh[TN], wl[TN]; };
-    auto load_frags = [&](int buf, int s, Frags& f) {
-        const char* sb = smem + buf * STAGE;
-        const int xa = offA ^ (s << 5), xw = offW ^ (s << 5);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-            f.wh[j] = *(const half8*)(sb + xw + j * MS * RB);
-            f.wl[j] = *(const half8*)(sb + xw + REG + j * MS * RB);
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-            f.ah[i] = *(const half8*)(sb + xa + i * MS * RB);
-            f.al[i] = *(const half8*)(sb + xa + REG + i * MS * RB);
-        }
-    };
-    f32x16 acc[TM][TN];
     const half8 down = (half8)(f16)X3_DOWN;
-    // VAR 32 (timing diagnostic, wrong results): each 32x32x16 MFMA replaced by two 16x16x32
-    // MFMAs on the same operands (equal MFMA cycles) -- what the 16x16 shape's clock would buy
-    auto mf = [&](half8 b, half8 a, f32x16 c) -> f32x16 {
-        if constexpr ((VAR & 32) != 0) {
-            f32x4 lo = {c[0], c[1], c[2], c[3]}, hi = {c[4], c[5], c[6], c[7]};
-            lo = __builtin_amdgcn_mfma_f32_16x16x32_f16(b, a, lo, 0, 0, 0);
-            hi = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, hi, 0, 0, 0);
-            c[0] = lo[0]; c[1] = lo[1]; c[2] = lo[2]; c[3] = lo[3];
-            c[4] = hi[0]; c[5] = hi[1]; c[6] = hi[2]; c[7] = hi[3];
-            return c;
-        } else {
-            return __builtin_amdgcn_mfma_f32_32x32x16_f16(b, a, c, 0, 0, 0);
-        }
-    };
-    auto mfma3 = [&](Frags& f) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] = mf(f.wh[j], f.ah[i], acc[i][j]);
-#pragma unroll
-        for (int j = 0; j < TN; ++j) f.wh[j] *= down;                  // W_hi / 64
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] = mf(f.wh[j], f.al[i], acc[i][j]);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) f.ah[i] *= down;                  // A_hi / 64
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j) acc[i][j] = mf(f.wl[j], f.ah[i], acc[i][j]);
-    };
 
-    // VAR 128: v_mfma_f32_16x16x32_f16 (one MFMA per BK = 32 step).  Lane l supplies row
-    // (l & 15) of a 16-row block at 16-B k-chunk (l >> 4): a wave reads 16 whole 64-B rows per
-    // ds_read_b128, which the g16 chunk swizzle keeps conflict-free.  The chip holds a higher
-    // clock under the 16x16 shape at equal MFMA cycles (MI355X_MICROARCH 'DVFS give-back' 7;
-    // +6-8 % here, rs_debug_gemm cfg 32 dbg 12).  acc16[i][j]: rows 16 i + (l & 15) of the
-    // wave tile, columns 16 j + 4 (l >> 4) .. +3.  Per K-step: W_hi, W_lo of the wave's 64
-    // columns once (+ W_hi / 64 in registers), then two halves of 4 row blocks each.
+    // v_mfma_f32_16x16x32_f16, one MFMA per BK = 32 step.  Lane l supplies row (l & 15) of a
+    // 16-row block at 16-B k-chunk (l >> 4): a wave reads 16 whole 64-B rows per ds_read_b128,
+    // which the g16 chunk swizzle keeps conflict-free.  The chip holds a higher clock under the
+    // 16x16 shape at equal MFMA cycles (MI355X_MICROARCH 'DVFS give-back' 7; +6-8 % over
+    // 32x32x16 here).  acc16[i][j]: rows 16 i + (l & 15) of the wave tile, columns
+    // 16 j + 4 (l >> 4) .. +3.  Per K-step: W_hi, W_lo of the wave's 64 columns once (+ W_hi / 64
+    // in registers), then two halves of 4 row blocks each.
     const int r16 = lane & 15, q4 = lane >> 4;
     const int offA16 = (wm * WTM + r16) * RB + ((q4 ^ g16(r16 >> 2)) << 4);
     const int offW16 = 2 * REG + (wn * WTN + r16) * RB + ((q4 ^ g16(r16 >> 2)) << 4);
     f32x4 acc16[8][4];
-    // VAR 4: the next step's eight DMA pieces ride this step's first MFMA groups; the last step
-    // of a tile passes k0n = 2^29 and issues none (a runtime test per piece).  VAR 8192 drops
-    // the test and stages that k0n anyway — past the panel descriptors' extent, which the
-    // buffer loads return as zeros without touching memory, into the buffer the next tile's
-    // stage 0 then overwrites (same wave, same rows, in order): one basic block per step, but
-    // measured 0-2 % slower (more live registers, spills outside the loop)
+    // the next step's eight DMA pieces ride this step's first MFMA groups (one per group of four
+    // MFMAs of row half 0); the last step of a tile passes k0n = 2^29 and issues none
     auto kstep16 = [&](int buf, int k0n) {
         const char* sb = smem + buf * STAGE;
         half8 wh[4], wl[4], wd[4];
@@ -1339,109 +907,28 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         const half8 a = pr == 1 ? al[ii] : ah[ii];
                         acc16[4 * h + ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b, a, acc16[4 * h + ii][j], 0, 0, 0);
                     }
-                    // the next step's eight DMA pieces, one per group of four MFMAs of half 0
-                    if constexpr ((VAR & 32768) != 0) {
-                        const int grp = 12 * h + 4 * pr + ii;
-                        if (wave < 4 && grp < 16 && k0n < (1 << 29)) {
-                            __builtin_amdgcn_sched_barrier(0);
-                            piece2(buf ^ 1, k0n, grp & 7, grp >> 3);
-                            __builtin_amdgcn_sched_barrier(0);
-                        }
-                    } else if constexpr ((VAR & 4) != 0) {
-                        // VAR 16384: the pieces spread over the whole step (every third group)
-                        constexpr bool SPREAD = (VAR & 16384) != 0;
-                        const int grp = 12 * h + 4 * pr + ii;
-                        const bool at = SPREAD ? grp % 3 == 0 : grp < 8;
-                        if (at && ((VAR & 8192) != 0 || k0n < (1 << 29))) {
-                            __builtin_amdgcn_sched_barrier(0);
-                            piece(buf ^ 1, k0n, SPREAD ? grp / 3 : grp);
-                            __builtin_amdgcn_sched_barrier(0);
-                        }
+                    const int grp = 12 * h + 4 * pr + ii;
+                    if (grp < 8 && k0n < (1 << 29)) {
+                        __builtin_amdgcn_sched_barrier(0);
+                        piece(buf ^ 1, k0n, grp);
+                        __builtin_amdgcn_sched_barrier(0);
                     }
                 }
             }
         }
     };
 
-    // VAR 524288 (16x16 form): the younger wave half (waves 4-7) runs half a K-step behind the
-    // older half (MI355X_MICROARCH 'Two waves per SIMD' item 9).  After the barrier of step k it
-    // first runs the second row half (h = 1) of step k-1 from fragments it read into registers
-    // before that barrier (the DMA of step k+1 into that buffer is issued only after it, riding
-    // these MFMAs), then reads and runs (k, h = 0), and reads (k, h = 1) to carry across the
-    // next barrier.  So at each barrier only the older half opens with an LDS read burst while
-    // the younger half's MFMAs keep each SIMD's pipe busy.  Same fragments, same MFMAs in the
-    // same accumulator order: results bitwise equal to the unstaggered form.
-    constexpr bool STAG = M16 && (VAR & 524288) != 0;
-    auto read_w16 = [&](int buf, half8 (&wh)[4], half8 (&wl)[4], half8 (&wd)[4]) {
-        const char* sb = smem + buf * STAGE;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            wh[j] = *(const half8*)(sb + offW16 + j * 1024);
-            wl[j] = *(const half8*)(sb + offW16 + REG + j * 1024);
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) wd[j] = wh[j] * down;
-    };
-    auto read_a16 = [&](int buf, int h, half8 (&ah)[4], half8 (&al)[4]) {
-        const char* sb = smem + buf * STAGE;
-#pragma unroll
-        for (int ii = 0; ii < 4; ++ii) {
-            ah[ii] = *(const half8*)(sb + offA16 + (4 * h + ii) * 1024);
-            al[ii] = *(const half8*)(sb + offA16 + REG + (4 * h + ii) * 1024);
-        }
-    };
-    // one row half's 48 MFMAs; the eight DMA pieces of (dbuf, k0n) ride its first 8 groups
-    auto mf_half16 = [&](auto hc, half8 (&wh)[4], half8 (&wl)[4], half8 (&wd)[4], half8 (&ah)[4], half8 (&al)[4],
-                         int dbuf, int k0n) {
-        constexpr int h = decltype(hc)::value;
-#pragma unroll
-        for (int pr = 0; pr < 3; ++pr) {
-            if (pr == 2) {
-#pragma unroll
-                for (int ii = 0; ii < 4; ++ii) ah[ii] *= down;
-            }
-#pragma unroll
-            for (int ii = 0; ii < 4; ++ii) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const half8 b = pr == 0 ? wh[j] : pr == 1 ? wd[j] : wl[j];
-                    const half8 a = pr == 1 ? al[ii] : ah[ii];
-                    acc16[4 * h + ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b, a, acc16[4 * h + ii][j], 0, 0, 0);
-                }
-                const int grp = 4 * pr + ii;
-                if (grp < 8 && k0n < (1 << 29)) {
-                    __builtin_amdgcn_sched_barrier(0);
-                    piece(dbuf, k0n, grp);
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-        }
-    };
-    const bool young = STAG && wave >= NW / 2;
-
     int m0, n0;
     tile_of(t, m0, n0);
-    set_src(m0, n0);
     set_rsrc(m0, n0);
     stage(0, 0);
     int par = 0;                                                  // buffer of K-step 0
     bool first = true;
-    Frags F;
     for (;;) {
-        if constexpr (M16) {
 #pragma unroll
-            for (int i = 0; i < 8; ++i)
+        for (int i = 0; i < 8; ++i)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) acc16[i][j] = (f32x4)(0.f);
-        } else {
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) acc[i][j] = (f32x16)(0.f);
-        }
-        // STAG: the fragments carried across a barrier (scoped to the tile, so none is live
-        // across the epilogue)
-        half8 cwh[4], cwl[4], cwd[4], cah[4], cal[4];
+            for (int j = 0; j < 4; ++j) acc16[i][j] = (f32x4)(0.f);
         for (int kt = 0; kt < nk; ++kt) {
             const int cur = (par + kt) & 1;
             // step kt landed for this wave (at a tile's first step the previous tile's stores
@@ -1452,162 +939,49 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             } else if (kt == 0 && !first) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             asm volatile("s_barrier" ::: "memory");
-            if constexpr (STAG) {
-                // one code path for both halves (one register set): the younger half runs the
-                // (kt-1, h = 1) block first, the older half (kt, h = 1) last
-                using H0 = std::integral_constant<int, 0>;
-                using H1 = std::integral_constant<int, 1>;
-                const int k0n = kt + 1 < nk ? (kt + 1) * BK : (1 << 29);
-                __builtin_amdgcn_sched_barrier(0);
-                // VAR 2097152: the younger half's pieces ride its (kt, h = 0) block instead — the
-                // second half of the step, away from the older half's pieces
-                constexpr bool LATE_DMA = (VAR & 2097152) != 0;
-                if (young && kt > 0) mf_half16(H1(), cwh, cwl, cwd, cah, cal, cur ^ 1, LATE_DMA ? (1 << 29) : k0n);
-                read_w16(cur, cwh, cwl, cwd);
-                read_a16(cur, 0, cah, cal);
-                mf_half16(H0(), cwh, cwl, cwd, cah, cal, cur ^ 1, !young || kt == 0 || LATE_DMA ? k0n : (1 << 29));
-                read_a16(cur, 1, cah, cal);
-                if (!young) mf_half16(H1(), cwh, cwl, cwd, cah, cal, cur ^ 1, 1 << 29);
-                __builtin_amdgcn_sched_barrier(0);
-                continue;
-            }
-            if constexpr ((VAR & 8388608) != 0) {
-                // VAR 8388608 (diagnostic): the A slice of step kt + 2 touched into L2 by one
-                // plain 4-B load per lane (lane = (row, part)), so the A pieces' DMA hits L2
-                if (kt + 2 < nk) {
-                    const f16* pa = A + (size_t)(m0 + (tid & 255)) * ld2 + (tid >> 8) * K + (kt + 2) * BK;
-                    unsigned dummy;
-                    asm volatile("global_load_dword %0, %1, off" : "=v"(dummy) : "v"(pa) : "memory");
-                }
-            }
-            if constexpr (M16) {
-                const bool st_ok = kt + 1 < nk;
-                if ((VAR & 4) == 0 && (VAR & 32768) == 0 && st_ok) stage(cur ^ 1, (kt + 1) * BK);
-                __builtin_amdgcn_sched_barrier(0);
-                kstep16(cur, st_ok ? (kt + 1) * BK : (1 << 29));
-                __builtin_amdgcn_sched_barrier(0);
-                continue;
-            }
-            if constexpr ((VAR & 4) != 0) {
-                // VAR 4: step kt+1's eight DMA pieces spread over substep 0's MFMAs (one or
-                // two per group of four), so neither wave of a SIMD spends the start of the
-                // step issuing DMA while its partner does the same and the MFMA pipe idles
-                const bool st_ok = kt + 1 < nk;
-                load_frags(cur, 0, F);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int q = 0; q < 6; ++q) {
-                    // MFMAs 4q .. 4q+3 of the substep: product q / 2, row pair (q & 1)
-                    const int pr = q >> 1;
-                    if (q == 2) {
-#pragma unroll
-                        for (int j = 0; j < TN; ++j) F.wh[j] *= down;
-                    }
-                    if (q == 4) {
-#pragma unroll
-                        for (int i = 0; i < TM; ++i) F.ah[i] *= down;
-                    }
-#pragma unroll
-                    for (int ii = 0; ii < 2; ++ii)
-#pragma unroll
-                        for (int j = 0; j < TN; ++j) {
-                            const int i = 2 * (q & 1) + ii;
-                            const half8 a = pr == 0 ? F.ah[i] : pr == 1 ? F.al[i] : F.ah[i];
-                            const half8 b = pr == 2 ? F.wl[j] : F.wh[j];
-                            acc[i][j] = mf(b, a, acc[i][j]);
-                        }
-                    __builtin_amdgcn_sched_barrier(0);
-                    if (st_ok) {
-                        piece(cur ^ 1, (kt + 1) * BK, q < 2 ? 2 * q : q + 2);
-                        if (q < 2) piece(cur ^ 1, (kt + 1) * BK, 2 * q + 1);
-                    }
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-                load_frags(cur, 1, F);
-                mfma3(F);
-                __builtin_amdgcn_sched_barrier(0);
-                continue;
-            }
-            if (kt + 1 < nk) stage(cur ^ 1, (kt + 1) * BK);
             __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                load_frags(cur, s, F);
-                mfma3(F);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        }
-        if constexpr (STAG) {
-            if (young) mf_half16(std::integral_constant<int, 1>(), cwh, cwl, cwd, cah, cal, 0, 1 << 29);   // (nk-1, h = 1)
+            kstep16(cur, kt + 1 < nk ? (kt + 1) * BK : (1 << 29));
+            __builtin_amdgcn_sched_barrier(0);
         }
         // ---- transition
         const int last = (par + nk - 1) & 1;                      // buffer of the last K-step
         const int cm0 = m0, cn0 = n0;
-        // bias of this tile (16-B quads of the lane's 4 consecutive columns): only the bias
-        // loads are outstanding here (the last K-step issued no DMA), so one vmcnt(0) waits
-        // for exactly them; inline asm keeps the compiler from placing its own wait
-        f32x4 bq[TN * 4];
-        if constexpr (M16) {
-            // columns 16 j + 4 (l >> 4) .. +3 of the wave's 64
+        // bias of this tile (16-B quads of the lane's 4 consecutive columns, 16 j + 4 (l >> 4) of
+        // the wave's 64): only the bias loads are outstanding here (the last K-step issued no
+        // DMA), so one vmcnt(0) waits for exactly them; inline asm keeps the compiler from placing
+        // its own wait
+        f32x4 bq[4];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const float* bp = ep.bias + cn0 + wn * WTN + (PERM ? 32 * (j >> 1) + 8 * q4 + 4 * (j & 1) : 16 * j + 4 * q4);
-                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bq[j]) : "v"(bp) : "memory");
-            }
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]) : : "memory");
-        } else {
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    const float* bp = ep.bias + cn0 + wn * WTN + MS * j + 8 * g + 4 * fh;
-                    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bq[4 * j + g]) : "v"(bp) : "memory");
-                }
-            asm volatile("s_waitcnt vmcnt(0)"
-                         : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]), "+v"(bq[4]), "+v"(bq[5]), "+v"(bq[6]),
-                           "+v"(bq[7])
-                         :
-                         : "memory");
+        for (int j = 0; j < 4; ++j) {
+            const float* bp = ep.bias + cn0 + wn * WTN + (PERM ? 32 * (j >> 1) + 8 * q4 + 4 * (j & 1) : 16 * j + 4 * q4);
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bq[j]) : "v"(bp) : "memory");
         }
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]) : : "memory");
         // the next tile's stage 0 (into the buffer step nk-2 used) lands while this epilogue runs
-        bool more = false;
-        auto next_tile = [&](int tt) {
-            t = tt;
-            more = t < n_tiles;
-            if (more) {
-                tile_of(t, m0, n0);
-                set_src(m0, n0);
-                set_rsrc(m0, n0);
-                stage(last ^ 1, 0);
-            }
-        };
         // (issuing it after the LayerNorm epilogue's residual loads instead, so that their waits
         // need not cover this DMA, measured -2.7 %: profiles/r3p2_lnperm_ab.txt)
-        next_tile(t + gridDim.x);
-        if constexpr (M16) {
-            // bias (+ GELU) of row blocks [i0, i1)
-            auto finish = [&](int i0, int i1) {
+        bool more = false;
+        t += gridDim.x;
+        more = t < n_tiles;
+        if (more) {
+            tile_of(t, m0, n0);
+            set_rsrc(m0, n0);
+            stage(last ^ 1, 0);
+        }
+        // bias (+ GELU) of row blocks [i0, i1)
+        auto finish = [&](int i0, int i1) {
 #pragma unroll
-                for (int i = i0; i < i1; ++i)
+            for (int i = i0; i < i1; ++i)
 #pragma unroll
-                    for (int j = 0; j < 4; ++j)
+                for (int j = 0; j < 4; ++j)
 #pragma unroll
-                        for (int e = 0; e < 4; e += 2) {
-                            f32x2 v = {acc16[i][j][e] + bq[j][e], acc16[i][j][e + 1] + bq[j][e + 1]};
-                            if constexpr (EPI == EPI_GELU_F16) v = gelu2(v);
-                            acc16[i][j][e] = v.x;
-                            acc16[i][j][e + 1] = v.y;
-                        }
-            };
-            // EPI_LNRES_IMG: h <- image(LN(acc + bias + h)) over whole rows.  This tile's 256
-            // columns give per-row partials (sum, M2 about the tile's own mean); the gang (the row
-            // panel's column tiles) hands them to each other as tagged 8-B granules {launch tag,
-            // value} written by single sc1 stores and polled with sc1 loads until every tag is
-            // this launch's (cdna_hip_programming §6 Guideline 16, R2: the data is the flag — no
-            // drain, counter or fence), and every tile combines the partials in column-tile order
-            // (Chan's pairwise form), so a row's tiles normalise with bit-identical statistics.
-            // The poll is bounded: a timeout sets *lnerr (the host fails the call) instead of
-            // hanging the launch.
+                    for (int e = 0; e < 4; e += 2) {
+                        f32x2 v = {acc16[i][j][e] + bq[j][e], acc16[i][j][e + 1] + bq[j][e + 1]};
+                        if constexpr (EPI == EPI_GELU_F16) v = gelu2(v);
+                        acc16[i][j][e] = v.x;
+                        acc16[i][j][e + 1] = v.y;
+                    }
+        };
             auto lnres_epilogue = [&]() {
                 const int H = ep.nlog, ldc = ep.ldc, ntn = n_tiles_n;
                 const int panel = cm0 / BM, tcol = cn0 / BM;
@@ -1785,9 +1159,9 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         for (int e = 0; e < 4; ++e) acc16[i][j][e] = ln_apply(acc16[i][j][e], st, gq[j][e], bb[j][e]);
                 }
             };
-            // VAR 512 (fp16-image epilogues): each row-block pair's bias + GELU right before its
-            // slab pass, so that VALU work overlaps the previous pair's LDS and global stores
-            constexpr bool LATE = (VAR & 512) != 0 && EPI != EPI_BIAS_F32 && (VAR & 2) == 0 && !LNR;
+            // the GELU image: each row-block pair's bias + GELU right before its slab pass, so that
+            // VALU work overlaps the previous pair's LDS and global stores
+            constexpr bool LATE = EPI == EPI_GELU_F16 && (VAR & 2) == 0;
             if constexpr (LNR) lnres_epilogue();
             else if constexpr (!LATE) finish(0, 8);
             if constexpr ((VAR & 2) != 0) {      // diagnostic: no epilogue stores (acc kept alive)
@@ -1805,17 +1179,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             // VAR 33554432 (timing diagnostic, wrong results): every tile stores onto the rows of
             // row panel 0 (L2-resident lines), separating the store path from the HBM write burst
             const int sm0 = (VAR & 33554432) ? 0 : cm0;
-            if constexpr (EPI == EPI_BIAS_F32 && (VAR & 256) != 0) {
-                // VAR 256: direct 16-B stores from the accumulator layout (4 lanes cover 64
-                // contiguous bytes of a row), no slab pass
-#pragma unroll
-                for (int i = 0; i < 8; ++i)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        float* ob = (float*)ep.out + (size_t)(cm0 + wm * WTM + 16 * i + r16) * ep.ldc + cn0 + wn * WTN + 16 * j + 4 * q4;
-                        st16<64>((uint4*)ob, __builtin_bit_cast(uint4, acc16[i][j]));
-                    }
-            } else if constexpr (EPI == EPI_BIAS_F32) {
+            if constexpr (EPI == EPI_BIAS_F32) {
                 // 32 x 32 fp32 slab blocks: row blocks 2 i2 + a, column blocks 2 j2 + b
 #pragma unroll
                 for (int i2 = 0; i2 < 4; ++i2)
@@ -1835,15 +1199,14 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         for (int it = 0; it < 4; ++it) st16<64>((uint4*)(ob + (size_t)(it * 8 + rr0) * ep.ldc), v[it]);
                     }
             } else {
-                // fp16 image(s) in 32 x 64 slab blocks (row blocks 2 i2 + a, all four column
-                // blocks): image 0 = hi, image 1 (GELU / LayerNorm, two-part) = lo*64
-                constexpr int NIMG = EPI == EPI_GELU_F16 || LNR ? 2 : 1;
+                // two-part images in 32 x 64 slab blocks (row blocks 2 i2 + a, all four column
+                // blocks): image 0 = hi, image 1 = lo*64
                 // row-block pair outermost: its accumulators die after both images are out
 #pragma unroll
                 for (int i2 = 0; i2 < 4; ++i2) {
                     if constexpr (LATE) finish(2 * i2, 2 * i2 + 2);
 #pragma unroll
-                    for (int img = 0; img < NIMG; ++img) {
+                    for (int img = 0; img < 2; ++img) {
 #pragma unroll
                         for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -1870,83 +1233,6 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             if (!more) break;
             par = last ^ 1;
             first = false;
-            continue;
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-            for (int j = 0; j < TN; ++j)
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-#pragma unroll
-                    for (int e = 0; e < 4; e += 2) {
-                        f32x2 v = {acc[i][j][4 * g + e] + bq[4 * j + g][e], acc[i][j][4 * g + e + 1] + bq[4 * j + g][e + 1]};
-                        if constexpr (EPI == EPI_GELU_F16) v = gelu2(v);
-                        acc[i][j][4 * g + e] = v.x;
-                        acc[i][j][4 * g + e + 1] = v.y;
-                    }
-        if constexpr ((VAR & 2) != 0) {          // diagnostic: no epilogue stores (acc kept alive)
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) asm volatile("" ::"v"(acc[i][j]));
-            if (!more) break;
-            par = last ^ 1;
-            first = false;
-            continue;
-        }
-        // stores: each 32 x 32 (fp32) / 32 x 64 (fp16) block through the wave's private slab
-        char* slb = slabs + wave * 4096;
-        const int rr0 = lane >> 3, c16 = lane & 7;
-        if constexpr (EPI == EPI_BIAS_F32) {
-#pragma unroll
-            for (int i = 0; i < TM; ++i)
-#pragma unroll
-                for (int j = 0; j < TN; ++j) {
-#pragma unroll
-                    for (int g = 0; g < 4; ++g)
-                        *(f32x4*)(slb + frow * 128 + (((2 * g + fh) ^ (frow & 7)) << 4)) =
-                            (f32x4){acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]};
-                    float* ob = (float*)ep.out + (size_t)(cm0 + wm * WTM + MS * i) * ep.ldc + cn0 + wn * WTN + MS * j + 4 * c16;
-                    uint4 v[4];
-                    slab_read4(slb, rr0, c16, v);
-#pragma unroll
-                    for (int it = 0; it < 4; ++it) st16<64>((uint4*)(ob + (size_t)(it * 8 + rr0) * ep.ldc), v[it]);
-                }
-        } else {
-            // fp16 image(s) of the 32 x 64 block i: image 0 = hi, image 1 (GELU, two-part) = lo*64
-            constexpr int NIMG = EPI == EPI_GELU_F16 ? 2 : 1;
-#pragma unroll
-            for (int img = 0; img < NIMG; ++img)
-#pragma unroll
-                for (int i = 0; i < TM; ++i) {
-#pragma unroll
-                    for (int j = 0; j < TN; ++j)
-#pragma unroll
-                        for (int gp = 0; gp < 2; ++gp) {
-                            half8 h;
-#pragma unroll
-                            for (int e = 0; e < 8; ++e) {
-                                const float x = acc[i][j][8 * gp + e];
-                                const f16 hi = (f16)x;
-                                h[e] = img == 0 ? hi : x3_lo(x, hi);
-                            }
-                            const uint4 hv = __builtin_bit_cast(uint4, h);
-                            const auto s0 = __builtin_amdgcn_permlane32_swap(hv.x, hv.z, false, false);
-                            const auto s1 = __builtin_amdgcn_permlane32_swap(hv.y, hv.w, false, false);
-                            const int c = 4 * j + 2 * gp + fh;
-                            *(uint4*)(slb + frow * 128 + ((c ^ (frow & 7)) << 4)) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
-                        }
-                    f16* ob = (f16*)ep.out + (size_t)(cm0 + wm * WTM + MS * i) * ep.ldc + img * ep.nlog + cn0 + wn * WTN + 8 * c16;
-                    uint4 v[4];
-                    slab_read4(slb, rr0, c16, v);
-#pragma unroll
-                    for (int it = 0; it < 4; ++it) st16<64>((uint4*)(ob + (size_t)(it * 8 + rr0) * ep.ldc), v[it]);
-                }
-        }
-        if (!more) break;
-        par = last ^ 1;
-        first = false;
     }
 }
 
@@ -1980,7 +1266,7 @@ hipError_t smem_attr_once(const void* fn, int smem, std::atomic<unsigned>& devs)
     return hipSuccess;
 }
 
-template <int EPI, int VAR = 262144>
+template <int EPI, int VAR = 0>
 hipError_t launch_x3s(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep, hipStream_t st,
                       int ldw = 0, bool coop = false) {
     constexpr int smem = 2 * 65536;                  // ring (2 x 64 KiB); + 32 KiB static wave slabs
@@ -2079,108 +1365,38 @@ hipError_t launch_t(const f16* A, const f16* W, int M_pad, int N_pad, int K, con
     return hipGetLastError();
 }
 
-// Tile configuration (selected per call; env RS_GEMM_CFG overrides for A/B runs):
-//   0: 256x256, 8 waves (2x4, 128x64 per wave), 2 stages (128 KiB LDS)
-//   1: 256x128, 8 waves (4x2,  64x64 per wave), 3 stages (144 KiB LDS)
-//   2: 128x128, 4 waves (2x2,  64x64 per wave), 2 stages ( 64 KiB LDS)
-//   3: 256x128, 8 waves (4x2,  64x64 per wave), 3 stages of BK=32 (72 KiB LDS: 2 blocks/CU)
-//   4: 256x256, 8 waves (2x4, 128x64 per wave), 3 stages of BK=32 (96 KiB LDS)
-//   5: 256x128, 4 waves (2x2, 128x64 per wave), 3 stages of BK=32 (72 KiB LDS: 2 blocks/CU)
-//   6: 256x128, 4 waves (2x2, 128x64 per wave), 2 stages of BK=32 (48 KiB LDS: 3 blocks/CU)
-int g_cfg = -1;
-
-int pick_cfg(int N_pad) {
-    if (g_cfg < 0) {
-        const char* e = getenv("RS_GEMM_CFG");
-        g_cfg = e ? atoi(e) : 100;
-    }
-    int c = g_cfg;
-    if (c == 100) c = (N_pad % 256 == 0) ? 0 : 1;
-    if ((c == 0 || c == 4 || c == 7) && N_pad % 256) c = 1;
-    return c;
-}
-
+// fp16-operand GEMMs (the fp16 precision mode, the K-concatenated fp16x3 form RS_X3S=0, the
+// last layer's query rows and the MLM head), the measured-best variant per epilogue:
+//   * bias / GELU fp16 outputs (kx = 1): the persistent kernel, younger wave half at s_setprio 1
+//     and one MFMA substep behind, wave-private epilogue slabs without the epilogue barrier for
+//     the bias epilogue (VAR 786432 | 1048576; +1.2 / +1.5 / +1.6-1.9 %, profiles/r1_session3_probes.txt);
+//   * the GELU three-part image of the K-concatenated fp16x3 form: the persistent kernel (VAR 4194304);
+//   * everything else (fp32 outputs, the residual epilogues, the decoder logsumexp): the pipelined
+//     256 x 256 (N % 256 == 0) or 256 x 128 kernel, 16x16x32 MFMA except the logsumexp epilogue
+//     (32x32x16), non-temporal stores for fp16 outputs (VAR 64).
+// Measured-slower alternatives (tile configurations 2-7, 32x32x16 in the pipelined kernel, the
+// unstaggered persistent schedules, direct residual stores, ...) are recorded in profiles/r1_*;
+// their code paths were removed in round 4.
 template <int EPI>
 hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep,
                       hipStream_t st, int tag) {
-    // Production variant: software-pipelined K loop (VAR 128) + non-temporal stores (VAR 64)
-    // for the epilogues selected by RS_GEMM_NT: "f16" (default: fp16 outputs stream past L2,
-    // keeping the A panels resident), "all", "none".
-    static const unsigned nt_mask = [] {
-        const char* v = getenv("RS_GEMM_NT");
-        const unsigned f16 = (1u << EPI_BIAS_F16) | (1u << EPI_GELU_F16);
-        if (v && !strcmp(v, "all")) return ~0u;
-        if (v && !strcmp(v, "none")) return 0u;
-        return f16;
-    }();
-    const int cfg = pick_cfg(N_pad);
-    // MFMA shape: 16x16x32 by default (RS_GEMM_MS=32 selects 32x32x16).  Same cycles per
-    // FLOP, but the chip holds a higher clock under the 16x16 loop on random data
-    // (MI355X_MICROARCH.md 'DVFS give-back' item 7): +5-8 % on the pipelined kernel
-    // (tools/gemm_bench.py, profiles/r1_gemm_ms16.txt) and -5..-7 % O-proj / FFN2 time end to
-    // end.  The persistent kernel keeps 32x32x16 (RS_GEMM_MS_PERSIST=16 to switch, 0: 16x16
-    // for K >= 2048 only): with 16x16 its QKV launches took +7 % end to end.  The decoder's
-    // logsumexp epilogue keeps 32x32x16.
-    static const int ms = getenv("RS_GEMM_MS") ? atoi(getenv("RS_GEMM_MS")) : 16;
-    static const int ms_p = getenv("RS_GEMM_MS_PERSIST") ? atoi(getenv("RS_GEMM_MS_PERSIST")) : 32;
-    // RS_GEMM_PERSIST=0 disables the persistent kernel (fp16-output epilogues, kx = 1)
-    static const int persist = getenv("RS_GEMM_PERSIST") ? atoi(getenv("RS_GEMM_PERSIST")) : 1;
-    // RS_GEMM_PRIO (default 1): the persistent kernel's younger wave half runs at s_setprio 1
-    // (+1-3 % per GEMM shape, tools/gemm_bench.py cfg 9/15, 11/16); RS_GEMM_STAGGER=1 (default):
-    // that half also runs one MFMA substep behind (cfg 17-20; +1.5 % end to end over the
-    // priority alone), 2: stagger without the priority (no gain), 0: priority only
-    static const int prio = getenv("RS_GEMM_PRIO") ? atoi(getenv("RS_GEMM_PRIO")) : 1;
-    static const int stag = getenv("RS_GEMM_STAGGER") ? atoi(getenv("RS_GEMM_STAGGER")) : (prio ? 1 : 0);
-    // RS_GEMM_PERSIST_X3 (default 1): BertIntermediate of the fp16x3 mode on the persistent
-    // kernel too (GELU output written as the three-part operand image)
-    static const int persist_x3 = getenv("RS_GEMM_PERSIST_X3") ? atoi(getenv("RS_GEMM_PERSIST_X3")) : 1;
+    const bool n256 = N_pad % 256 == 0;
     if constexpr (EPI == EPI_GELU_F16) {
-        if (persist && persist_x3 && cfg == 0 && ep.kx == 3)
-            return launch_persist<EPI, 786432 | 4194304>(A, W, M_pad, N_pad, K, ep, st);
+        if (n256 && ep.kx == 3) return launch_persist<EPI, 786432 | 4194304>(A, W, M_pad, N_pad, K, ep, st);
     }
     if constexpr (EPI == EPI_BIAS_F16 || EPI == EPI_GELU_F16) {
-        if (persist && cfg == 0 && (EPI == EPI_BIAS_F16 || ep.kx == 1)) {
-            if (ms_p == 16 || (ms_p == 0 && K >= 2048)) return launch_persist<EPI, 8192>(A, W, M_pad, N_pad, K, ep, st);
-            // RS_GEMM_SLAB (default 1): bias-epilogue launches with wave-private epilogue slabs
-            // and no epilogue barrier (+1.6-1.9 % per shape; the GELU epilogue measured -0.6 %)
-            static const int slab = getenv("RS_GEMM_SLAB") ? atoi(getenv("RS_GEMM_SLAB")) : 1;
+        if (n256 && (EPI == EPI_BIAS_F16 || ep.kx == 1)) {
             constexpr int SLAB = EPI == EPI_BIAS_F16 ? 1048576 : 0;
-            if (stag == 1)
-                return slab ? persist_tagged<EPI, 786432 | SLAB>(tag, A, W, M_pad, N_pad, K, ep, st)
-                            : persist_tagged<EPI, 786432>(tag, A, W, M_pad, N_pad, K, ep, st);
-            if (stag == 2) return persist_tagged<EPI, 524288>(tag, A, W, M_pad, N_pad, K, ep, st);
-            if (prio) return persist_tagged<EPI, 262144>(tag, A, W, M_pad, N_pad, K, ep, st);
-            return persist_tagged<EPI, 0>(tag, A, W, M_pad, N_pad, K, ep, st);
+            return persist_tagged<EPI, 786432 | SLAB>(tag, A, W, M_pad, N_pad, K, ep, st);
         }
-    }
-    if ((nt_mask >> EPI) & 1u) {
-        if constexpr (EPI != EPI_LSE) {
-            if (ms == 16 && cfg == 0) return launch_t<256, 256, 2, 4, 2, 64, EPI, 192 | 8192>(A, W, M_pad, N_pad, K, ep, st);
-            if (ms == 16 && cfg == 1) return launch_t<256, 128, 4, 2, 3, 64, EPI, 192 | 8192>(A, W, M_pad, N_pad, K, ep, st);
-        }
-        if (cfg == 0) return launch_t<256, 256, 2, 4, 2, 64, EPI, 192>(A, W, M_pad, N_pad, K, ep, st);
-        if (cfg == 1) return launch_t<256, 128, 4, 2, 3, 64, EPI, 192>(A, W, M_pad, N_pad, K, ep, st);
-    }
-    // RS_GEMM_RESEPI=direct: residual GEMMs store fp32 straight from the accumulators
-    static const int res_direct = [] {
-        const char* v = getenv("RS_GEMM_RESEPI");
-        return v && !strcmp(v, "direct") ? 1 : 0;
-    }();
-    if (EPI == EPI_RESLN_F32 && res_direct && cfg == 0)
-        return launch_t<256, 256, 2, 4, 2, 64, EPI, 160>(A, W, M_pad, N_pad, K, ep, st);
-    if constexpr (EPI != EPI_LSE) {
-        if (ms == 16 && cfg == 0) return launch_t<256, 256, 2, 4, 2, 64, EPI, 128 | 8192>(A, W, M_pad, N_pad, K, ep, st);
-        if (ms == 16 && cfg == 1) return launch_t<256, 128, 4, 2, 3, 64, EPI, 128 | 8192>(A, W, M_pad, N_pad, K, ep, st);
-    }
-    switch (cfg) {
-        case 0: return launch_t<256, 256, 2, 4, 2, 64, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
-        case 1: return launch_t<256, 128, 4, 2, 3, 64, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
-        case 3: return launch_t<256, 128, 4, 2, 3, 32, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
-        case 4: return launch_t<256, 256, 2, 4, 3, 32, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
-        case 5: return launch_t<256, 128, 2, 2, 3, 32, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
-        case 6: return launch_t<256, 128, 2, 2, 2, 32, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
-        case 7: return launch_t<256, 256, 2, 4, 4, 32, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
-        default: return launch_t<128, 128, 2, 2, 2, 64, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
+        if (n256) return launch_t<256, 256, 2, 4, 2, 64, EPI, 192 | 8192>(A, W, M_pad, N_pad, K, ep, st);
+        return launch_t<256, 128, 4, 2, 3, 64, EPI, 192 | 8192>(A, W, M_pad, N_pad, K, ep, st);
+    } else if constexpr (EPI == EPI_LSE) {
+        if (n256) return launch_t<256, 256, 2, 4, 2, 64, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
+        return launch_t<256, 128, 4, 2, 3, 64, EPI, 128>(A, W, M_pad, N_pad, K, ep, st);
+    } else {
+        if (n256) return launch_t<256, 256, 2, 4, 2, 64, EPI, 128 | 8192>(A, W, M_pad, N_pad, K, ep, st);
+        return launch_t<256, 128, 4, 2, 3, 64, EPI, 128 | 8192>(A, W, M_pad, N_pad, K, ep, st);
     }
 }
 
@@ -2197,27 +1413,15 @@ int gemm_lnres_workgroups(int N_pad) {
     return ntn > 0 ? cus / ntn * ntn : 0;
 }
 
-// Production split-operand fp16x3 GEMM: LDS-DMA by buffer_load ... lds (VAR 16) spread over the
-// MFMAs (VAR 4), younger wave half at s_setprio 1 (VAR 262144); tools/x3s_bench.py.
+// Production split-operand fp16x3 GEMM (gemm_x3s_kernel; tools/x3s_epi_probe.py).
 hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_pad, int N_pad, int K,
                            const EpiArgs& ep, hipStream_t st) {
     if (M_pad % 256 || N_pad % 256 || K % 32 || K < 64 || ldw < 2 * K || M_pad <= 0) return hipErrorInvalidValue;
     // the buffer descriptors address one 256-row panel: 32-bit byte offsets
     if ((long long)256 * ldw * 2 >= (1ll << 31) || (long long)256 * 2 * K * 2 >= (1ll << 31)) return hipErrorInvalidValue;
-    // 16x16x32 MFMA (default; +4-7 % per shape over 32x32x16, tools/x3s_bench.py);
-    // RS_X3S_MFMA=32 keeps the 32x32x16 form for A/B runs
-    static const bool mf32 = getenv("RS_X3S_MFMA") && !strcmp(getenv("RS_X3S_MFMA"), "32");
-    constexpr int V = 262144 | 16 | 4 | 128 | 512, V32 = 262144 | 16 | 4;
     switch (epi) {
-        case EPI_BIAS_F32:
-            return mf32 ? launch_x3s<EPI_BIAS_F32, V32>(A, W, M_pad, N_pad, K, ep, st, ldw)
-                        : launch_x3s<EPI_BIAS_F32, V>(A, W, M_pad, N_pad, K, ep, st, ldw);
-        case EPI_GELU_F16:
-            return mf32 ? launch_x3s<EPI_GELU_F16, V32>(A, W, M_pad, N_pad, K, ep, st, ldw)
-                        : launch_x3s<EPI_GELU_F16, V>(A, W, M_pad, N_pad, K, ep, st, ldw);
-        case EPI_BIAS_F16:
-            return mf32 ? launch_x3s<EPI_BIAS_F16, V32>(A, W, M_pad, N_pad, K, ep, st, ldw)
-                        : launch_x3s<EPI_BIAS_F16, V>(A, W, M_pad, N_pad, K, ep, st, ldw);
+        case EPI_BIAS_F32: return launch_x3s<EPI_BIAS_F32, 0>(A, W, M_pad, N_pad, K, ep, st, ldw);
+        case EPI_GELU_F16: return launch_x3s<EPI_GELU_F16, 0>(A, W, M_pad, N_pad, K, ep, st, ldw);
         case EPI_LNRES_IMG: {
             // Output columns permuted inside 32-column groups (VAR 16777216: 16-B epilogue loads,
             // +1.1 % end to end, profiles/r3p2_lnperm_ab.txt); VAR 67108864 is a name tag only (the
@@ -2233,7 +1437,7 @@ hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_p
             //       grid the occupancy does not admit.
             const char* g = getenv("RS_LNGANG");
             const bool xcd = g && !strcmp(g, "xcd");
-            constexpr int VL = V | 16777216;
+            constexpr int VL = 16777216;
             if (xcd) {
                 if (K > 1024) return launch_x3s<EPI_LNRES_IMG, VL | 67108864 | 134217728>(A, W, M_pad, N_pad, K, ep, st, ldw, true);
                 return launch_x3s<EPI_LNRES_IMG, VL | 134217728>(A, W, M_pad, N_pad, K, ep, st, ldw, true);
@@ -2270,191 +1474,46 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
     const f16* a = (const f16*)A;
     const f16* w = (const f16*)W;
     hipError_t e = hipErrorInvalidValue;
-#define RS_DBG(D)                                                                                     \
-    switch (cfg) {                                                                                    \
-        case 0: e = launch_t<256, 256, 2, 4, 2, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
-        case 1: e = launch_t<256, 128, 4, 2, 3, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
-        case 3: e = launch_t<256, 128, 4, 2, 3, 32, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
-        case 5: e = launch_t<256, 128, 2, 2, 3, 32, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
-        case 6: e = launch_t<256, 128, 2, 2, 2, 32, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
-        case 4: e = launch_t<256, 256, 2, 4, 3, 32, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
-        case 7: e = launch_t<256, 256, 2, 4, 4, 32, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
-        case 8: e = launch_t<256, 256, 2, 2, 2, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
-        default: e = launch_t<128, 128, 2, 2, 2, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;   \
-    }
-#define RS_DBG16(D)                                                                                   \
-    switch (cfg) {                                                                                    \
-        case 0: e = launch_t<256, 256, 2, 4, 2, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
-        case 1: e = launch_t<256, 128, 4, 2, 3, 64, EPI_BIAS_F16, D>(a, w, M, N, K, ep, st); break;    \
-        default: return -1;                                                                           \
-    }
     if (M % 256 || N % 256 || K % 64) return -1;
-    if (cfg == 33 || cfg == 34) {  // production x3s with W rows of 3K halfs (three-part weight image): 33 fp32, 34 GELU
+    if (cfg == 31 || cfg == 32) {  // split-operand fp16x3 (A [M, 2K], W [N, 2K] images): 31 GELU image, 32 fp32
+        // dbg: 0 production, 60 the ping-pong kernel (k_gemm_pp.hip); timing diagnostics of
+        // gemm_x3s_kernel (wrong results): 1 no K-loop staging, 2 no epilogue stores (20 / 52:
+        // the same, round-3 / round-4 probe numbering), 3 neither, 50 DMA never waited for (the
+        // next tile never waits for this tile's stores), 51 stores onto row panel 0 (no HBM write
+        // burst), 53 both
         ep.nlog = N;
-        if (cfg == 34) ep.ldc = 2 * N;
-        if (dbg == 1) e = launch_x3s<EPI_BIAS_F32, 262144>(a, w, M, N, K, ep, st, 3 * K);
-        else if (dbg == 2) e = launch_x3s<EPI_BIAS_F32, 262144 | 16>(a, w, M, N, K, ep, st, 3 * K);
-        else if (dbg == 3) e = launch_x3s<EPI_BIAS_F32, 262144 | 4>(a, w, M, N, K, ep, st, 3 * K);
-        else e = launch_gemm_x3s(cfg == 33 ? EPI_BIAS_F32 : EPI_GELU_F16, a, w, 3 * K, M, N, K, ep, st);
-        return e == hipSuccess ? 0 : -2;
-    }
-    if (cfg >= 30 && cfg <= 32) {  // split-operand fp16x3 (A [M, 2K], W [N, 2K] images): 30 fp16, 31 GELU image, 32 fp32
-        ep.nlog = N;
+        const int epi = cfg == 31 ? EPI_GELU_F16 : EPI_BIAS_F32;
         if (cfg == 31) ep.ldc = 2 * N;
-        if (cfg == 32 && dbg == 1) e = launch_x3s<EPI_BIAS_F32, 262144 | 1>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 2) e = launch_x3s<EPI_BIAS_F32, 262144 | 2>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 3) e = launch_x3s<EPI_BIAS_F32, 262144 | 3>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 4) e = launch_x3s<EPI_BIAS_F32, 0>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 5) e = launch_x3s<EPI_BIAS_F32, 262144 | 4>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 6) e = launch_x3s<EPI_BIAS_F32, 262144 | 4 | 2>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 7) e = launch_x3s<EPI_BIAS_F32, 262144 | 4 | 2 | 8>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 8) e = launch_x3s<EPI_BIAS_F32, 262144 | 2 | 8>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 9) e = launch_x3s<EPI_BIAS_F32, 262144 | 16>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 10) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 11) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 2>(a, w, M, N, K, ep, st);
-
-        else if (cfg == 32 && dbg == 12) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 32>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 13) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 32 | 3>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 14) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 3>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 16) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 17) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 128>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 18) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 3>(a, w, M, N, K, ep, st);
-        else if (cfg == 31 && dbg == 16) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 20) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 2>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 21) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 256>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 23) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 2 | 1024>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 24) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 2 | 2048>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 25) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 2 | 4096>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 26) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 8192>(a, w, M, N, K, ep, st);
-        else if (cfg == 31 && dbg == 26) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 8192>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 27) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 16384>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 28) e = launch_x3s<EPI_BIAS_F32, 16 | 4 | 128 | 512>(a, w, M, N, K, ep, st);
-        else if (cfg == 31 && dbg == 27) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 16384>(a, w, M, N, K, ep, st);
-        else if (cfg == 31 && dbg == 28) e = launch_x3s<EPI_GELU_F16, 16 | 4 | 128 | 512>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 29) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 128 | 512 | 32768>(a, w, M, N, K, ep, st);
-        else if (cfg == 31 && dbg == 29) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 128 | 512 | 32768>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 19) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4>(a, w, M, N, K, ep, st);
-        else if (cfg == 31 && dbg == 22) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512>(a, w, M, N, K, ep, st);
-        else if (cfg == 31 && dbg == 19) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4>(a, w, M, N, K, ep, st);
-        else if (cfg == 30 && dbg == 19) e = launch_x3s<EPI_BIAS_F16, 262144 | 16 | 4>(a, w, M, N, K, ep, st);
-        else if (cfg == 30 && dbg == 16) e = launch_x3s<EPI_BIAS_F16, 262144 | 16 | 4 | 128>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 15) e = launch_x3s<EPI_BIAS_F32, 262144>(a, w, M, N, K, ep, st);
-        // half-step stagger of the younger wave half (VAR 524288): 40 production + stagger,
-        // 41 without staging or epilogue, 42 without epilogue, 43 the unstaggered 'neither'
-        else if (cfg == 32 && dbg == 40) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 524288>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 41) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 524288 | 3>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 42) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 524288 | 2>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 43) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 3>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 44) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 524288 | 2097152>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 45) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 524288 | 2097152 | 2>(a, w, M, N, K, ep, st);
-        else if (cfg == 31 && dbg == 44) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 524288 | 2097152>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 46) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 2 | 8>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 47) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 524288 | 2 | 8>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 48) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 8388608>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 49) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 8388608 | 2>(a, w, M, N, K, ep, st);
-        else if (cfg == 31 && dbg == 48) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 8388608>(a, w, M, N, K, ep, st);
-        else if (cfg == 31 && dbg == 40) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 524288>(a, w, M, N, K, ep, st);
-        else if (cfg == 30 && dbg == 40) e = launch_x3s<EPI_BIAS_F16, 262144 | 16 | 4 | 128 | 512 | 524288>(a, w, M, N, K, ep, st);
-        // round 4 epilogue probes: 50 production + DMA never waited for (so the next tile's K loop
-        // never waits for this tile's stores), 51 stores aliased onto panel 0 (no HBM write burst),
-        // 52 production without the epilogue (GELU image)
-        else if (cfg == 32 && dbg == 50) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 8>(a, w, M, N, K, ep, st);
-        else if (cfg == 31 && dbg == 50) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 8>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 51) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 33554432>(a, w, M, N, K, ep, st);
-        else if (cfg == 31 && dbg == 51) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 33554432>(a, w, M, N, K, ep, st);
-        else if (cfg == 31 && dbg == 52) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 2>(a, w, M, N, K, ep, st);
-        else if (cfg == 32 && dbg == 53) e = launch_x3s<EPI_BIAS_F32, 262144 | 16 | 4 | 128 | 512 | 8 | 33554432>(a, w, M, N, K, ep, st);
-        else if (cfg == 31 && dbg == 53) e = launch_x3s<EPI_GELU_F16, 262144 | 16 | 4 | 128 | 512 | 8 | 33554432>(a, w, M, N, K, ep, st);
-        // dbg 60: the ping-pong kernel (k_gemm_pp.hip) on the same operands
-        else if ((cfg == 32 || cfg == 31) && dbg == 60)
-            e = launch_gemm_pp(cfg == 32 ? EPI_BIAS_F32 : EPI_GELU_F16, a, w, 2 * K, M, N, K, ep, st);
-        else {   // dbg 0: the production variant (launch_gemm_x3s)
-            const int epi = cfg == 30 ? EPI_BIAS_F16 : cfg == 31 ? EPI_GELU_F16 : EPI_BIAS_F32;
-            e = launch_gemm_x3s(epi, a, w, 2 * K, M, N, K, ep, st);
+#define RS_X3(VAR_)                                                                        \
+    (cfg == 31 ? launch_x3s<EPI_GELU_F16, VAR_>(a, w, M, N, K, ep, st) : launch_x3s<EPI_BIAS_F32, VAR_>(a, w, M, N, K, ep, st))
+        switch (dbg) {
+            case 0: e = launch_gemm_x3s(epi, a, w, 2 * K, M, N, K, ep, st); break;
+            case 60: e = launch_gemm_pp(epi, a, w, 2 * K, M, N, K, ep, st); break;
+            case 1: e = RS_X3(1); break;
+            case 2: case 20: case 52: e = RS_X3(2); break;
+            case 3: e = RS_X3(3); break;
+            case 50: e = RS_X3(8); break;
+            case 51: e = RS_X3(33554432); break;
+            case 53: e = RS_X3(8 | 33554432); break;
+            default: return -1;
         }
+#undef RS_X3
         return e == hipSuccess ? 0 : -2;
     }
-    if (cfg == 23 || cfg == 24) {  // + next tile's DMA issued before the epilogue math: 23 bias, 24 GELU
-        e = cfg == 23 ? launch_persist<EPI_BIAS_F16, 786432 | 1048576 | 2097152>(a, w, M, N, K, ep, st)
-                      : launch_persist<EPI_GELU_F16, 786432 | 1048576 | 2097152>(a, w, M, N, K, ep, st);
-        return e == hipSuccess ? 0 : -2;
+    // fp16 kernels: 9 / 11 persistent bias / GELU with the plain schedule (the bitwise reference
+    // of the production schedule), 21 / 18 the production persistent schedules, 0 (dbg 8384) the
+    // pipelined kernel with non-temporal stores
+    switch (cfg) {
+        case 9: e = launch_persist<EPI_BIAS_F16>(a, w, M, N, K, ep, st); break;
+        case 11: e = launch_persist<EPI_GELU_F16>(a, w, M, N, K, ep, st); break;
+        case 21: e = launch_persist<EPI_BIAS_F16, 786432 | 1048576>(a, w, M, N, K, ep, st); break;
+        case 18: e = launch_persist<EPI_GELU_F16, 262144 | 524288>(a, w, M, N, K, ep, st); break;
+        case 0:
+            if (dbg != 8384) return -1;
+            e = launch_t<256, 256, 2, 4, 2, 64, EPI_BIAS_F16, 8384>(a, w, M, N, K, ep, st);
+            break;
+        default: return -1;
     }
-    if (cfg == 21 || cfg == 22) {  // + private epilogue slabs, no epilogue barrier: 21 bias, 22 GELU
-        e = cfg == 21 ? launch_persist<EPI_BIAS_F16, 786432 | 1048576>(a, w, M, N, K, ep, st)
-                      : launch_persist<EPI_GELU_F16, 786432 | 1048576>(a, w, M, N, K, ep, st);
-        return e == hipSuccess ? 0 : -2;
-    }
-    if (cfg == 17 || cfg == 18) {  // persistent, prio + staggered younger half: 17 bias, 18 GELU
-        e = cfg == 17 ? launch_persist<EPI_BIAS_F16, 262144 | 524288>(a, w, M, N, K, ep, st)
-                      : launch_persist<EPI_GELU_F16, 262144 | 524288>(a, w, M, N, K, ep, st);
-        return e == hipSuccess ? 0 : -2;
-    }
-    if (cfg == 19 || cfg == 20) {  // persistent, staggered younger half without prio: 19 bias, 20 GELU
-        e = cfg == 19 ? launch_persist<EPI_BIAS_F16, 524288>(a, w, M, N, K, ep, st)
-                      : launch_persist<EPI_GELU_F16, 524288>(a, w, M, N, K, ep, st);
-        return e == hipSuccess ? 0 : -2;
-    }
-    if (cfg == 15 || cfg == 16) {  // persistent, younger wave half at s_setprio 1: 15 bias, 16 GELU
-        e = cfg == 15 ? launch_persist<EPI_BIAS_F16, 262144>(a, w, M, N, K, ep, st)
-                      : launch_persist<EPI_GELU_F16, 262144>(a, w, M, N, K, ep, st);
-        return e == hipSuccess ? 0 : -2;
-    }
-    if (cfg == 13 || cfg == 14) {  // persistent, padded (pre-swizzle) epilogue slab: 13 bias, 14 GELU
-        e = cfg == 13 ? launch_persist<EPI_BIAS_F16, 32768>(a, w, M, N, K, ep, st)
-                      : launch_persist<EPI_GELU_F16, 32768>(a, w, M, N, K, ep, st);
-        return e == hipSuccess ? 0 : -2;
-    }
-    if (cfg >= 9 && cfg <= 12) {   // persistent fp16-output kernel (11/12: GELU; 10/12: 16x16x32)
-        e = cfg == 9 ? launch_persist<EPI_BIAS_F16>(a, w, M, N, K, ep, st)
-          : cfg == 10 ? (dbg ? launch_persist<EPI_BIAS_F16, 8192 | 16384>(a, w, M, N, K, ep, st)
-                             : launch_persist<EPI_BIAS_F16, 8192>(a, w, M, N, K, ep, st))
-          : cfg == 11 ? launch_persist<EPI_GELU_F16>(a, w, M, N, K, ep, st)
-                      : (dbg ? launch_persist<EPI_GELU_F16, 8192 | 16384>(a, w, M, N, K, ep, st)
-                             : launch_persist<EPI_GELU_F16, 8192>(a, w, M, N, K, ep, st));
-        return e == hipSuccess ? 0 : -2;
-    }
-    switch (dbg) {
-        case 0: RS_DBG(0); break;
-        case 4: RS_DBG(4); break;
-        case 6: RS_DBG(6); break;
-        case 8: RS_DBG(8); break;
-        case 16: RS_DBG(16); break;
-        case 32: RS_DBG(32); break;
-        case 40: RS_DBG(40); break;
-        case 64: RS_DBG(64); break;
-        case 96: RS_DBG(96); break;
-        case 128: RS_DBG(128); break;
-        case 131: RS_DBG(131); break;
-        case 192: RS_DBG(192); break;
-        case 256: RS_DBG(256); break;
-        case 704: RS_DBG(704); break;
-        case 1216: RS_DBG(1216); break;
-        case 2240: RS_DBG(2240); break;
-        case 208: RS_DBG(208); break;
-        case 200: RS_DBG(200); break;
-        case 160: RS_DBG(160); break;
-        case 6336: RS_DBG(6336); break;
-        case 2242: RS_DBG(2242); break;
-        case 2243: RS_DBG(2243); break;
-        case 1218: RS_DBG(1218); break;
-        case 1219: RS_DBG(1219); break;
-        case 194: RS_DBG(194); break;
-        case 706: RS_DBG(706); break;
-        case 320: RS_DBG(320); break;
-        case 259: RS_DBG(259); break;
-        case 1: RS_DBG(1); break;
-        case 2: RS_DBG(2); break;
-        // 16x16x32 MFMA (BK = 64 configurations only): pipelined / + nt stores / neither
-        case 8320: RS_DBG16(8320); break;
-        case 8384: RS_DBG16(8384); break;
-        case 8323: RS_DBG16(8323); break;
-        case 8322: RS_DBG16(8322); break;
-        case 8321: RS_DBG16(8321); break;
-        case 270464: RS_DBG16(270464); break;     // 8320 + younger half at s_setprio 1
-        default: RS_DBG(3); break;
-    }
-#undef RS_DBG
-#undef RS_DBG16
     return e == hipSuccess ? 0 : -2;
 }
 

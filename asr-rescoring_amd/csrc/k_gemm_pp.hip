@@ -66,6 +66,7 @@ gemm_pp_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int 
     const int stride = 2 * G;
     auto count = [&](int f) { return f < n_tiles ? (n_tiles - f + stride - 1) / stride : 0; };
     const int T0 = count(2 * wg), T1 = count(2 * wg + 1);
+    if (T0 == 0) return;                                // (the launch sizes the grid so this never happens)
     const int Tm = h ? T1 : T0;
     const int pre = h ? D : 0;
     const int total = max(T0 * P, T1 > 0 ? D + T1 * P : 0);

@@ -77,14 +77,13 @@ def _split2(x):
     return torch.cat([hi, ((x - hi.float()) * 64.0).half()], dim=1).contiguous()
 
 
-@pytest.mark.parametrize("dbg,M", [(0, 1024), (0, 40960), (19, 40960)])
+@pytest.mark.parametrize("dbg,M", [(0, 1024), (0, 40960), (60, 1024), (60, 40960)])
 @pytest.mark.parametrize("name,N,K,gelu", SHAPES)
 def test_x3s_vs_torch_fp32(gemm, name, N, K, gelu, dbg, M):
-    """Split-operand fp16x3 GEMM (gemm_x3s_kernel through cfg 31/32 of rs_debug_gemm; dbg 0 =
-    the production 16x16x32 form, 19 = the 32x32x16 form): fp32 output and the two-part GELU
-    image vs an fp32 torch matmul, at fp32-level accuracy (3 fp16 products; measured ~2e-6 of
-    max |C|).  M = 40960 gives every persistent workgroup several tiles (tile transitions,
-    the last tile of each workgroup)."""
+    """Split-operand fp16x3 GEMM (cfg 31/32 of rs_debug_gemm; dbg 0 = gemm_x3s_kernel, 60 = the
+    ping-pong kernel): fp32 output and the two-part GELU image vs an fp32 torch matmul, at
+    fp32-level accuracy (3 fp16 products; measured ~2e-6 of max |C|).  M = 40960 gives every
+    persistent workgroup several tiles (tile transitions, the last tile of each workgroup)."""
     g = torch.Generator(device="cuda").manual_seed(11)
     A = torch.randn(M, K, device="cuda", generator=g)
     W = torch.randn(N, K, device="cuda", generator=g) * 0.05
