@@ -141,7 +141,7 @@ hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_p
 // the same with the epilogue overlapped by the other half of the workgroup (k_gemm_pp.hip):
 // EPI_BIAS_F32 or EPI_GELU_F16, K % 64 == 0
 hipError_t launch_gemm_pp(int epi, const f16* A, const f16* W, int ldw, int M_pad, int N_pad, int K, const EpiArgs& ep,
-                          hipStream_t st);
+                          hipStream_t st, int dv = 0);
 int gemm_row_align();   // M padding granularity required by launch_gemm
 int gemm_lnres_workgroups(int N_pad);   // grid of the fused residual + LayerNorm GEMM (whole gangs)
 

@@ -1489,6 +1489,11 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         switch (dbg) {
             case 0: e = launch_gemm_x3s(epi, a, w, 2 * K, M, N, K, ep, st); break;
             case 60: e = launch_gemm_pp(epi, a, w, 2 * K, M, N, K, ep, st); break;
+            // ping-pong timing diagnostics (fp32 output): 61 no epilogue stores, 62 halves in
+            // phase, 63 both, 64 no W loads, 65 no W loads + no stores, 73 no loads at all + no stores
+            case 61: case 62: case 63: case 64: case 65: case 73:
+                e = launch_gemm_pp(epi, a, w, 2 * K, M, N, K, ep, st, dbg - 60);
+                break;
             case 1: e = RS_X3(1); break;
             case 2: case 20: case 52: e = RS_X3(2); break;
             case 3: e = RS_X3(3); break;

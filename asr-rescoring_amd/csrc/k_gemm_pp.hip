@@ -39,7 +39,9 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int PP_E = 4;            // epilogue intervals per tile
 
-template <int EPI>
+// DV: timing diagnostics (wrong results; rs_debug_gemm dbg 61..): 1 no epilogue stores, 2 halves
+// in phase (D = 0), 4 no W loads (stale W registers), 8 no A DMA (stale LDS)
+template <int EPI, int DV = 0>
 __global__ void __launch_bounds__(512)
 gemm_pp_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int ldw, int n_tiles_n, int n_tiles,
                EpiArgs ep) {
@@ -57,7 +59,7 @@ gemm_pp_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int 
     const int r16 = lane & 15, q4 = lane >> 4;
     const int nk = K / BK;
     const int P = nk + E;                               // intervals per tile (nk even: P even)
-    const int D = (P / 2) & ~1;                         // half 1's lag (even: W register parity)
+    const int D = (DV & 2) ? 0 : (P / 2) & ~1;          // half 1's lag (even: W register parity)
 
     // ---- tile sequence of this half: grouped-order indices 2 wg + h, + 2 G, ... -----------
     const int G = gridDim.x, bid = blockIdx.x;
@@ -101,6 +103,7 @@ gemm_pp_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int 
         rsW = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (size_t)n0 * ldw), (short)0, 256 * ldw * 2, 0x00020000);
     };
     auto piece = [&](int buf, int k0, int p) {
+        if constexpr ((DV & 8) != 0) return;
         auto* dst = (__attribute__((address_space(3))) void*)(smem + ring_off + buf * STAGE + (p & 1) * PART +
                                                                (wn + 4 * (p >> 1)) * 1024);
         const int so = soffA(p) + k0 * 2;             // (a call in the builtin's argument list
@@ -154,8 +157,10 @@ gemm_pp_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int 
             if (ib < 4) {
                 __builtin_amdgcn_sched_barrier(0);
                 if (a_next) piece(nbuf, k0n, ib);
-                wnext[ib][0] = __builtin_amdgcn_raw_buffer_load_b128(rsW, voffW, soffW(ib, 0) + k0n * 2, 0);
-                wnext[ib][1] = __builtin_amdgcn_raw_buffer_load_b128(rsW, voffW, soffW(ib, 1) + k0n * 2, 0);
+                if constexpr ((DV & 4) == 0) {
+                    wnext[ib][0] = __builtin_amdgcn_raw_buffer_load_b128(rsW, voffW, soffW(ib, 0) + k0n * 2, 0);
+                    wnext[ib][1] = __builtin_amdgcn_raw_buffer_load_b128(rsW, voffW, soffW(ib, 1) + k0n * 2, 0);
+                }
                 __builtin_amdgcn_sched_barrier(0);
             }
         }
@@ -168,6 +173,13 @@ gemm_pp_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int 
     const int rr0 = lane >> 3, c16 = lane & 7;
     auto epi_chunk = [&](auto ec, int cm0, int cn0) {
         constexpr int e = decltype(ec)::value;          // compile-time: acc16 stays in registers
+        if constexpr ((DV & 1) != 0) {
+#pragma unroll
+            for (int a = 0; a < 2; ++a)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) asm volatile("" ::"v"(acc16[2 * e + a][j]));
+            return;
+        }
         if (e == 0) {
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
@@ -303,7 +315,7 @@ int n_cus_pp() {
     return n;
 }
 
-template <int EPI>
+template <int EPI, int DV = 0>
 hipError_t launch_pp(const f16* A, const f16* W, int ldw, int M_pad, int N_pad, int K, const EpiArgs& ep, hipStream_t st) {
     constexpr int smem = 4 * 16384;                     // A rings (2 halves x 2 stages); + 32 KiB slabs
     if (K % 64 || K < 64 || M_pad % 256 || N_pad % 256 || ldw < 2 * K) return hipErrorInvalidValue;
@@ -313,7 +325,7 @@ hipError_t launch_pp(const f16* A, const f16* W, int ldw, int M_pad, int N_pad, 
     if (hipError_t e = hipGetDevice(&dev)) return e;
     const unsigned bit = 1u << (dev & 31);
     if (!(attr_devs.load(std::memory_order_acquire) & bit)) {
-        if (hipError_t e = hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI>, hipFuncAttributeMaxDynamicSharedMemorySize, smem))
+        if (hipError_t e = hipFuncSetAttribute((const void*)gemm_pp_kernel<EPI, DV>, hipFuncAttributeMaxDynamicSharedMemorySize, smem))
             return e;
         attr_devs.fetch_or(bit, std::memory_order_release);
     }
@@ -323,7 +335,7 @@ hipError_t launch_pp(const f16* A, const f16* W, int ldw, int M_pad, int N_pad, 
     static const int gm_env = getenv("RS_PP_GROUP_M") ? atoi(getenv("RS_PP_GROUP_M")) : 0;
     EpiArgs e2 = ep;
     e2.group_m = gm_env > 0 ? gm_env : 16;              // 128-row panels per group
-    hipLaunchKernelGGL((gemm_pp_kernel<EPI>), dim3(grid), dim3(512), smem, st, A, W, K, ldw, ntn, n_tiles, e2);
+    hipLaunchKernelGGL((gemm_pp_kernel<EPI, DV>), dim3(grid), dim3(512), smem, st, A, W, K, ldw, ntn, n_tiles, e2);
     return hipGetLastError();
 }
 
@@ -332,7 +344,18 @@ hipError_t launch_pp(const f16* A, const f16* W, int ldw, int M_pad, int N_pad, 
 // Split-operand GEMM with the epilogue overlapped (see top): EPI_BIAS_F32 or EPI_GELU_F16; the
 // same operands and contract as launch_gemm_x3s.
 hipError_t launch_gemm_pp(int epi, const f16* A, const f16* W, int ldw, int M_pad, int N_pad, int K, const EpiArgs& ep,
-                          hipStream_t st) {
+                          hipStream_t st, int dv) {
+    if (epi == EPI_BIAS_F32) {
+        switch (dv) {
+            case 1: return launch_pp<EPI_BIAS_F32, 1>(A, W, ldw, M_pad, N_pad, K, ep, st);
+            case 2: return launch_pp<EPI_BIAS_F32, 2>(A, W, ldw, M_pad, N_pad, K, ep, st);
+            case 3: return launch_pp<EPI_BIAS_F32, 3>(A, W, ldw, M_pad, N_pad, K, ep, st);
+            case 4: return launch_pp<EPI_BIAS_F32, 4>(A, W, ldw, M_pad, N_pad, K, ep, st);
+            case 5: return launch_pp<EPI_BIAS_F32, 5>(A, W, ldw, M_pad, N_pad, K, ep, st);
+            case 13: return launch_pp<EPI_BIAS_F32, 13>(A, W, ldw, M_pad, N_pad, K, ep, st);
+            default: break;
+        }
+    }
     switch (epi) {
         case EPI_BIAS_F32: return launch_pp<EPI_BIAS_F32>(A, W, ldw, M_pad, N_pad, K, ep, st);
         case EPI_GELU_F16: return launch_pp<EPI_GELU_F16>(A, W, ldw, M_pad, N_pad, K, ep, st);

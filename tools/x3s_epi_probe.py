@@ -32,7 +32,10 @@ def main():
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev).manual_seed(0)
     st = torch.cuda.current_stream().cuda_stream
-    for N, K in ((2304, 768), (3072, 768), (768, 3072)):
+    shapes = ((2304, 768), (3072, 768), (768, 3072))
+    if os.environ.get("SHAPES"):
+        shapes = [tuple(int(v) for v in x.split("x")) for x in os.environ["SHAPES"].split(",")]
+    for N, K in shapes:
         A2 = torch.randn(M, 2 * K, device=dev, generator=g).half()
         W2 = (torch.randn(N, 2 * K, device=dev, generator=g) * 0.05).half()
         b = torch.randn(N, device=dev, generator=g) * 0.1
@@ -41,8 +44,14 @@ def main():
         fl = 3 * 2.0 * M * N * K
         var = {"f32": (32, out32, {"prod": 0, "pp": 60, "nowait": 50, "alias": 51, "nw+al": 53, "noepi": 20}),
                "gelu2": (31, img, {"prod": 0, "pp": 60, "nowait": 50, "alias": 51, "nw+al": 53, "noepi": 52})}
+        if os.environ.get("PROBE") == "pp":
+            # the ping-pong kernel's costs (fp32 output): without stores, halves in phase, without
+            # W loads, with no loads at all; against gemm_x3s_kernel's no-epilogue / bare loop
+            var = {"f32": (32, out32, {"x3s": 0, "x3s-noepi": 20, "x3s-bare": 3, "pp": 60, "pp-noepi": 61,
+                                       "pp-inphase": 62, "pp-noepi-inphase": 63, "pp-noW": 64,
+                                       "pp-noW-noepi": 65, "pp-bare": 73})}
         # the ping-pong kernel is bitwise equal to the production kernel (same MFMA order)
-        for cfg, o in ((32, out32), (31, img)):
+        for cfg, o in ((32, out32), (31, img)) if os.environ.get("PROBE") != "pp" else ():
             o2 = torch.empty_like(o)
             assert fn(cfg, 0, A2.data_ptr(), W2.data_ptr(), b.data_ptr(), o.data_ptr(), M, N, K, st) == 0
             assert fn(cfg, 60, A2.data_ptr(), W2.data_ptr(), b.data_ptr(), o2.data_ptr(), M, N, K, st) == 0
