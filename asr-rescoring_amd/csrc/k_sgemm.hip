@@ -337,6 +337,173 @@ sgemm_pipe_kernel(const float* __restrict__ A, int lda, const float* __restrict_
         }
 }
 
+// Direct-to-register form for the ~1k-token GEMMs (cfg 11): a 64×64 output tile per workgroup of
+// 4 waves, each wave computing the whole 64×64 tile over every fourth K-step of the workgroup's K
+// range (K-step t goes to wave t mod 4), with its operands loaded from global memory straight
+// into the MFMA fragment registers: no LDS staging and no barrier in the K loop, and the next
+// K-step's fragments in flight while this one's 64 MFMAs run.  The four partial tiles meet in
+// LDS at the end and are summed in wave order (fixed: bitwise reproducible).  A 1.1k-token GEMM
+// has 18 × 12..48 such tiles — one to four rounds over 256 CUs with every SIMD busy, where the
+// 128×128 tile leaves 54 tiles for 256 CUs at N = 768 and needs a split-K workspace pass.
+// Fragment registers of a lane (c = lane & 31, h = lane >> 5), K-step k0, MFMA step kk:
+//   KC operand: row 32t + c of row tile t, k = k0 + 16h + kk — 64 contiguous bytes (4 × 16 B);
+//   MC operand: rows 2c and 2c + 1, k = k0 + 16h + kk — one 8-B load per k-row; row tile t takes
+//               row 2c + t (the permutation is undone where the partial tile goes to LDS).
+template <bool KC>
+struct SgDirect {
+    static constexpr unsigned kOob = 0x7FFFFFF0u;     // past the descriptor's extent: loads return 0
+    __amdgpu_buffer_rsrc_t rs;
+    unsigned voff[2];
+    int ld;
+
+    __device__ void init(const float* src, int ld_, int rows, int row0, int lane) {
+        ld = ld_;
+        rs = sg_rsrc(src, kOob);
+        const int c = lane & 31, h = lane >> 5;
+        if (KC) {
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                const int r = row0 + 32 * t + c;
+                voff[t] = r < rows ? (unsigned)((r * ld + 16 * h) * 4) : kOob;
+            }
+        } else {
+            const int r = row0 + 2 * c;                   // rows % 4 == 0 (host-checked): r + 1 too
+            voff[0] = r < rows ? (unsigned)((16 * h * ld + r) * 4) : kOob;
+            voff[1] = 0;
+        }
+    }
+    __device__ static int row(int t, int c) { return KC ? 32 * t + c : 2 * c + t; }
+    // f[t][kk] = operand(row(t, c), k0 + 16h + kk); k >= ke reads as 0 (only the tail step checks)
+    __device__ __forceinline__ void load(float (&f)[2][16], int k0, int ke, int h) const {
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        const bool full = k0 + 32 <= ke;                  // wave-uniform
+        if (KC) {
+            const int so = k0 * 4;
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    unsigned vo = voff[t] + 16 * q;
+                    if (!full) vo = k0 + 16 * h + 4 * q < ke ? vo : kOob;
+                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0);
+                    f[t][4 * q] = __builtin_bit_cast(float, v.x);
+                    f[t][4 * q + 1] = __builtin_bit_cast(float, v.y);
+                    f[t][4 * q + 2] = __builtin_bit_cast(float, v.z);
+                    f[t][4 * q + 3] = __builtin_bit_cast(float, v.w);
+                }
+        } else {
+#pragma unroll
+            for (int kk = 0; kk < 16; ++kk) {
+                const int so = (k0 + kk) * ld * 4;
+                unsigned vo = voff[0];
+                if (!full) vo = k0 + 16 * h + kk < ke ? vo : kOob;
+                const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, 0);
+                f[0][kk] = __builtin_bit_cast(float, v.x);
+                f[1][kk] = __builtin_bit_cast(float, v.y);
+            }
+        }
+    }
+};
+
+constexpr int kD64Pitch = 72;                            // LDS row pitch (floats) of a partial tile
+constexpr int kD64Smem = 4 * 64 * kD64Pitch * 4;         // 72 KiB: two workgroups per CU
+
+template <bool AKC, bool BKC>
+__global__ void __launch_bounds__(256, 2)
+sgemm_d64_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb, float* __restrict__ C,
+                 int ldc, int M, int N, int K, int kc, int accum, float* __restrict__ ws) {
+    extern __shared__ __attribute__((aligned(16))) float part[];          // [wave][64 rows][kD64Pitch]
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int tm, tn, z;
+    sg_tile((M + 63) / 64, (N + 63) / 64, tm, tn, z);
+    const int m0 = tm * 64, n0 = tn * 64;
+    const int kb = z * kc, ke = min(K, kb + kc);
+    const int h = lane >> 5, c = lane & 31;
+    SgDirect<AKC> oa;
+    SgDirect<BKC> ob;
+    oa.init(A, lda, M, m0, lane);
+    ob.init(B, ldb, N, n0, lane);
+
+    f32x16_t acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+    auto mm = [&](const float (&xa)[2][16], const float (&xb)[2][16]) {
+#pragma unroll
+        for (int kk = 0; kk < 16; ++kk)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[i][kk], xb[j][kk], acc[i][j], 0, 0, 0);
+    };
+    const int nt = (ke - kb + 31) / 32;                   // the workgroup's K-steps
+    float fa[2][16], fb[2][16], ga[2][16], gb[2][16];
+    if (wave < nt) {
+        oa.load(fa, kb + 32 * wave, ke, h);
+        ob.load(fb, kb + 32 * wave, ke, h);
+    }
+    // two K-steps per trip, the register sets swapping roles: (f) = step t, (g) = step t + 4
+    for (int t = wave; t < nt; t += 8) {
+        if (t + 4 < nt) {
+            oa.load(ga, kb + 32 * (t + 4), ke, h);
+            ob.load(gb, kb + 32 * (t + 4), ke, h);
+        }
+        mm(fa, fb);
+        if (t + 4 >= nt) break;
+        if (t + 8 < nt) {
+            oa.load(fa, kb + 32 * (t + 8), ke, h);
+            ob.load(fb, kb + 32 * (t + 8), ke, h);
+        }
+        mm(ga, gb);
+    }
+
+    // this wave's partial tile into LDS in (row, column) order
+    // D map of the 32x32 forms: column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+    float* pw = part + wave * 64 * kD64Pitch;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+                pw[SgDirect<AKC>::row(i, (r & 3) + 8 * (r >> 2) + 4 * h) * kD64Pitch + SgDirect<BKC>::row(j, c)] =
+                    acc[i][j][r];
+    __syncthreads();
+    // wave w closes rows 16w .. 16w + 15: the four partials summed in wave order, 16 columns a lane
+    const int ml = 16 * wave + (lane >> 2), cl = (lane & 3) * 16;
+    const int row = m0 + ml;
+    if (row >= M) return;
+    float* P = ws ? ws + (size_t)z * M * N : nullptr;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int col = n0 + cl + 4 * q;
+        if (col >= N) break;                              // N % 4 == 0: whole float4s
+        const int o = ml * kD64Pitch + cl + 4 * q;
+        float4 s = *(const float4*)(part + o);
+#pragma unroll
+        for (int p = 1; p < 4; ++p) {
+            const float4 v = *(const float4*)(part + p * 64 * kD64Pitch + o);
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+        if (P) {
+            *(float4*)(P + (size_t)row * N + col) = s;
+        } else {
+            float4* d = (float4*)(C + (size_t)row * ldc + col);
+            if (accum) {
+                const float4 v = *d;
+                s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+            }
+            *d = s;
+        }
+    }
+}
+
 // Stream-K form of the 128×128 kernel (the default): a persistent grid of G workgroups (two
 // per CU) first takes dp whole tiles each (round r: tile r·G + d), then splits the remaining
 // tiles' K-steps evenly — workgroup d takes iterations [d·I/G, (d+1)·I/G) of the flattened
@@ -546,13 +713,14 @@ sgemm_splitk_sum_kernel(const float* __restrict__ ws, int splits, int M, int N, 
 // resident at once), 2 = 256×128×32 (8 waves of 64×64, 1 per CU; half the operand bytes per
 // FLOP of a 128×128 tile on the A side).
 struct SgCfg { int bm, bn, bk, occ; };
-constexpr int kSgNCfg = 11;
+constexpr int kSgNCfg = 12;
 constexpr SgCfg kSgCfg[kSgNCfg] = {{128, 128, 32, 2}, {128, 128, 16, 4}, {256, 128, 32, 1},
                                    {128, 128, 16, 3}, {128, 128, 32, 1},    // 3, 4: sgemm_pipe_kernel
                                    {128, 64, 32, 2},  {128, 64, 32, 3},     // 5, 6: 4 waves of 32×64
                                    {64, 64, 32, 4},   {64, 64, 32, 6},      // 7, 8: 2 waves of 32×64
                                    {192, 128, 32, 2},                       // 9: 4 waves of 96×64
-                                   {256, 256, 32, 1}};                      // 10: 8 waves of 128×64
+                                   {256, 256, 32, 1},                       // 10: 8 waves of 128×64
+                                   {64, 64, 32, 2}};                        // 11: sgemm_d64_kernel
 
 // Modelled time (µs) of one configuration at a split count: dispatch rounds × (K-steps per
 // workgroup × the time a CU takes per K-step with its resident workgroups + a per-round
@@ -574,11 +742,13 @@ double sg_model(int cfg, int M, int N, int K, int sp, bool mcmc, int cus_) {
     const int steps = (K + g.bk - 1) / g.bk, per = (steps + sp - 1) / sp, spr = (steps + per - 1) / per;
     const double vol = (double)g.bm * g.bn * g.bk / (128.0 * 128.0 * 32.0);
     double t_one = 2.14 * vol, t_full = 3.74 * vol * g.occ / 2.0;
+    int kper = per;                                    // K-steps in a workgroup's critical path
     if (cfg == 9) { t_one = 3.43; t_full = 6.4; }
+    else if (cfg == 11) { t_one = 1.9; t_full = 3.8; kper = (per + 3) / 4; }   // 4 waves split the K-steps
     else if (mcmc) { t_one *= 1.1; t_full *= 1.1; }
     const long long wgs = tiles * spr, cus = cus_;
-    double t = wgs <= cus ? per * t_one + 5.44
-                          : (double)((wgs + cus * g.occ - 1) / (cus * g.occ)) * (per * t_full + 5.44);
+    double t = wgs <= cus ? kper * t_one + 5.44
+                          : (double)((wgs + cus * g.occ - 1) / (cus * g.occ)) * (kper * t_full + 5.44);
     if (spr > 1) t += 4.24 + (2.0 * spr + 1.0) * M * N * 4.0 * 0.127e-6;
     return t;
 }
@@ -612,7 +782,7 @@ int sg_splits(int cfg, int M, int N, int K, int* kc, bool mcmc, int cus) {
 
 // The tile configuration: 128×128 (cfg 0) or 192×128 (cfg 9), whichever the model times lower
 // at its best split (192×128 wins where the 128×128 grid leaves a half-empty last round, e.g.
-// 5300 × 2304).  RS_SGEMM_CFG=0..9 forces a configuration (A/B knob).  The choice depends on
+// 5300 × 2304).  RS_SGEMM_CFG=0..11 forces a configuration (A/B knob).  The choice depends on
 // the shape and the device's CU count only, so a shape's results stay bitwise reproducible on a
 // given device model.
 int sg_pick(int M, int N, int K, bool mcmc, int cus) {
@@ -771,7 +941,24 @@ static hipError_t sg_run(int cfg, int M, int N, int K, const float* A, int lda, 
     else if (cfg == 7) SG_FORMS(sgemm_dma_kernel, 64, 64, 32, 32, 4);
     else if (cfg == 8) SG_FORMS(sgemm_dma_kernel, 64, 64, 32, 32, 6);
     else if (cfg == 9) SG_FORMS(sgemm_dma_kernel, 192, 128, 96, 32, 2);
-    else SG_FORMS(sgemm_dma_kernel, 256, 256, 128, 32, 1);
+    else if (cfg == 10) SG_FORMS(sgemm_dma_kernel, 256, 256, 128, 32, 1);
+    else {
+        static const hipError_t attr = [] {
+            for (const void* f : {(const void*)sgemm_d64_kernel<true, true>, (const void*)sgemm_d64_kernel<true, false>,
+                                  (const void*)sgemm_d64_kernel<false, true>, (const void*)sgemm_d64_kernel<false, false>})
+                if (hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, kD64Smem)) return e;
+            return hipSuccess;
+        }();
+        if (attr != hipSuccess) return attr;
+#define D64_LAUNCH(AK, BK_)                                                                                    \
+    hipLaunchKernelGGL((sgemm_d64_kernel<AK, BK_>), grid, dim3(256), kD64Smem, s, A, lda, B, ldb, C, ldc, M, N, K, kc, \
+                       accum, P)
+        if (a_kc && b_kc) D64_LAUNCH(true, true);
+        else if (a_kc) D64_LAUNCH(true, false);
+        else if (b_kc) D64_LAUNCH(false, true);
+        else D64_LAUNCH(false, false);
+#undef D64_LAUNCH
+    }
 #undef SG_FORMS
 #undef SG_LAUNCH
     hipError_t e = hipGetLastError();

@@ -92,6 +92,39 @@ def test_c3_shape_pll_rows_and_rerank(w_base, oracle_model):
     assert np.array_equal(arg_g, arg_h) and bw_g == bw_h and cer_g == cer_h
 
 
+def test_c3_finetuned_lm_moves_the_pick(w_base):
+    """The reference's pipeline on the C3 shape: MLM fine-tuning on in-domain text
+    (MLM_PLL/main.py:117-161; here the utterances' reference sentences, the native trainer, 300
+    deterministic steps) -> scoring with that checkpoint (:184-186) -> fusion (rescore.py:25-58).
+    With this LM the best weight is > 0 and the reranked CER is below the AM-only CER, so the
+    101-weight argmax equality between the oracle's lm and the HIP lm is checked where the LM
+    actually moves the pick."""
+    from asr_rescoring_amd.scorer import PLLScorer
+    from asr_rescoring_amd import rerank
+    from asr_rescoring_amd.train import finetune_mlm_on_texts
+    from oracle import rescore_ref as RR
+    from oracle.bert_ref import TorchBert, pll_reference_pattern
+    nb = D.synthetic_nbest(6, 50, seed=31, hard=True)
+    w_ft, losses = finetune_mlm_on_texts(w_base, nb.refs, BERT_BASE, steps=300, lr=1e-4, seed=0, device=0)
+    assert np.isfinite(losses).all()
+    s = PLLScorer(w_ft, BERT_BASE, device=0, max_rows=65536)
+    try:
+        pll = s.score_nbest(nb.tokens, nb.hyp_off).cpu().numpy()
+    finally:
+        s.close()
+    _, ref_pll = pll_reference_pattern(TorchBert(w_ft, BERT_BASE), nb.tokens, nb.hyp_off, batch_size=64,
+                                       full_head=False)
+    assert rel_err(pll, ref_pll).max() < REL
+    hyps, N = _oracle_hyps(nb)
+    am = nb.am.reshape(nb.n_utt, N)
+    bw_o, cer_o, arg_o = RR.find_best_weight(am, ref_pll.reshape(nb.n_utt, N), hyps, nb.refs, n_best=N)
+    bw_h, cer_h, arg_h = RR.find_best_weight(am, pll.reshape(nb.n_utt, N), hyps, nb.refs, n_best=N)
+    assert np.array_equal(arg_o, arg_h) and bw_o == bw_h and cer_o == cer_h
+    bw_g, cer_g, arg_g, cers = rerank.find_best_weight(nb, pll, n_best=N)
+    assert np.array_equal(arg_g, arg_h) and bw_g == bw_h and cer_g == cer_h
+    assert bw_h > 0 and cer_h < cers[0], (bw_h, cer_h, cers[0])
+
+
 def test_c2_shape_cls(w_base, oracle_model):
     import torch
     from asr_rescoring_amd.scorer import RescoreBertHIP
