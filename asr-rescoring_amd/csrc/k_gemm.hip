@@ -21,6 +21,7 @@
 //  * Bijective XCD-aware block remap: consecutive tiles (same A row panel) share an XCD L2.
 #include "common.h"
 #include "gemm_dev.h"
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <type_traits>
@@ -803,14 +804,6 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         t = (int)*(const unsigned*)(slabs + 2048);
     }
     if ((unsigned)t >= (unsigned)n_tiles) return;
-    if constexpr ((VAR & 268435456) != 0) {
-        // VAR 268435456 (timing diagnostic): every other workgroup of an XCD starts ep.diag µs
-        // late, so the chip's epilogues (and their HBM write bursts) fall into two phases
-        if ((blockIdx.x >> 3) & 1) {
-            const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-            while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < (long long)ep.diag * 100) __builtin_amdgcn_s_sleep(8);
-        }
-    }
     // the younger wave half (waves 4-7, one per SIMD beside an older partner) at s_setprio 1
     // (MI355X_MICROARCH 'Two waves per SIMD' item 4)
     if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
@@ -1508,11 +1501,6 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
             case 50: e = RS_X3(8); break;
             case 51: e = RS_X3(33554432); break;
             case 53: e = RS_X3(8 | 33554432); break;
-            // desync probe: odd workgroups of each XCD start 10 (dbg - 70) µs late
-            case 71: case 72: case 73: case 74: case 75: case 76:
-                ep.diag = 10 * (dbg - 70);
-                e = RS_X3(268435456);
-                break;
             default: return -1;
         }
 #undef RS_X3

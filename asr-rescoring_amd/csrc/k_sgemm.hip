@@ -12,7 +12,8 @@
 //   wgrad    dW = dYᵀ· X    A = dY (MC)   B = X  (MC)
 //
 // Tiles (by shape, sg_pick's time model): 128×128 (4 waves of 64×64) or 192×128 (4 waves of
-// 96×64), two workgroups per CU (other tiles are A/B knobs); BK = 32; two LDS stages filled by LDS-DMA
+// 96×64), two workgroups per CU, or for the ~1k-token GEMMs the 64×64 direct-to-register form
+// (sgemm_d64_kernel, below; other tiles are A/B knobs); BK = 32; two LDS stages filled by LDS-DMA
 // (buffer_load_dwordx4 … lds, 1 KiB per wave-instruction) with one barrier per K-step and two
 // waves per SIMD.  No register staging and no transposing LDS writes: the DMA writes each
 // operand's natural image —
@@ -373,11 +374,12 @@ struct SgDirect {
         }
     }
     __device__ static int row(int t, int c) { return KC ? 32 * t + c : 2 * c + t; }
-    // f[t][kk] = operand(row(t, c), k0 + 16h + kk); k >= ke reads as 0 (only the tail step checks)
+    // f[t][kk] = operand(row(t, c), k0 + 16h + kk).  TAIL: the K-step crosses ke, and k >= ke
+    // reads as 0 (a select per load; only the last K-step of a split, outside the main loop).
+    // (The loads' vectors are bit_cast whole: with their elements extracted one by one (v.x, v.y,
+    // ...) hipcc / ROCm 7.2 shrank the 16-B load to ONE dword load — wrong values.)
+    template <bool TAIL>
     __device__ __forceinline__ void load(float (&f)[2][16], int k0, int ke, int h) const {
-        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-        const bool full = k0 + 32 <= ke;                  // wave-uniform
         if (KC) {
             const int so = k0 * 4;
 #pragma unroll
@@ -385,22 +387,22 @@ struct SgDirect {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     unsigned vo = voff[t] + 16 * q;
-                    if (!full) vo = k0 + 16 * h + 4 * q < ke ? vo : kOob;
-                    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0);
-                    f[t][4 * q] = __builtin_bit_cast(float, v.x);
-                    f[t][4 * q + 1] = __builtin_bit_cast(float, v.y);
-                    f[t][4 * q + 2] = __builtin_bit_cast(float, v.z);
-                    f[t][4 * q + 3] = __builtin_bit_cast(float, v.w);
+                    if (TAIL) vo = k0 + 16 * h + 4 * q < ke ? vo : kOob;
+                    const float4 v = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, vo, so, 0));
+                    f[t][4 * q] = v.x;
+                    f[t][4 * q + 1] = v.y;
+                    f[t][4 * q + 2] = v.z;
+                    f[t][4 * q + 3] = v.w;
                 }
         } else {
 #pragma unroll
             for (int kk = 0; kk < 16; ++kk) {
                 const int so = (k0 + kk) * ld * 4;
                 unsigned vo = voff[0];
-                if (!full) vo = k0 + 16 * h + kk < ke ? vo : kOob;
-                const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, 0);
-                f[0][kk] = __builtin_bit_cast(float, v.x);
-                f[1][kk] = __builtin_bit_cast(float, v.y);
+                if (TAIL) vo = k0 + 16 * h + kk < ke ? vo : kOob;
+                const float2 v = __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rs, vo, so, 0));
+                f[0][kk] = v.x;
+                f[1][kk] = v.y;
             }
         }
     }
@@ -442,25 +444,39 @@ sgemm_d64_kernel(const float* __restrict__ A, int lda, const float* __restrict__
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[i][kk], xb[j][kk], acc[i][j], 0, 0, 0);
     };
-    const int nt = (ke - kb + 31) / 32;                   // the workgroup's K-steps
+    // the workgroup's whole K-steps; this wave's: t = wave + 4 i, i < nw.  Every prefetch is
+    // issued (a step past the wave's last re-reads its last one), so no load in the loop sits
+    // under a branch — with conditional loads hipcc's waitcnt pass put vmcnt(0) before the MFMAs
+    const int nt = (ke - kb) / 32, nw = nt > wave ? (nt - wave + 3) / 4 : 0;
+    auto k_of = [&](int i) { return kb + 32 * (wave + 4 * min(i, nw - 1)); };
     float fa[2][16], fb[2][16], ga[2][16], gb[2][16];
-    if (wave < nt) {
-        oa.load(fa, kb + 32 * wave, ke, h);
-        ob.load(fb, kb + 32 * wave, ke, h);
+    if (nw > 0) {
+        oa.template load<false>(fa, k_of(0), ke, h);
+        ob.template load<false>(fb, k_of(0), ke, h);
     }
-    // two K-steps per trip, the register sets swapping roles: (f) = step t, (g) = step t + 4
-    for (int t = wave; t < nt; t += 8) {
-        if (t + 4 < nt) {
-            oa.load(ga, kb + 32 * (t + 4), ke, h);
-            ob.load(gb, kb + 32 * (t + 4), ke, h);
-        }
+    // two K-steps per trip, the register sets swapping roles: (f) = step i, (g) = step i + 1.
+    // No branch inside a trip (hipcc sank a prefetch whose only use lay behind a branch down to
+    // that use), sched_barriers keep each prefetch above the MFMAs that hide it; an odd last
+    // step runs after the loop on (f), which the last trip's second prefetch filled.
+    int i = 0;
+    for (; i + 1 < nw; i += 2) {
+        oa.template load<false>(ga, k_of(i + 1), ke, h);
+        ob.template load<false>(gb, k_of(i + 1), ke, h);
+        __builtin_amdgcn_sched_barrier(0);
         mm(fa, fb);
-        if (t + 4 >= nt) break;
-        if (t + 8 < nt) {
-            oa.load(fa, kb + 32 * (t + 8), ke, h);
-            ob.load(fb, kb + 32 * (t + 8), ke, h);
-        }
+        __builtin_amdgcn_sched_barrier(0);
+        oa.template load<false>(fa, k_of(i + 2), ke, h);
+        ob.template load<false>(fb, k_of(i + 2), ke, h);
+        __builtin_amdgcn_sched_barrier(0);
         mm(ga, gb);
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (i < nw) mm(fa, fb);
+    // the partial K-step at the end of K (K % 32 != 0): the wave whose turn it is
+    if (kb + 32 * nt < ke && wave == nt % 4) {
+        oa.template load<true>(fa, kb + 32 * nt, ke, h);
+        ob.template load<true>(fb, kb + 32 * nt, ke, h);
+        mm(fa, fb);
     }
 
     // this wave's partial tile into LDS in (row, column) order
@@ -742,13 +758,20 @@ double sg_model(int cfg, int M, int N, int K, int sp, bool mcmc, int cus_) {
     const int steps = (K + g.bk - 1) / g.bk, per = (steps + sp - 1) / sp, spr = (steps + per - 1) / per;
     const double vol = (double)g.bm * g.bn * g.bk / (128.0 * 128.0 * 32.0);
     double t_one = 2.14 * vol, t_full = 3.74 * vol * g.occ / 2.0;
-    int kper = per;                                    // K-steps in a workgroup's critical path
-    if (cfg == 9) { t_one = 3.43; t_full = 6.4; }
-    else if (cfg == 11) { t_one = 1.9; t_full = 3.8; kper = (per + 3) / 4; }   // 4 waves split the K-steps
-    else if (mcmc) { t_one *= 1.1; t_full *= 1.1; }
     const long long wgs = tiles * spr, cus = cus_;
-    double t = wgs <= cus ? kper * t_one + 5.44
-                          : (double)((wgs + cus * g.occ - 1) / (cus * g.occ)) * (kper * t_full + 5.44);
+    double t;
+    if (cfg == 11) {
+        // 64×64 direct-to-register tiles: a wave runs every fourth K-step; small workgroups are
+        // dispatched as slots free up, so the load is continuous in the grid size rather than in
+        // whole rounds.  Fitted to the 27 training shapes (profiles/r4f_sgemm_cfg11.txt, 9 % rms):
+        // 1.55 µs per wave K-step alone, 4.5 µs per K-step-round at two workgroups per CU, 10 µs
+        t = 10.0 + (per + 3) / 4 * std::max(1.55, (double)wgs / (cus * g.occ) * 4.5);
+    } else {
+        if (cfg == 9) { t_one = 3.43; t_full = 6.4; }
+        else if (mcmc) { t_one *= 1.1; t_full *= 1.1; }
+        t = wgs <= cus ? per * t_one + 5.44
+                       : (double)((wgs + cus * g.occ - 1) / (cus * g.occ)) * (per * t_full + 5.44);
+    }
     if (spr > 1) t += 4.24 + (2.0 * spr + 1.0) * M * N * 4.0 * 0.127e-6;
     return t;
 }
@@ -780,8 +803,8 @@ int sg_splits(int cfg, int M, int N, int K, int* kc, bool mcmc, int cus) {
     return (steps + per - 1) / per;
 }
 
-// The tile configuration: 128×128 (cfg 0) or 192×128 (cfg 9), whichever the model times lower
-// at its best split (192×128 wins where the 128×128 grid leaves a half-empty last round, e.g.
+// The tile configuration: 128×128 (cfg 0), 192×128 (cfg 9) or 64×64 direct (cfg 11), whichever
+// the model times lower at its best split (192×128 wins where the 128×128 grid leaves a half-empty last round, e.g.
 // 5300 × 2304).  RS_SGEMM_CFG=0..11 forces a configuration (A/B knob).  The choice depends on
 // the shape and the device's CU count only, so a shape's results stay bitwise reproducible on a
 // given device model.
@@ -802,6 +825,11 @@ int sg_pick(int M, int N, int K, bool mcmc, int cus) {
             best = cfg;
         }
     }
+    // the 64×64 direct-to-register form where its (coarser) model wins by 10 %: the ~1k-token
+    // GEMMs whose 128×128 grid needs split-K (1100 × 768 × 768: 27.5 -> 18.7 µs)
+    int kc = 0;
+    const int sp11 = sg_splits(11, M, N, K, &kc, mcmc, cus);
+    if (sg_model(11, M, N, K, sp11, mcmc, cus) < 0.9 * tb) best = 11;
     return best;
 }
 

@@ -26,11 +26,13 @@ def test_192x128_where_the_128x128_grid_leaves_a_half_round(pick):
     assert pick(5300, 3072, 768) == (0, 1)
 
 
-def test_small_batches_split_k(pick):
-    cfg, sp = pick(1100, 768, 768)
-    assert cfg == 0 and 2 <= sp <= 8
+def test_small_batches_64x64_direct_or_split_k(pick):
+    # 1100 x 768 x 768: 54 tiles of 128x128 need split-K; 216 tiles of the 64x64 direct form fill
+    # the chip in one pass (27.5 -> 18.7 us, profiles/r4f_sgemm_cfg11.txt)
+    assert pick(1100, 768, 768) == (11, 1)
+    assert pick(2304, 768, 1100, 1) == (11, 1)  # a ~1k-token weight gradient (55.1 -> 44.9 us)
     cfg, sp = pick(768, 768, 5300, 1)           # weight gradient over 5.3k tokens
-    assert sp > 1
+    assert cfg == 0 and sp > 1
 
 
 def test_choice_is_a_function_of_shape_and_cus(pick):

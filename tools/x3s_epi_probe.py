@@ -50,10 +50,6 @@ def main():
             var = {"f32": (32, out32, {"x3s": 0, "x3s-noepi": 20, "x3s-bare": 3, "pp": 60, "pp-noepi": 61,
                                        "pp-inphase": 62, "pp-noepi-inphase": 63, "pp-noW": 64,
                                        "pp-noW-noepi": 65, "pp-bare": 69})}
-        if os.environ.get("PROBE") == "desync":
-            # odd workgroups of each XCD start 10-60 µs late (wrong order of nothing: same results)
-            var = {k: (c, o, {"prod": 0, "d10": 71, "d20": 72, "d30": 73, "d40": 74, "d60": 76})
-                   for k, (c, o, _) in var.items()}
         # the ping-pong kernel is bitwise equal to the production kernel (same MFMA order)
         for cfg, o in ((32, out32), (31, img)) if os.environ.get("PROBE") != "pp" else ():
             o2 = torch.empty_like(o)
