@@ -18,7 +18,8 @@ import __graft_entry__  # noqa: E402
 __graft_entry__._import_pkg()
 from asr_rescoring_amd import _lib  # noqa: E402
 
-NAMES = {0: "tr", 1: "mfma", 2: "valu", 3: "mem1", 4: "mem4", 5: "tr-headmajor", 6: "attn16"}
+NAMES = {0: "tr", 1: "mfma", 2: "valu", 3: "mem1", 4: "mem4", 5: "tr-headmajor", 6: "attn16", 8: "x3", 10: "x3v2-48",
+         11: "x3v2-64"}
 
 
 def main():
@@ -50,12 +51,29 @@ def main():
         q, k, v = x[:, 0].transpose(0, 1), x[:, 1].transpose(0, 1), x[:, 2].transpose(0, 1)
         p = torch.softmax(q @ k.transpose(1, 2) * 0.125, dim=-1)
         refs.append((r0, t, (p @ v).transpose(0, 1).reshape(t, H)))
+    # split-precision kinds (8, 10, 11): fp32 qkv [rows, 3H] in, three-part fp16 image [rows, 3H] out
+    qkv32 = ctx3 = None
+    if any(k in (8, 10, 11) for k in kinds):
+        qkv32 = qkv.float()
+        ctx3 = torch.zeros(rows, 3 * H, device=dev, dtype=torch.float16)
     for kind in kinds:
-        call = lambda: fn(kind, qkv.data_ptr(), d_len.data_ptr(), d_row.data_ptr(), n_seq, H, heads, ctx.data_ptr(), st)  # noqa
+        x3 = kind in (8, 10, 11)
+        qp, cp = (qkv32.data_ptr(), ctx3.data_ptr()) if x3 else (qkv.data_ptr(), ctx.data_ptr())
+        call = lambda: fn(kind, qp, d_len.data_ptr(), d_row.data_ptr(), n_seq, H, heads, cp, st)  # noqa
+        byts = rows * (3 * H * 4 + 3 * H * 2) if x3 else rows * (3 * H + H) * 2
         ctx.zero_()
         assert call() == 0
         torch.cuda.synchronize()
-        err = max((ctx[r0:r0 + t].float() - ref).abs().max().item() for r0, t, ref in refs) if kind in (0, 1, 2, 5, 6) else float('nan')
+        if x3:
+            ctx3.zero_()
+            assert call() == 0
+            torch.cuda.synchronize()
+            # hi + lo / 4096 of the three-part image (LO_SCALE 2^12)
+            img = ctx3.float()
+            out = img[:, :H] + img[:, H:2 * H] / 4096.0
+            err = max((out[r0:r0 + t] - ref).abs().max().item() for r0, t, ref in refs)
+        else:
+            err = max((ctx[r0:r0 + t].float() - ref).abs().max().item() for r0, t, ref in refs) if kind in (0, 1, 2, 5, 6) else float('nan')
         for _ in range(3):
             call()
         res = []
