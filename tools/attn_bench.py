@@ -68,9 +68,9 @@ def main():
             ctx3.zero_()
             assert call() == 0
             torch.cuda.synchronize()
-            # hi + lo / 4096 of the three-part image (LO_SCALE 2^12)
+            # three-part image [hi | hi/64 | lo*64] (common.h put_split4, kx = 3): hi + lo / 64
             img = ctx3.float()
-            out = img[:, :H] + img[:, H:2 * H] / 4096.0
+            out = img[:, :H] + img[:, 2 * H:3 * H] / 64.0
             err = max((out[r0:r0 + t] - ref).abs().max().item() for r0, t, ref in refs)
         else:
             err = max((ctx[r0:r0 + t].float() - ref).abs().max().item() for r0, t, ref in refs) if kind in (0, 1, 2, 5, 6) else float('nan')
