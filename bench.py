@@ -220,6 +220,17 @@ def main():
                 "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes": alg_bytes,
                 "launches": n, "avg_launch_ms": round(ms / max(n, 1), 4),
                 "flops_per_launch": fl / max(n, 1), "algorithmic_flops_per_launch": fl / kx / max(n, 1)}
+        # MFMA busy of the same kernel kind from the committed rocprofv3 PMC pass
+        # (SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE over the CUs, tools/pmc_mfma.py)
+        mfma_files = sorted(f for f in os.listdir(os.path.join(REPO, "profiles")) if f.endswith("_pmc_mfma.json"))
+        tag = {"qkv": "x3s:qkv", "oproj": "x3s:oproj", "ffn1": "x3s:ffn1", "ffn2": "x3s:ffn2"}.get(dom)
+        if tag and kx == 3 and mfma_files:
+            pm = json.load(open(os.path.join(REPO, "profiles", mfma_files[-1])))
+            hit = [v for k, v in pm.items() if k.startswith(tag)]
+            if hit:
+                roof["mfma_busy"] = hit[0].get("mfma_busy")
+                roof["mfma_busy_clock_GHz"] = hit[0].get("clock_GHz")
+                roof["mfma_busy_source"] = f"profiles/{mfma_files[-1]}"
 
     # ---- reranked 1-best CER (second half of BASELINE.json's metric), rank-0 shard -------
     # HIP fusion over the 101-weight grid + corpus CER on this step's LM scores, checked
