@@ -41,7 +41,8 @@ import torch.nn.functional as Fn
 
 
 class TorchBert:
-    """fp32 BERT on CPU from an HF-keyed weight dict (numpy arrays)."""
+    """fp32 BERT from an HF-keyed weight dict (numpy arrays); on the CPU (the oracle), or on a
+    GPU as the plain torch fp32 reference of a larger parity test (``device="cuda"``)."""
 
     def __init__(self, weights: Dict[str, np.ndarray], shape, device: str = "cpu"):
         self.s = shape
@@ -155,9 +156,9 @@ def pll_reference_pattern(model: TorchBert, tokens: np.ndarray, hyp_off: np.ndar
     with torch.no_grad():
         for b0 in range(0, len(rows), batch_size):
             chunk = rows[b0:b0 + batch_size]
-            ids = _pad([r[1] for r in chunk])
-            am = _pad([[1] * len(r[1]) for r in chunk])
-            labels = _pad([r[3] for r in chunk])
+            ids = _pad([r[1] for r in chunk]).to(model.device)
+            am = _pad([[1] * len(r[1]) for r in chunk]).to(model.device)
+            labels = _pad([r[3] for r in chunk]).to(model.device)
             mpos = [r[2] for r in chunk]
             hid = model.encoder(ids, am)
             rng = list(range(len(chunk)))

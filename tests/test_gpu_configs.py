@@ -125,6 +125,41 @@ def test_c3_finetuned_lm_moves_the_pick(w_base):
     assert bw_h > 0 and cer_h < cers[0], (bw_h, cer_h, cers[0])
 
 
+def test_c3_50_utterances_finetuned_vs_torch_fp32_on_gpu(w_base):
+    """Wider scoring parity at the C3 shape: 50 utterances x N=50 (about 80k masked forwards) with
+    a fine-tuned LM (the reference's fine-tune -> score -> fuse pipeline, MLM_PLL/main.py:117-161,
+    :184-186, rescore.py:25-45), against the same restatement run as a plain torch fp32 reference on
+    the GPU (the CPU oracle would take an hour at this size): PLL within 1e-3 (fp32-class: ~1e-6),
+    the 101-weight argmax and corpus CER equal for every utterance, and the LM moves the pick."""
+    import torch
+    from asr_rescoring_amd.scorer import PLLScorer
+    from asr_rescoring_amd.train import finetune_mlm_on_texts
+    from oracle import rescore_ref as RR
+    from oracle.bert_ref import TorchBert, pll_reference_pattern
+    nb = D.synthetic_nbest(50, 50, seed=7, hard=True)
+    w_ft, _ = finetune_mlm_on_texts(w_base, nb.refs, BERT_BASE, steps=300, lr=1e-4, seed=0, device=0)
+    s = PLLScorer(w_ft, BERT_BASE, device=0, max_rows=262144)
+    try:
+        pll = s.score_nbest(nb.tokens, nb.hyp_off).cpu().numpy()
+    finally:
+        s.close()
+    prev = torch.backends.cuda.matmul.allow_tf32
+    torch.backends.cuda.matmul.allow_tf32 = False
+    try:
+        _, ref_pll = pll_reference_pattern(TorchBert(w_ft, BERT_BASE, device="cuda"), nb.tokens, nb.hyp_off,
+                                           batch_size=512, full_head=False)
+    finally:
+        torch.backends.cuda.matmul.allow_tf32 = prev
+    assert rel_err(pll, ref_pll).max() < REL
+    hyps, N = _oracle_hyps(nb)
+    am = nb.am.reshape(nb.n_utt, N)
+    bw_o, cer_o, arg_o = RR.find_best_weight(am, ref_pll.reshape(nb.n_utt, N), hyps, nb.refs, n_best=N)
+    bw_h, cer_h, arg_h = RR.find_best_weight(am, pll.reshape(nb.n_utt, N), hyps, nb.refs, n_best=N)
+    assert np.array_equal(arg_o, arg_h) and bw_o == bw_h and cer_o == cer_h
+    am_only = RR.corpus_cer(nb.refs, [utt[i] for utt, i in zip(hyps, arg_h[0])])      # weight 0
+    assert bw_h > 0 and cer_h < am_only, (bw_h, cer_h, am_only)
+
+
 def test_c2_shape_cls(w_base, oracle_model):
     import torch
     from asr_rescoring_amd.scorer import RescoreBertHIP
