@@ -351,116 +351,6 @@ attn_full_kernel(const QT* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H
     }
 }
 
-// MFMA attention (fp16 mode): one wave per (sequence, head); queries and keys in blocks
-// of 64 (two 32-row tiles each), online softmax across key blocks.
-//   X = S^T = K . Q^T   (v_mfma_f32_32x32x16_f16, A = K rows, B = Q rows: both 16-byte
-//                        row loads straight from the QKV buffer)
-//   accumulator layout: lane = query, registers = keys  -> softmax over keys in-lane
-//   (+ one xor-32 shuffle), no cross-lane reductions per element.
-//   O^T = V^T . P^T      the fp16 P built from X's registers is the B operand as is
-//                        (k-step s of key tile kt = registers 8s..8s+7, key order
-//                        16s + 8(j>>2) + 4h + (j&3)); V^T comes from LDS, written
-//                        transposed once per key block.
-__global__ void __launch_bounds__(64, 4)
-attn_mfma_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
-                 f16* __restrict__ ctx, int kx) {
-    constexpr int VTS = 72;                       // V^T row stride (halfs): 64 keys + pad
-    __shared__ __attribute__((aligned(16))) f16 sVT[64 * VTS];
-    const int s = s0 + blockIdx.x, hd = blockIdx.y;
-    const int T = sm.len[s], rs = sm.row[s] - row0;
-    const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5;
-    const int ld = 3 * H;
-    const f16* base = qkv + (size_t)rs * ld + hd * 64;
-    const float scale = 0.125f;                   // head_dim ** -0.5
-    const bool one_block = T <= 64;               // V^T staged once for all query tiles
-
-    for (int q0 = 0; q0 < T; q0 += 32) {
-        // Q fragments (B operand): lane (query r, half h), k-step s: dims 16s + 8h .. +7
-        const int t = q0 + r;
-        half8 qf[4];
-#pragma unroll
-        for (int ks = 0; ks < 4; ++ks)
-            qf[ks] = t < T ? *(const half8*)(base + (size_t)t * ld + ks * 16 + hf * 8) : (half8){};
-        f32x16 o[2] = {(f32x16){}, (f32x16){}};  // O^T[d tile], lane = query
-        float m = -INFINITY, l = 0.f;
-
-        for (int k0 = 0; k0 < T; k0 += 64) {
-            if (!one_block || q0 == 0) {
-                // ---- V^T of this key block into LDS (zeros past T)
-                __syncthreads();
-#pragma unroll
-                for (int it = 0; it < 8; ++it) {
-                    const int kr = it * 8 + (lane >> 3), d0 = (lane & 7) * 8;
-                    const half8 v = k0 + kr < T ? *(const half8*)(base + (size_t)(k0 + kr) * ld + 2 * H + d0) : (half8){};
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) sVT[(d0 + e) * VTS + kr] = v[e];
-                }
-            }
-            if (!one_block || q0 == 0) __syncthreads();   // sVT written by every lane
-            // ---- one 32-key tile at a time: X = K . Q^T, online softmax, O^T += V^T . P^T
-            for (int kt = 0; kt < 2 && k0 + kt * 32 < T; ++kt) {
-                const int key = k0 + kt * 32 + r;
-                f32x16 x = {};
-#pragma unroll
-                for (int ks = 0; ks < 4; ++ks) {
-                    const half8 kf = key < T ? *(const half8*)(base + (size_t)key * ld + H + ks * 16 + hf * 8) : (half8){};
-                    x = __builtin_amdgcn_mfma_f32_32x32x16_f16(kf, qf[ks], x, 0, 0, 0);
-                }
-                float bm = -INFINITY;
-#pragma unroll
-                for (int j = 0; j < 16; ++j) {
-                    const int kj = k0 + kt * 32 + (j & 3) + 8 * (j >> 2) + 4 * hf;
-                    const float v = kj < T ? x[j] * scale : -INFINITY;
-                    x[j] = v;
-                    bm = fmaxf(bm, v);
-                }
-                bm = fmaxf(bm, __shfl_xor(bm, 32));
-                const float mn = fmaxf(m, bm);
-                const float alpha = __expf(m - mn);
-                half8 pf[2];                          // k-steps of this key tile
-                float ls = 0.f;
-#pragma unroll
-                for (int sk = 0; sk < 2; ++sk)
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        const f16 ph = (f16)__expf(x[sk * 8 + e] - mn);
-                        pf[sk][e] = ph;
-                        ls += (float)ph;
-                    }
-                ls += __shfl_xor(ls, 32);
-                l = l * alpha + ls;
-                m = mn;
-#pragma unroll
-                for (int dt = 0; dt < 2; ++dt) {
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) o[dt][j] *= alpha;
-                    const int d = dt * 32 + r;
-#pragma unroll
-                    for (int sk = 0; sk < 2; ++sk) {
-                        const int kb = kt * 32 + sk * 16 + 4 * hf;
-                        const half4 lo = *(const half4*)(sVT + d * VTS + kb);
-                        const half4 hi = *(const half4*)(sVT + d * VTS + kb + 8);
-                        const half8 vf = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-                        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_f16(vf, pf[sk], o[dt], 0, 0, 0);
-                    }
-                }
-            }
-        }
-        // ---- store: lane = query, registers = dims (j&3) + 8(j>>2) + 4h of d tile dt
-        if (t < T) {
-            const float il = 1.0f / l;
-            f16* orow = ctx + (size_t)(rs + t) * kx * H;
-#pragma unroll
-            for (int dt = 0; dt < 2; ++dt)
-#pragma unroll
-                for (int g = 0; g < 4; ++g)
-                    put_split4(orow, hd * 64 + dt * 32 + 8 * g + 4 * hf, H, kx,
-                               make_float4(o[dt][4 * g] * il, o[dt][4 * g + 1] * il,
-                                           o[dt][4 * g + 2] * il, o[dt][4 * g + 3] * il));
-        }
-    }
-}
-
 // One wave per (sequence, head), MFMA, latency-lean variant:
 //  * K fragments (A operand of X = K.Q^T) go straight from HBM into registers and stay
 //    resident across the query tiles (T <= 64: one key block, loaded once);
@@ -469,20 +359,20 @@ attn_mfma_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int 
 //    scalar transposing writes.  V row stride 96 halfs makes those reads conflict-free
 //    (the 8 (row, 16-column) blocks of a 32-lane half land on disjoint 8-bank ranges);
 //  * all of a key block's global loads are in flight before the first is consumed.
-// Numerics are those of attn_mfma_kernel (fp16 P, fp32 accumulation, online softmax).
+// Numerics: fp16 P, fp32 accumulation, online softmax across 64-key blocks.
 // DEDUP (layer 0): qkv holds the chunk's unique rows; position t of sequence s reads row
 // urow_m[s] when t is its masked position, urow_h[s] + t otherwise.
 template <bool DEDUP>
 __global__ void __launch_bounds__(64, 3)
 attn_tr_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
-               f16* __restrict__ ctx, int kx, int heads_fast) {
+               f16* __restrict__ ctx, int kx) {
     typedef __fp16 fp16x4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
     constexpr int VR = 96;
     __shared__ __attribute__((aligned(16))) f16 sV[64 * VR];
-    // heads_fast = number of heads: 1-D grid, the heads of one sequence are consecutive
-    // workgroups (their 128-B slices of the same rows are fetched together); 0: grid (seq, head)
-    const int s = s0 + (heads_fast ? (int)blockIdx.x / heads_fast : (int)blockIdx.x);
-    const int hd = heads_fast ? (int)blockIdx.x % heads_fast : (int)blockIdx.y;
+    // grid (sequence, head) (a head-major 1-D grid, the heads of a sequence adjacent, measured
+    // 7 % slower, round 1)
+    const int s = s0 + (int)blockIdx.x;
+    const int hd = (int)blockIdx.y;
     const int T = sm.len[s], rs = sm.row[s] - row0;
     const int lane = threadIdx.x, r = lane & 31, hf = lane >> 5;
     const int ld = 3 * H;
@@ -750,173 +640,13 @@ attn16_kernel(const f16* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
 // stored scaled by 2^12 (LO_SCALE) and their products go to separate accumulators scaled back
 // by 2^-12: 1e-7-level error instead of 3e-5 (tools/diag/attn_split_check.py).  P is split
 // after the exponential; the softmax row sum adds the fp32 P.  V is staged as two fp16 images
-// (hi, scaled lo) with the same 80-half rows.  T <= 64 (one key block; the host routes longer
+// (hi, scaled lo).  T <= 64 (one key block; the host routes longer
 // sequences to attn_full_kernel<float>).
 constexpr float LO_SCALE = 4096.f, LO_UNSCALE = 1.f / 4096.f;
 // DEDUP (MLM layer 0): Q, K, V rows come from the chunk's unique rows (row t of copy s is
 // unique row urow_m[s] at its masked position, urow_h[s] + t elsewhere), as attn16_kernel.
-template <bool DEDUP>
-__global__ void __launch_bounds__(64, 2)
-attn16x3_kernel(const float* __restrict__ qkv, SeqMeta sm, int s0, int row0, int H,
-                f16* __restrict__ ctx, int kx) {
-    typedef __fp16 fp16x4 __attribute__((__vector_size__(4 * sizeof(__fp16))));
-    constexpr int VR = 80;
-    __shared__ __attribute__((aligned(16))) f16 sVh[64 * VR];
-    __shared__ __attribute__((aligned(16))) f16 sVl[64 * VR];
-    const int s = s0 + blockIdx.x, hd = blockIdx.y;
-    const int T = sm.len[s], rs = sm.row[s] - row0;
-    const int lane = threadIdx.x, r16 = lane & 15, g = lane >> 4;
-    const int ld = 3 * H;
-    const int ub = DEDUP ? sm.urow_h[s] : rs;
-    const int mp = DEDUP ? sm.mask_pos[s] : -1, um = DEDUP ? sm.urow_m[s] : 0;
-    const float* base = qkv + (size_t)ub * ld + hd * 64;
-    const float* mbase = qkv + (size_t)um * ld + hd * 64;
-    auto rowp = [&](int t) -> const float* {
-        if constexpr (DEDUP) return t == mp ? mbase : base + (size_t)t * ld;
-        else return base + (size_t)t * ld;
-    };
-    const float scale = 0.125f;
-    const int tr_off = (4 * g + ((lane & 15) >> 2)) * VR + 4 * (lane & 3);
-    auto tr_read = [&](const f16* p) {
-        const fp16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4f16((__attribute__((address_space(3))) fp16x4*)p);
-        return __builtin_bit_cast(half4, v);
-    };
-    // every V and K load of the (sequence, head) issued before any is used: 32 float4 per lane
-    // in flight (latency-bound kernel, 2 waves per SIMD), then V -> hi / lo LDS images and K
-    // -> hi / lo fragments
-    float4 vraw[16], kraw[4][2][2];
-#pragma unroll
-    for (int it = 0; it < 16; ++it) {
-        const int kr = it * 4 + (lane >> 4), c4 = (lane & 15) * 4;
-        vraw[it] = kr < T ? *(const float4*)(rowp(kr) + 2 * H + c4) : make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            const int key = kt * 16 + r16;
-            const float* kp = rowp(key) + H + ks * 32 + g * 8;
-            kraw[kt][ks][0] = key < T ? *(const float4*)kp : make_float4(0.f, 0.f, 0.f, 0.f);
-            kraw[kt][ks][1] = key < T ? *(const float4*)(kp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-    // the first query tile's rows, prefetched the same way
-    float4 qraw[2][2];
-    auto load_q = [&](int q0) {
-        const int t = q0 + r16;
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-            const float* qp = rowp(t) + ks * 32 + g * 8;
-            qraw[ks][0] = t < T ? *(const float4*)qp : make_float4(0.f, 0.f, 0.f, 0.f);
-            qraw[ks][1] = t < T ? *(const float4*)(qp + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-    };
-    load_q(0);
-    auto split_raw = [](const float4 (&r)[2], half8& hi, half8& lo) {
-        const float v[8] = {r[0].x, r[0].y, r[0].z, r[0].w, r[1].x, r[1].y, r[1].z, r[1].w};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-            hi[e] = (f16)v[e];
-            lo[e] = (f16)((v[e] - (float)hi[e]) * LO_SCALE);
-        }
-    };
-#pragma unroll
-    for (int it = 0; it < 16; ++it) {
-        const int kr = it * 4 + (lane >> 4), c4 = (lane & 15) * 4;
-        const float4 v = vraw[it];
-        const half4 h = {(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
-        const half4 l = {(f16)((v.x - (float)h[0]) * LO_SCALE), (f16)((v.y - (float)h[1]) * LO_SCALE),
-                         (f16)((v.z - (float)h[2]) * LO_SCALE), (f16)((v.w - (float)h[3]) * LO_SCALE)};
-        *(half4*)(sVh + kr * VR + c4) = h;
-        *(half4*)(sVl + kr * VR + c4) = l;
-    }
-    half8 kfh[4][2], kfl[4][2];
-#pragma unroll
-    for (int kt = 0; kt < 4; ++kt)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) split_raw(kraw[kt][ks], kfh[kt][ks], kfl[kt][ks]);
-    __syncthreads();
-    half8 vfh[4][2], vfl[4][2];
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int m2 = 0; m2 < 2; ++m2) {
-            const int o = (32 * m2) * VR + 16 * dt + tr_off;
-            half4 lo = tr_read(sVh + o), hi = tr_read(sVh + o + 16 * VR);
-            vfh[dt][m2] = (half8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-            lo = tr_read(sVl + o);
-            hi = tr_read(sVl + o + 16 * VR);
-            vfl[dt][m2] = (half8){lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        }
-    const int nkt = min(4, (T + 15) >> 4), nm = (nkt + 1) >> 1;
-    for (int q0 = 0; q0 < T; q0 += 16) {
-        const int t = q0 + r16;
-        half8 qh[2], ql[2];
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) split_raw(qraw[ks], qh[ks], ql[ks]);
-        if (q0 + 16 < T) load_q(q0 + 16);             // next tile's rows under this tile's math
-        f32x4 x[4];
-        float bm = -INFINITY;
-#pragma unroll
-        for (int kt = 0; kt < 4; ++kt) {
-            x[kt] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-            if (kt < nkt) {
-                f32x4 a = {}, al = {};
-#pragma unroll
-                for (int ks = 0; ks < 2; ++ks) {
-                    al = __builtin_amdgcn_mfma_f32_16x16x32_f16(kfl[kt][ks], qh[ks], al, 0, 0, 0);
-                    al = __builtin_amdgcn_mfma_f32_16x16x32_f16(kfh[kt][ks], ql[ks], al, 0, 0, 0);
-                    a = __builtin_amdgcn_mfma_f32_16x16x32_f16(kfh[kt][ks], qh[ks], a, 0, 0, 0);
-                }
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                    const int key = kt * 16 + 4 * g + e;
-                    const float v = key < T ? __builtin_fmaf(al[e], LO_UNSCALE, a[e]) * scale : -INFINITY;
-                    x[kt][e] = v;
-                    bm = fmaxf(bm, v);
-                }
-            }
-        }
-        bm = fmaxf(bm, __shfl_xor(bm, 16));
-        bm = fmaxf(bm, __shfl_xor(bm, 32));
-        half8 ph[2], pl[2];
-        float ls = 0.f;
-#pragma unroll
-        for (int m2 = 0; m2 < 2; ++m2)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const float p = __expf(x[2 * m2 + (j >> 2)][j & 3] - bm);
-                ph[m2][j] = (f16)p;
-                pl[m2][j] = (f16)((p - (float)ph[m2][j]) * LO_SCALE);
-                ls += p;
-            }
-        ls += __shfl_xor(ls, 16);
-        ls += __shfl_xor(ls, 32);
-        f32x4 o[4];
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-            f32x4 oh = {}, ol = {};
-#pragma unroll
-            for (int m2 = 0; m2 < 2; ++m2)
-                if (m2 < nm) {
-                    ol = __builtin_amdgcn_mfma_f32_16x16x32_f16(vfl[dt][m2], ph[m2], ol, 0, 0, 0);
-                    ol = __builtin_amdgcn_mfma_f32_16x16x32_f16(vfh[dt][m2], pl[m2], ol, 0, 0, 0);
-                    oh = __builtin_amdgcn_mfma_f32_16x16x32_f16(vfh[dt][m2], ph[m2], oh, 0, 0, 0);
-                }
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[dt][e] = __builtin_fmaf(ol[e], LO_UNSCALE, oh[e]);
-        }
-        if (t < T) {
-            const float il = 1.0f / ls;
-            f16* orow = ctx + (size_t)(rs + t) * kx * H;
-#pragma unroll
-            for (int dt = 0; dt < 4; ++dt)
-                put_split4(orow, hd * 64 + dt * 16 + 4 * g, H, kx,
-                           make_float4(o[dt][0] * il, o[dt][1] * il, o[dt][2] * il, o[dt][3] * il));
-        }
-    }
-}
-
-// attn16x3_kernel re-laid for occupancy: V staged for R = 48 or 64 key rows only (R = 48 when
+//
+// Layout: V staged for R = 48 or 64 key rows only (R = 48 when
 // every sequence of the chunk has T <= 48: the 16 rows past it are zeros the second 32-key
 // block reads from registers), 128-B LDS rows without padding — the 16-B chunks XOR-swizzled
 // by (row & 6), which keeps the ds_read_b64_tr_b16 lane groups on distinct banks — and the
@@ -1391,21 +1121,9 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
                                  int H, int heads, f16* ctx, int kx, hipStream_t st, bool dedup, int max_len) {
     if (s1 <= s0) return hipSuccess;
     const dim3 grid(s1 - s0, heads);
-    // RS_ATTN_ORDER: "seq" (default: grid (sequence, head)) or "head" (1-D grid, heads of a
-    // sequence adjacent: 7 % slower, tools/attn_bench.py kind 5)
-    static const int head_order = [] {
-        const char* v = getenv("RS_ATTN_ORDER");
-        return v && !strcmp(v, "head") ? 1 : 0;
-    }();
-    const dim3 grid_tr = head_order ? dim3((s1 - s0) * heads) : grid;
-    const int hf = head_order ? heads : 0;
-    // RS_ATTN16: 1 = 16x16x32 attention (attn16_kernel), 0 = 32x32x16 (attn_tr_kernel)
-    const char* a16 = getenv("RS_ATTN16");
-    // (T > 64 re-stages K/V per 16-query tile: slower than the 32-query tiles there)
-    const bool use16 = !(a16 && !strcmp(a16, "0")) && !head_order && max_len > 0 && max_len <= 64;
-    // RS_ATTN_V2 (default 1): attn16x3v2_kernel (R = 48 rows when max_len <= 48); 0 = attn16x3_kernel
-    const char* av2 = getenv("RS_ATTN_V2");
-    const bool v2 = !(av2 && !strcmp(av2, "0"));
+    // 16x16x32 tiles while every sequence of the chunk has T <= 64 (longer ones re-stage K/V per
+    // 16-query tile: the 32-query tiles of attn_tr_kernel are faster there)
+    const bool short16 = max_len > 0 && max_len <= 64;
     auto x3v2 = [&](auto dd) {
         constexpr bool D = decltype(dd)::value;
         if (max_len <= 48)
@@ -1414,49 +1132,30 @@ hipError_t launch_attention_full(const void* qkv, bool qkv32, SeqMeta sm, int s0
             hipLaunchKernelGGL((attn16x3v2_kernel<D, 64>), grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
     };
     if (dedup && qkv32) {                         // fp16x3 split-operand layer 0 (T <= 64)
-        if (kx != 2 || H % 64 || max_len <= 0 || max_len > 64) return hipErrorInvalidValue;
-        if (v2) x3v2(std::true_type{});
-        else hipLaunchKernelGGL(attn16x3_kernel<true>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
+        if (kx != 2 || H % 64 || !short16) return hipErrorInvalidValue;
+        x3v2(std::true_type{});
         return hipGetLastError();
     }
     if (dedup) {                                  // fp16 QKV, kx == 1 (host gates it)
         if (kx != 1 || H % 64) return hipErrorInvalidValue;
-        if (use16) {
-            hipLaunchKernelGGL(attn16_kernel<true>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
-            return hipGetLastError();
-        }
-        hipLaunchKernelGGL(attn_tr_kernel<true>, grid_tr, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx, hf);
+        if (short16) hipLaunchKernelGGL(attn16_kernel<true>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
+        else hipLaunchKernelGGL(attn_tr_kernel<true>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
         return hipGetLastError();
     }
-    // RS_ATTN: "tr" (default, transposed-read MFMA), "mfma" (LDS-transposed V), "valu"
-    static const int kind = [] {
-        const char* v = getenv("RS_ATTN");
-        if (v && !strcmp(v, "valu")) return 2;
-        if (v && !strcmp(v, "mfma")) return 1;
-        return 0;
-    }();
-    // RS_ATTN16X3=0: fp32 VALU attention in the fp16x3 mode instead of the split-MFMA kernel
-    const char* a16x3 = getenv("RS_ATTN16X3");
-    const bool use16x3 = !(a16x3 && !strcmp(a16x3, "0")) && max_len > 0 && max_len <= 64 && H % 64 == 0;
-    if (qkv32 && use16x3 && v2)
+    if (qkv32 && short16 && H % 64 == 0) {
         x3v2(std::false_type{});
-    else if (qkv32 && use16x3)
-        hipLaunchKernelGGL(attn16x3_kernel<false>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
-    else if (qkv32 && v2 && !(a16x3 && !strcmp(a16x3, "0")) && H % 64 == 0) {
+    } else if (qkv32 && H % 64 == 0) {
         // a chunk with some T > 64: its T <= 64 sequences on the split-MFMA kernel, the longer
         // ones (online softmax over 64-key blocks) on the fp32 VALU kernel; each skips the other's
         hipLaunchKernelGGL((attn16x3v2_kernel<false, 64>), grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx);
         hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx, 64);
-    } else if (qkv32)
+    } else if (qkv32) {
         hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, s0, row0, H, ctx, kx, 0);
-    else if (kind == 0 && use16)
+    } else if (short16) {
         hipLaunchKernelGGL(attn16_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
-    else if (kind == 2)
-        hipLaunchKernelGGL(attn_full_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx, 0);
-    else if (kind == 1)
-        hipLaunchKernelGGL(attn_mfma_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
-    else
-        hipLaunchKernelGGL(attn_tr_kernel<false>, grid_tr, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx, hf);
+    } else {
+        hipLaunchKernelGGL(attn_tr_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, s0, row0, H, ctx, kx);
+    }
     return hipGetLastError();
 }
 
@@ -1530,8 +1229,10 @@ attn_memskel_kernel(const f16* __restrict__ qkv, SeqMeta sm, int H, f16* __restr
 }
 
 // Timing/diagnostic entry (not part of the scoring path): one attention launch over
-// sequences [0, n_seq) with explicit kernel kind (0 tr, 1 mfma, 2 valu); len / row device
-// int32 arrays; qkv fp16 [rows, 3H]; ctx fp16 [rows, H].
+// sequences [0, n_seq) with an explicit kernel kind: 0 attn_tr_kernel, 6 attn16_kernel (fp16
+// qkv [rows, 3H], ctx fp16 [rows, H]); 9 attn_full_kernel<float>, 10 / 11 attn16x3v2_kernel with
+// 48 / 64 staged key rows (fp32 qkv [rows, 3H], ctx the three-part fp16 image [rows, 3H]);
+// 3 / 4 the memory skeleton (one / four heads per block).  len / row: device int32 arrays.
 extern "C" int rs_debug_attention(int kind, const void* qkv, const int* len, const int* row, int n_seq,
                                   int H, int heads, void* ctx, void* stream) {
     SeqMeta sm{};
@@ -1539,28 +1240,22 @@ extern "C" int rs_debug_attention(int kind, const void* qkv, const int* len, con
     sm.row = row;
     const dim3 grid(n_seq, heads);
     hipStream_t st = (hipStream_t)stream;
-    if (kind == 0)      // (sequence, head) grid
-        hipLaunchKernelGGL(attn_tr_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1, 0);
-    else if (kind == 8) // split-precision 16x16x32 attention over fp32 qkv [rows, 3H], ctx fp16 image [rows, 3H]
-        hipLaunchKernelGGL(attn16x3_kernel<false>, grid, dim3(64), 0, st, (const float*)qkv, sm, 0, 0, H, (f16*)ctx, 3);
-    else if (kind == 10) // attn16x3v2_kernel, R = 48 (every T <= 48)
+    if (kind == 0)
+        hipLaunchKernelGGL(attn_tr_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
+    else if (kind == 10)
         hipLaunchKernelGGL((attn16x3v2_kernel<false, 48>), grid, dim3(64), 0, st, (const float*)qkv, sm, 0, 0, H, (f16*)ctx, 3);
-    else if (kind == 11) // attn16x3v2_kernel, R = 64 (every T <= 64)
+    else if (kind == 11)
         hipLaunchKernelGGL((attn16x3v2_kernel<false, 64>), grid, dim3(64), 0, st, (const float*)qkv, sm, 0, 0, H, (f16*)ctx, 3);
-    else if (kind == 9) // fp32 VALU attention (same I/O as kind 8)
+    else if (kind == 9)
         hipLaunchKernelGGL(attn_full_kernel<float>, grid, dim3(64), 0, st, (const float*)qkv, sm, 0, 0, H, (f16*)ctx, 3, 0);
-    else if (kind == 6) // 16x16x32 attention
+    else if (kind == 6)
         hipLaunchKernelGGL(attn16_kernel<false>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
-    else if (kind == 5) // head-fastest 1-D grid
-        hipLaunchKernelGGL(attn_tr_kernel<false>, dim3(n_seq * heads), dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1, heads);
-    else if (kind == 1)
-        hipLaunchKernelGGL(attn_mfma_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1);
-    else if (kind == 2)
-        hipLaunchKernelGGL(attn_full_kernel<f16>, grid, dim3(64), 0, st, (const f16*)qkv, sm, 0, 0, H, (f16*)ctx, 1, 0);
     else if (kind == 3)
         hipLaunchKernelGGL(attn_memskel_kernel, grid, dim3(64), 0, st, (const f16*)qkv, sm, H, (f16*)ctx, 1);
-    else   // kind 4: memory skeleton, 4 heads per 256-thread block
+    else if (kind == 4)
         hipLaunchKernelGGL(attn_memskel_kernel, dim3(n_seq, heads / 4), dim3(256), 0, st, (const f16*)qkv, sm, H, (f16*)ctx, 4);
+    else
+        return -1;
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 

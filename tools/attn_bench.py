@@ -3,7 +3,7 @@
 Lengths T ~ U{lo..hi} (default 26..44, the C3 masked-copy lengths), random fp16 Q/K/V.
 Prints per kernel kind: time per launch, effective HBM bandwidth (Q,K,V read + ctx write),
 and max |err| vs a torch fp32 reference on the first sequences.
-usage: python tools/attn_bench.py [n_seq] [lo] [hi]   (env KINDS=0,1,2)
+usage: python tools/attn_bench.py [n_seq] [lo] [hi]   (env KINDS=0,6,10)
 """
 import ctypes
 import os
@@ -18,15 +18,14 @@ import __graft_entry__  # noqa: E402
 __graft_entry__._import_pkg()
 from asr_rescoring_amd import _lib  # noqa: E402
 
-NAMES = {0: "tr", 1: "mfma", 2: "valu", 3: "mem1", 4: "mem4", 5: "tr-headmajor", 6: "attn16", 8: "x3", 10: "x3v2-48",
-         11: "x3v2-64"}
+NAMES = {0: "tr", 3: "mem1", 4: "mem4", 6: "attn16", 9: "x3-valu", 10: "x3v2-48", 11: "x3v2-64"}
 
 
 def main():
     n_seq = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
     lo = int(sys.argv[2]) if len(sys.argv) > 2 else 26
     hi = int(sys.argv[3]) if len(sys.argv) > 3 else 44
-    kinds = [int(k) for k in os.environ.get("KINDS", "0,1").split(",")]
+    kinds = [int(k) for k in os.environ.get("KINDS", "0,6").split(",")]
     H, heads = 768, 12
     lib = _lib.load()
     fn = lib.rs_debug_attention
@@ -51,13 +50,13 @@ def main():
         q, k, v = x[:, 0].transpose(0, 1), x[:, 1].transpose(0, 1), x[:, 2].transpose(0, 1)
         p = torch.softmax(q @ k.transpose(1, 2) * 0.125, dim=-1)
         refs.append((r0, t, (p @ v).transpose(0, 1).reshape(t, H)))
-    # split-precision kinds (8, 10, 11): fp32 qkv [rows, 3H] in, three-part fp16 image [rows, 3H] out
+    # split-precision kinds (9, 10, 11): fp32 qkv [rows, 3H] in, three-part fp16 image [rows, 3H] out
     qkv32 = ctx3 = None
-    if any(k in (8, 10, 11) for k in kinds):
+    if any(k in (9, 10, 11) for k in kinds):
         qkv32 = qkv.float()
         ctx3 = torch.zeros(rows, 3 * H, device=dev, dtype=torch.float16)
     for kind in kinds:
-        x3 = kind in (8, 10, 11)
+        x3 = kind in (9, 10, 11)
         qp, cp = (qkv32.data_ptr(), ctx3.data_ptr()) if x3 else (qkv.data_ptr(), ctx.data_ptr())
         call = lambda: fn(kind, qp, d_len.data_ptr(), d_row.data_ptr(), n_seq, H, heads, cp, st)  # noqa
         byts = rows * (3 * H * 4 + 3 * H * 2) if x3 else rows * (3 * H + H) * 2
@@ -73,7 +72,7 @@ def main():
             out = img[:, :H] + img[:, 2 * H:3 * H] / 64.0
             err = max((out[r0:r0 + t] - ref).abs().max().item() for r0, t, ref in refs)
         else:
-            err = max((ctx[r0:r0 + t].float() - ref).abs().max().item() for r0, t, ref in refs) if kind in (0, 1, 2, 5, 6) else float('nan')
+            err = max((ctx[r0:r0 + t].float() - ref).abs().max().item() for r0, t, ref in refs) if kind in (0, 6) else float('nan')
         for _ in range(3):
             call()
         res = []

@@ -1,4 +1,4 @@
-"""Diagnostic: split-precision attention (kind 8) vs fp32 VALU (kind 9), fp16 kernel (kind 6) and fp64 torch."""
+"""Diagnostic: split-precision attention (attn16x3v2, kind 11) vs fp32 VALU (kind 9), fp16 kernel (kind 6) and fp64 torch."""
 import os
 import sys
 
@@ -29,7 +29,7 @@ for scale in (0.6, 60.0):
         p = torch.softmax(q @ k.transpose(1, 2) * 0.125, dim=-1)
         refs.append((p @ v).transpose(0, 1).reshape(t, H))
     ref = torch.cat(refs)
-    c8 = _run(8, qkv, T, row, H, heads, kx=3).double()
+    c8 = _run(11, qkv, T, row, H, heads, kx=3).double()
     c9 = _run(9, qkv, T, row, H, heads, kx=3).double()
     c6 = _run(6, qkv.half(), T, row, H, heads).double()
     o8 = c8[:, :H] + c8[:, 2 * H:] / 64
