@@ -62,7 +62,6 @@ struct EpiArgs {
     unsigned* ln_next;     // host: the first ticket of the next launch on lncnt[0] (owned with lncnt)
     float ln_eps;
     int diag;              // EPI_LNRES_IMG timing diagnostics (RS_LNFUSE_DIAG; 0 in production)
-    int rev;               // gemm_x3s_kernel: row panels walked last to first
 };
 inline size_t lnres_granules(int m_pad) { return (size_t)m_pad * 4 * 2; }     // <= 4 column tiles
 
@@ -115,7 +114,6 @@ struct SeqMeta {
     const int* row;        // first token row of the sequence (global row index)
     const int* urow_h;     // layer-0 dedup: first unique row of the sequence's hypothesis (chunk-local)
     const int* urow_m;     // layer-0 dedup: the sequence's [MASK] unique row (chunk-local)
-    int rev;               // split-precision attention: sequences walked last to first
 };
 
 __device__ __forceinline__ float wave_sum(float v) {

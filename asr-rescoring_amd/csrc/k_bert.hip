@@ -660,7 +660,7 @@ attn16x3v2_kernel(const float* __restrict__ qkv, SeqMeta sm, int s0, int row0, i
     constexpr int KT = R / 16;                    // 16-key tiles staged
     __shared__ __attribute__((aligned(16))) f16 sVh[R * 64];
     __shared__ __attribute__((aligned(16))) f16 sVl[R * 64];
-    const int s = s0 + (sm.rev ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x), hd = blockIdx.y;
+    const int s = s0 + blockIdx.x, hd = blockIdx.y;
     const int T = sm.len[s], rs = sm.row[s] - row0;
     if (T > R) return;                            // (mixed chunks: the long ones run on attn_full)
     const int lane = threadIdx.x, r16 = lane & 15, g = lane >> 4;

@@ -809,9 +809,8 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     if (wave >= NW / 2) __builtin_amdgcn_s_setprio(1);
     auto tile_of = [&](int tt, int& m0, int& n0) {
         if constexpr (LNR) {                      // row panel t / ntn, column tile t % ntn
-            const int pn = tt / n_tiles_n;
-            m0 = (ep.rev ? n_tiles / n_tiles_n - 1 - pn : pn) * BM;
-            n0 = (tt - pn * n_tiles_n) * BM;
+            m0 = (tt / n_tiles_n) * BM;
+            n0 = (tt - (tt / n_tiles_n) * n_tiles_n) * BM;
             return;
         }
         const int xcd = tt & 7, pos = tt >> 3, q = n_tiles >> 3, r = n_tiles & 7;
@@ -821,7 +820,6 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         const int gm = min(GM, n_tiles_m - g * GM);
         const int tn = loc / gm;
         m0 = (g * GM + (loc - tn * gm)) * BM;
-        if (ep.rev) m0 = (n_tiles_m - 1) * BM - m0;
         n0 = tn * BM;
     };
     // LDS-DMA: buffer_load_dwordx4 ... lds (32-bit lane offsets into a per-tile panel buffer
@@ -1179,8 +1177,6 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             }
             char* slb = slabs + wave * 4096;
             const int rr0 = lane >> 3, c16 = lane & 7;
-            // VAR 1073741824 (A/B): default-policy stores instead of non-temporal
-            constexpr int SPOL = (VAR & 1073741824) ? 0 : 64;
             // VAR 33554432 (timing diagnostic, wrong results): every tile stores onto the rows of
             // row panel 0 (L2-resident lines), separating the store path from the HBM write burst
             const int sm0 = (VAR & 33554432) ? 0 : cm0;
@@ -1201,7 +1197,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         uint4 v[4];
                         slab_read4(slb, rr0, c16, v);
 #pragma unroll
-                        for (int it = 0; it < 4; ++it) st16<SPOL>((uint4*)(ob + (size_t)(it * 8 + rr0) * ep.ldc), v[it]);
+                        for (int it = 0; it < 4; ++it) st16<64>((uint4*)(ob + (size_t)(it * 8 + rr0) * ep.ldc), v[it]);
                     }
             } else {
                 // two-part images in 32 x 64 slab blocks (row blocks 2 i2 + a, all four column
@@ -1231,7 +1227,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         uint4 v[4];
                         slab_read4(slb, rr0, c16, v);
 #pragma unroll
-                        for (int it = 0; it < 4; ++it) st16<SPOL>((uint4*)(ob + (size_t)(it * 8 + rr0) * ep.ldc), v[it]);
+                        for (int it = 0; it < 4; ++it) st16<64>((uint4*)(ob + (size_t)(it * 8 + rr0) * ep.ldc), v[it]);
                     }
                 }
             }
@@ -1505,7 +1501,6 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
             case 50: e = RS_X3(8); break;
             case 51: e = RS_X3(33554432); break;
             case 53: e = RS_X3(8 | 33554432); break;
-            case 56: e = RS_X3(1073741824); break;     // default-policy epilogue stores
             default: return -1;
         }
 #undef RS_X3

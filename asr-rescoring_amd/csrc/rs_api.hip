@@ -420,17 +420,10 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
     EpiArgs ep{};
     // split-operand GEMM over m_valid rows: A two-part image, W rows of ldw halfs; profiled as
     // MFMA work (three products of logical K)
-    // RS_ALT_DIR (A/B, read per call): consecutive split-operand kernels of a layer walk their
-    // row panels / sequences in alternating directions, so each starts on the rows its producer
-    // wrote last (still in the MALL)
-    const char* altd = getenv("RS_ALT_DIR");
-    const bool alt = altd && !strcmp(altd, "1");
-    int flip = 0;
     auto gx = [&](int kind, int epi, const f16* A, const f16* W, int ldw, int m_valid, int N, int K, EpiArgs e,
                   int n_flop_cols) -> int {
         const int al = gemm_row_align();
         e.m_valid = m_valid;
-        e.rev = alt ? (flip++ & 1) : 0;
         ProfScope ps(m, st, kind, 2.0 * m_valid * (double)n_flop_cols * 3.0 * K);
         const int M_pad = (m_valid + al - 1) / al * al;
         if ((epi == EPI_BIAS_F32 || epi == EPI_GELU_F16) && K % 64 == 0 && pp_on())
@@ -495,9 +488,7 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
             // the residual blocks close in ln_res32 (x32 <- LN(x32) + o32, next two-part image)
             {
                 ProfScope ps(m, st, RS_K_ATTN, 0);
-                SeqMeta sma = sm;
-                sma.rev = alt ? (flip++ & 1) : 0;
-                HIPTRY(launch_attention_full(qkv, true, sma, c.s0, c.s1, 0, H, nh, ctx, 2, st, uq, c.max_len));
+                HIPTRY(launch_attention_full(qkv, true, sm, c.s0, c.s1, 0, H, nh, ctx, 2, st, uq, c.max_len));
             }
             float* o32 = (float*)qkv;
             // residual block: h16 <- image(LN(A·Wᵀ + b + h16)) in the GEMM epilogue (lnfuse), or

@@ -50,9 +50,6 @@ def main():
             var = {"f32": (32, out32, {"x3s": 0, "x3s-noepi": 20, "x3s-bare": 3, "pp": 60, "pp-noepi": 61,
                                        "pp-inphase": 62, "pp-noepi-inphase": 63, "pp-noW": 64,
                                        "pp-noW-noepi": 65, "pp-bare": 69})}
-        if os.environ.get("PROBE") == "spol":
-            # default-policy (write-back) epilogue stores against the production non-temporal ones
-            var = {k: (c, o, {"prod": 0, "wb": 56}) for k, (c, o, _) in var.items()}
         # the ping-pong kernel is bitwise equal to the production kernel (same MFMA order)
         for cfg, o in ((32, out32), (31, img)) if os.environ.get("PROBE") != "pp" else ():
             o2 = torch.empty_like(o)
