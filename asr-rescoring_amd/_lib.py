@@ -14,7 +14,9 @@ import os
 import torch  # noqa: F401  (must load torch's HIP runtime before librescore.so)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(PKG_DIR, "librescore.so")
+# RS_LIBRESCORE: another in-tree build of the same library (A/B timing of two builds in one GPU
+# session, tools/lib_ab.sh); default the library build.py writes
+LIB_PATH = os.environ.get("RS_LIBRESCORE") or os.path.join(PKG_DIR, "librescore.so")
 
 RS_HEAD_MLM, RS_HEAD_CLS, RS_HEAD_EMB = 1, 2, 4
 RS_FUSE = {"norm": 0, "legacy": 1, "am_norm": 2}

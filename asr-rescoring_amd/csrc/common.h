@@ -52,14 +52,13 @@ struct EpiArgs {
     const float* res_b0;
     // EPI_LNRES_IMG: LN = (res_g, res_b, ln_eps) over nlog columns; lnx: lnres_granules(M)
     // 8-B granules [M/256][N/256][256][2] {ln_tag, sum | M2} (zeroed once by the owner); lncnt:
-    // 4 words, [0] the monotonic first-tile ticket counter (zeroed once by the owner); lnerr (sticky, the caller's):
-    // set to 1 when a statistics wait timed out; ln_tag: set by the launch
+    // lnres_counter_bytes() of gang-ticket words and gang-id slots (zeroed once by the owner, left
+    // zeroed by every launch); lnerr (sticky, the caller's): set to 1 when a statistics or gang wait
+    // timed out; ln_tag: set by the launch
     void* lnx;
     unsigned* lncnt;
     unsigned* lnerr;
     unsigned ln_tag;
-    unsigned ln_base;      // first ticket of this launch on lncnt[0] (ticket gangs; set by the launch)
-    unsigned* ln_next;     // host: the first ticket of the next launch on lncnt[0] (owned with lncnt)
     float ln_eps;
     int diag;              // EPI_LNRES_IMG timing diagnostics (RS_LNFUSE_DIAG; 0 in production)
 };
@@ -138,12 +137,9 @@ hipError_t launch_gemm(int epi, const f16* A, const f16* W, int M_pad, int N_pad
 // EPI_GELU_F16 (two-part image out, ep.nlog = N apart).  N_pad % 256 == 0, K % 32 == 0, K >= 64.
 hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_pad, int N_pad, int K,
                            const EpiArgs& ep, hipStream_t st);
-// the same with the epilogue overlapped by the other half of the workgroup (k_gemm_pp.hip):
-// EPI_BIAS_F32 or EPI_GELU_F16, K % 64 == 0
-hipError_t launch_gemm_pp(int epi, const f16* A, const f16* W, int ldw, int M_pad, int N_pad, int K, const EpiArgs& ep,
-                          hipStream_t st, int dv = 0);
 int gemm_row_align();   // M padding granularity required by launch_gemm
 int gemm_lnres_workgroups(int N_pad);   // grid of the fused residual + LayerNorm GEMM (whole gangs)
+size_t lnres_counter_bytes();           // EpiArgs.lncnt size
 
 // kx: width factor of the fp16 operand images written (1 or 3, see put_split);
 // qkv32: the QKV projection is fp32 (fp16x3 mode) instead of fp16.

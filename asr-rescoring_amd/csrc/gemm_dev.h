@@ -1,4 +1,4 @@
-// Device helpers shared by the GEMM kernels (k_gemm.hip, k_gemm_pp.hip).
+// Device helpers shared by the GEMM kernels (k_gemm.hip).
 #pragma once
 #include "common.h"
 

@@ -746,6 +746,118 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
 // Epilogues: EPI_BIAS_F32 (fp32 [M, ldc]), EPI_GELU_F16 (two-part GELU image, nlog apart),
 // EPI_BIAS_F16; bias added in the epilogue (its loads ride the last K-step).  Rows up to
 // M_pad are stored (the buffers are M_pad rows).
+// ---- LayerNorm-epilogue gangs: first-tile tickets (thread 0 of a workgroup) -------------------
+// Counter words of ep.lncnt (zeroed once by the owner; the last workgroup to finish a launch zeroes
+// them again, lnr_done, so each launch on the stream starts from zero — no host-side ticket state):
+enum : int {
+    LNC_TICKET = 0,        // global start-order ticket
+    LNC_DONE = 16,         // workgroups finished
+    LNC_LOCAL = 32,        // + 16 x: XCD x's local ticket (own 64-B line each)
+    LNC_STARTED = 160,     // workgroups that took their local ticket
+    LNC_OVF = 176,         // overflow ticket
+    LNC_GANGS = 192,       // gang ids handed out
+    LNC_WORDS = 256,
+    LNC_TAB = 128,         // u64 index of the gang-id slots {ln_tag, id}: [8][128] local, then [256] overflow
+    LNC_TAB_N = 8 * 128 + 256,
+};
+constexpr size_t lnr_counter_bytes() { return (size_t)LNC_TAB * 8 + (size_t)LNC_TAB_N * 8; }
+
+typedef __attribute__((address_space(1))) unsigned lgu32;
+typedef __attribute__((address_space(1))) unsigned long long lgu64;
+__device__ __forceinline__ unsigned lnr_add(unsigned* c, int w, unsigned v = 1u) {
+    return __hip_atomic_fetch_add((lgu32*)(c + w), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned lnr_ld(const unsigned* c, int w) {
+    return __hip_atomic_load((const lgu32*)(c + w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// XCD: gangs inside one XCD (its column tiles then read their shared A panel through one L2) —
+// XCD x's workgroups take local tickets in start order; every n_tiles_n consecutive local tickets
+// below cap = floor(floor(G / 8) / ntn) * ntn form a gang, the rest (and the members of a local gang
+// that can never fill: its XCD received fewer workgroups, seen once every workgroup of the grid has
+// taken its local ticket) form gangs from a global overflow ticket, again in start order.  With the
+// observed round-robin placement no workgroup waits for the grid to start; the protocol does not
+// depend on placement (HIP promises none).  Otherwise: gangs of consecutive global tickets.
+// A gang's member that completes it takes the gang id and publishes it tagged with ln_tag; the
+// others poll (bounded: a timeout sets the sticky error word and returns an id past the tiles).
+template <bool XCD>
+__device__ unsigned lnr_gang_ticket(const EpiArgs& ep, int ntn_) {
+    unsigned* c = ep.lncnt;
+    if constexpr (!XCD) return lnr_add(c, LNC_TICKET);
+    const unsigned ntn = (unsigned)ntn_, G = gridDim.x;
+    const unsigned long long tag = (unsigned long long)ep.ln_tag << 32;
+    unsigned long long* tab = (unsigned long long*)c + LNC_TAB;
+    const unsigned spin_max = (ep.diag & 8) ? (1u << 8) : (1u << 20);
+    auto join = [&](unsigned long long* slot, bool completes, unsigned& gid) -> bool {   // false: timed out
+        if (completes) {
+            gid = lnr_add(c, LNC_GANGS);
+            __hip_atomic_store((lgu64*)slot, tag | gid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return true;
+        }
+        for (unsigned spins = 0; spins < spin_max; ++spins) {
+            const unsigned long long v = __hip_atomic_load((const lgu64*)slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((v >> 32) == (tag >> 32)) {
+                gid = (unsigned)v;
+                return true;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        return false;
+    };
+    unsigned x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    x &= 7;
+    const unsigned cap = (G / 8) / ntn * ntn;
+    const unsigned lc = lnr_add(c, LNC_LOCAL + 16 * (int)x);
+    lnr_add(c, LNC_STARTED);                                  // after the local ticket
+    unsigned gid = 0, mem = 0;
+    bool ovf = lc >= cap, ok = true;
+    if (!ovf) {
+        const unsigned k = lc / ntn;
+        mem = lc - k * ntn;
+        unsigned long long* slot = tab + x * 128 + k;
+        if (mem + 1 == ntn) {
+            ok = join(slot, true, gid);
+        } else {
+            ok = false;
+            for (unsigned spins = 0; spins < spin_max; ++spins) {
+                const unsigned long long v = __hip_atomic_load((const lgu64*)slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((v >> 32) == (tag >> 32)) {
+                    gid = (unsigned)v;
+                    ok = true;
+                    break;
+                }
+                // every workgroup has its local ticket: XCD x's count is final
+                if (lnr_ld(c, LNC_STARTED) == G && lnr_ld(c, LNC_LOCAL + 16 * (int)x) < ntn * (k + 1)) {
+                    ovf = ok = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+        }
+    }
+    if (ovf && ok) {
+        const unsigned o = lnr_add(c, LNC_OVF), k = o / ntn;
+        mem = o - k * ntn;
+        ok = k < 256 && join(tab + 8 * 128 + k, mem + 1 == ntn, gid);
+    }
+    if (!ok) {
+        __hip_atomic_store((lgu32*)ep.lnerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return 0xffffffffu;
+    }
+    return gid * ntn + mem;
+}
+
+// End of a workgroup (thread 0): the last of the grid zeroes the counters for the next launch
+// (every workgroup has taken its tickets by then: each adds to LNC_DONE after its own).
+__device__ __forceinline__ void lnr_done(const EpiArgs& ep) {
+    unsigned* c = ep.lncnt;
+    if (lnr_add(c, LNC_DONE) + 1 != gridDim.x) return;
+    const int w[] = {LNC_TICKET, LNC_STARTED, LNC_OVF, LNC_GANGS, LNC_DONE};
+    for (int x = 0; x < 8; ++x) __hip_atomic_store((lgu32*)(c + LNC_LOCAL + 16 * x), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = 0; i < 5; ++i) __hip_atomic_store((lgu32*)(c + w[i]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 template <int EPI, int VAR>
 __global__ void __launch_bounds__(512)
 gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int ldw, int n_tiles_n, int n_tiles,
@@ -757,6 +869,13 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     constexpr int NSTORE = 32;                   // epilogue stores per wave per tile
     static_assert(EPI == EPI_BIAS_F32 || EPI == EPI_GELU_F16 || EPI == EPI_LNRES_IMG, "x3s epilogues");
     constexpr bool LNR = EPI == EPI_LNRES_IMG;
+    // VAR 268435456 (LayerNorm epilogue): the residual image is read during the K loop, one unit
+    // of NRU per K-step into RRU registers and added into the accumulators at the next step, so
+    // the epilogue no longer starts with a 256-KB read every CU issues at the same moment
+    constexpr bool KRES = LNR && (VAR & 268435456) != 0;
+    constexpr int NRU = (VAR & 536870912) ? 16 : 8;    // units: row blocks (8) or half blocks (16)
+    constexpr int RRU = NRU == 8 ? 4 : 2;               // uint4 registers per unit
+    constexpr bool EARLYG = (VAR & 1073741824) == 0;
     static_assert(!LNR || (VAR & 2) == 0, "the LayerNorm epilogue has no no-store diagnostic");
     static_assert((VAR & 16777216) == 0 || LNR, "the permuted-column layout is written for the LayerNorm epilogue");
     extern __shared__ __attribute__((aligned(16))) char smem[];        // the LDS-DMA ring (2 stages)
@@ -771,37 +890,21 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     int t = blockIdx.x;
     typedef __attribute__((address_space(1))) unsigned gu32;
     typedef __attribute__((address_space(1))) unsigned long long gu64;
-    if constexpr (LNR && (VAR & 134217728) != 0) {
-        // VAR 134217728: gangs formed inside XCD groups (blocks b, b + 8, ... share an XCD as
-        // dispatched; a different placement changes only speed): the workgroups of group x = b & 7
-        // take gangs of n_tiles_n consecutive positions p = b >> 3; the few left over in each
-        // group form the last gangs across groups.  A gang's column tiles then read their shared
-        // A panel through one L2.  Needs every workgroup resident: cooperative launch (RS_LNGANG=xcd).
-        const int G = gridDim.x, ntn = n_tiles_n, x = blockIdx.x & 7, pp = blockIdx.x >> 3;
-        int loc_before = 0, left_before = 0, nloc = 0, total_loc = 0;
-        for (int y = 0; y < 8; ++y) {
-            const int ny = G > y ? (G - y + 7) / 8 : 0, ly = ny / ntn * ntn;
-            if (y < x) {
-                loc_before += ly;
-                left_before += ny - ly;
-            }
-            if (y == x) nloc = ly;
-            total_loc += ly;
-        }
-        t = pp < nloc ? loc_before + pp : total_loc + left_before + (pp - nloc);
-    } else if constexpr (LNR) {
-        // first tiles by ticket, in the order workgroups start: each row panel's column tiles
-        // form a gang of workgroups that have all started (so the statistics exchange cannot
-        // wait on a workgroup that is not resident, at any residency), and a gang walks the
-        // panels p, p + G, p + 2G, ... (G = gangs) with each member keeping its column:
-        // t += gridDim.x.  The exchange (lnres_epilogue) is within a gang only.
-        if (tid == 0) {
-            // a monotonic counter: this launch's tickets start at ep.ln_base (kept by the host)
-            const unsigned c = __hip_atomic_fetch_add((gu32*)ep.lncnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            *(unsigned*)(slabs + 2048) = c - ep.ln_base;
-        }
+    if constexpr (LNR) {
+        // Gangs: a row panel's n_tiles_n column tiles are computed by n_tiles_n workgroups that
+        // exchange row statistics (lnres_epilogue), so a gang must consist of workgroups that have
+        // all STARTED: gangs are formed from tickets taken at start, never from blockIdx.  A gang
+        // (id g of G / ntn) walks the panels g, g + G / ntn, ...; member m keeps column tile m:
+        // first tile g * ntn + m, then t += gridDim.x.  lnr_gang_ticket (thread 0) returns g * ntn + m.
+        if (tid == 0) *(unsigned*)(slabs + 2048) = lnr_gang_ticket<(VAR & 134217728) != 0>(ep, n_tiles_n);
         __syncthreads();
         t = (int)*(const unsigned*)(slabs + 2048);
+    }
+    if ((unsigned)t >= (unsigned)n_tiles) {
+        if constexpr (LNR) {
+            if (tid == 0) lnr_done(ep);
+        }
+        return;
     }
     if ((unsigned)t >= (unsigned)n_tiles) return;
     // the younger wave half (waves 4-7, one per SIMD beside an older partner) at s_setprio 1
@@ -830,7 +933,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     const int pswz = ((lane & 3) ^ g16(prow >> 2)) * 8;
     const size_t ld2 = (size_t)2 * K;
     __amdgpu_buffer_rsrc_t rsA, rsW;
-    int voffA[4], voffW[4];                       // lane byte offsets: (p & 1) row half x (r & 1) hi / lo
+    int voffA, voffW;                             // lane byte offsets of row half 0, hi part
     // VAR 16777216: output columns permuted inside each 32-column group so that a lane's two
     // 16-column MFMA blocks 2m, 2m + 1 hold 8 CONSECUTIVE output columns (32 m + 8 q4 .. + 7)
     // instead of two runs of 4: W image row 32 m + 16 jj + 4 q + e is W row 32 m + 8 q + 4 jj + e.
@@ -839,13 +942,10 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     auto wperm = [](int L) {
         return PERM ? (L & ~31) | (((L >> 2) & 3) << 3) | (((L >> 4) & 1) << 2) | (L & 3) : L;
     };
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int l = 0; l < 2; ++l) {
-            voffA[2 * h + l] = ((prow + 128 * h) * (int)ld2 + l * K + pswz) * 2;
-            voffW[2 * h + l] = (wperm(prow + 128 * h) * ldw + l * K + pswz) * 2;
-        }
+    // row half 1 (+128 rows: wperm keeps the row's 32-group) and the lo part (+K) are uniform
+    // byte offsets added in the scalar offset, so one lane offset per operand
+    voffA = (prow * (int)ld2 + pswz) * 2;
+    voffW = (wperm(prow) * ldw + pswz) * 2;
     auto set_rsrc = [&](int m0, int n0) {
         rsA = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * ld2), (short)0, (int)(256 * ld2 * 2), 0x00020000);
         rsW = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (size_t)n0 * ldw), (short)0, 256 * ldw * 2, 0x00020000);
@@ -854,8 +954,8 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         if constexpr ((VAR & 1) != 0) return;     // diagnostic: no K-loop staging (stale tiles)
         const int r = p >> 1;
         auto* dst = (__attribute__((address_space(3))) void*)(smem + buf * STAGE + r * REG + ((p & 1) * 8 + wave) * 1024);
-        const int vo = (r < 2 ? voffA : voffW)[2 * (p & 1) + (r & 1)];
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 16, vo, k0 * 2, 0, 0);
+        const int so = ((p & 1) * 128 * (r < 2 ? (int)ld2 : ldw) + (r & 1) * K + k0) * 2;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 16, r < 2 ? voffA : voffW, so, 0, 0);
     };
     auto stage = [&](int buf, int k0) {
 #pragma unroll
@@ -877,15 +977,16 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     // the next step's eight DMA pieces ride this step's first MFMA groups (one per group of four
     // MFMAs of row half 0); the last step of a tile passes k0n = 2^29 and issues none
     auto kstep16 = [&](int buf, int k0n) {
+        // k0n opaque: the pieces' scalar offsets are formed here, not hoisted out of the peeled
+        // steps as dozens of live SGPR constants
+        asm volatile("" : "+s"(k0n));
         const char* sb = smem + buf * STAGE;
-        half8 wh[4], wl[4], wd[4];
+        half8 wh[4], wl[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             wh[j] = *(const half8*)(sb + offW16 + j * 1024);
             wl[j] = *(const half8*)(sb + offW16 + REG + j * 1024);
         }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) wd[j] = wh[j] * down;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             half8 ah[4], al[4];
@@ -900,15 +1001,26 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
 #pragma unroll
                     for (int ii = 0; ii < 4; ++ii) ah[ii] *= down;              // A_hi / 64
                 }
+                // groups of four MFMAs: product 1 (W_hi / 64 . A_lo·64) by column block, its factor
+                // formed right there (opaque to CSE: no 16 registers of W_hi / 64 held across the
+                // step), products 0 and 2 by row block; per accumulator the order of the three
+                // products is unchanged
 #pragma unroll
-                for (int ii = 0; ii < 4; ++ii) {
+                for (int g = 0; g < 4; ++g) {
+                    if (pr == 1) {
+                        half8 wdj = wh[g];
+                        asm volatile("" : "+v"(wdj));
+                        wdj *= down;                                            // W_hi / 64
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const half8 b = pr == 0 ? wh[j] : pr == 1 ? wd[j] : wl[j];
-                        const half8 a = pr == 1 ? al[ii] : ah[ii];
-                        acc16[4 * h + ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b, a, acc16[4 * h + ii][j], 0, 0, 0);
+                        for (int ii = 0; ii < 4; ++ii)
+                            acc16[4 * h + ii][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wdj, al[ii], acc16[4 * h + ii][g], 0, 0, 0);
+                    } else {
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+                            acc16[4 * h + g][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pr == 0 ? wh[j] : wl[j], ah[g],
+                                                                                         acc16[4 * h + g][j], 0, 0, 0);
                     }
-                    const int grp = 12 * h + 4 * pr + ii;
+                    const int grp = 12 * h + 4 * pr + g;
                     if (grp < 8 && k0n < (1 << 29)) {
                         __builtin_amdgcn_sched_barrier(0);
                         piece(buf ^ 1, k0n, grp);
@@ -925,13 +1037,38 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     stage(0, 0);
     int par = 0;                                                  // buffer of K-step 0
     bool first = true;
+    // KRES: residual image unit u of the tile (row block u of the wave tile, or half block u >> 1,
+    // column half u & 1) in the permuted-column accumulator layout: per row block ii and column half
+    // mm, 8 consecutive columns 32 mm + 8 q4 of the lane's row as one 16-B load per image (hi, lo·64)
+    uint4 rres[RRU];
+    auto res_load = [&](int u, int rm0, int rn0) __attribute__((always_inline)) {
+        const int ii = NRU == 8 ? u : u >> 1;
+        const f16* p = (const f16*)ep.out + (size_t)(rm0 + wm * WTM + 16 * ii + r16) * ep.ldc + rn0 + wn * WTN + 8 * q4;
+#pragma unroll
+        for (int k = 0; k < RRU / 2; ++k) {
+            const int mm = NRU == 8 ? k : (u & 1);
+            rres[2 * k] = *(const uint4*)(p + 32 * mm);
+            rres[2 * k + 1] = *(const uint4*)(p + 32 * mm + ep.nlog);
+        }
+    };
+    auto res_add = [&](int u) __attribute__((always_inline)) {      // u: a compile-time constant at every call
+        const int ii = NRU == 8 ? u : u >> 1;
+#pragma unroll
+        for (int k = 0; k < RRU / 2; ++k) {
+            const int mm = NRU == 8 ? k : (u & 1);
+            const half8 vh = __builtin_bit_cast(half8, rres[2 * k]);
+            const half8 vl = __builtin_bit_cast(half8, rres[2 * k + 1]);
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                acc16[ii][2 * mm + (e >> 2)][e & 3] += __builtin_fmaf((float)vl[e], X3_DOWN, (float)vh[e]);
+        }
+    };
     for (;;) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc16[i][j] = (f32x4)(0.f);
-        for (int kt = 0; kt < nk; ++kt) {
-            const int cur = (par + kt) & 1;
+        auto kstep_full = [&](int kt) __attribute__((always_inline)) {
             // step kt landed for this wave (at a tile's first step the previous tile's stores
             // are younger and stay in flight); the barrier: landed for every wave, and every
             // wave is done reading step kt-1's buffer, which now receives step kt+1
@@ -941,7 +1078,29 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             asm volatile("s_barrier" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
-            kstep16(cur, kt + 1 < nk ? (kt + 1) * BK : (1 << 29));
+        };
+        int kt0 = 0;
+        if constexpr (KRES) {
+            // the first NRU + 1 K-steps peeled (acc16 indices must be compile-time): step u adds
+            // unit u - 1 (landed with that step's vmcnt(0)) and issues unit u's loads; with fewer
+            // K-steps than units the rest of the residual is loaded and added without a step
+#pragma unroll
+            for (int u = 0; u <= NRU; ++u) {
+                const bool step = u < nk;
+                if (step) kstep_full(u);
+                if (u >= 1) res_add(u - 1);
+                if (u < NRU) res_load(u, m0, n0);
+                __builtin_amdgcn_sched_barrier(0);
+                if (step) {
+                    kstep16((par + u) & 1, u + 1 < nk ? (u + 1) * BK : (1 << 29));
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+            kt0 = NRU + 1;
+        }
+        for (int kt = kt0; kt < nk; ++kt) {
+            kstep_full(kt);
+            kstep16((par + kt) & 1, kt + 1 < nk ? (kt + 1) * BK : (1 << 29));
             __builtin_amdgcn_sched_barrier(0);
         }
         // ---- transition
@@ -951,13 +1110,25 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         // the wave's 64): only the bias loads are outstanding here (the last K-step issued no
         // DMA), so one vmcnt(0) waits for exactly them; inline asm keeps the compiler from placing
         // its own wait
-        f32x4 bq[4];
+        f32x4 bq[4], gq[4], bb[4];               // bias; (KRES) LayerNorm weight / bias of the lane's columns
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const float* bp = ep.bias + cn0 + wn * WTN + (PERM ? 32 * (j >> 1) + 8 * q4 + 4 * (j & 1) : 16 * j + 4 * q4);
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bq[j]) : "v"(bp) : "memory");
+            const int cj = cn0 + wn * WTN + (PERM ? 32 * (j >> 1) + 8 * q4 + 4 * (j & 1) : 16 * j + 4 * q4);
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bq[j]) : "v"(ep.bias + cj) : "memory");
+            if constexpr (KRES && EARLYG) {
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(gq[j]) : "v"(ep.res_g + cj) : "memory");
+                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bb[j]) : "v"(ep.res_b + cj) : "memory");
+            }
         }
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]) : : "memory");
+        if constexpr (KRES && EARLYG) {
+            asm volatile("s_waitcnt vmcnt(0)"
+                         : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]), "+v"(gq[0]), "+v"(gq[1]), "+v"(gq[2]),
+                           "+v"(gq[3]), "+v"(bb[0]), "+v"(bb[1]), "+v"(bb[2]), "+v"(bb[3])
+                         :
+                         : "memory");
+        } else {
+            asm volatile("s_waitcnt vmcnt(0)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]) : : "memory");
+        }
         // the next tile's stage 0 (into the buffer step nk-2 used) lands while this epilogue runs
         // (issuing it after the LayerNorm epilogue's residual loads instead, so that their waits
         // need not cover this DMA, measured -2.7 %: profiles/r3p2_lnperm_ab.txt)
@@ -990,18 +1161,24 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 const f16* img = (const f16*)ep.out;
                 const int c0 = cn0 + wn * WTN + 4 * q4;
                 // x = (acc + bias) + h, the residual image h = hi + lo/64 read in the accumulator
-                // layout, four row blocks at a time (as ln_res_img forms it)
-                // (loading it costs ~3 % of the step at C3 — 256 KB per tile at the ~50 GB/s one CU
-                // streams, RS_LNFUSE_DIAG=4 — and prefetching half of it beside the bias loads
-                // measured no better; the permuted-column layout (PERM) halves its load count:
-                // +1.1 % end to end)
+                // layout.  KRES: h is already in the accumulators (added during the K loop).  Else
+                // read here, four row blocks at a time (as ln_res_img forms it) — every CU issues
+                // its 256 KB at the same moment (~3 % of the step at C3); the permuted-column layout
+                // (PERM) halves its load count: +1.1 % end to end
+                if constexpr (KRES) {
+#pragma unroll
+                    for (int i = 0; i < 8; ++i)
+#pragma unroll
+                        for (int j = 0; j < 4; ++j)
+#pragma unroll
+                            for (int e = 0; e < 4; ++e) acc16[i][j][e] += bq[j][e];
+                } else {
 #pragma unroll
                 for (int hh = 0; hh < 2; ++hh) {
                     half4 rh0[4][4], rl0[4][4];
-                    const int rskip = (ep.diag & 4) ? 0 : 1;     // diag 4 (timing only): the tile's first rows
 #pragma unroll
                     for (int ii = 0; ii < 4; ++ii) {
-                        const f16* prow_img = img + (size_t)(cm0 + rskip * (wm * WTM + 16 * (4 * hh + ii) + r16)) * ldc;
+                        const f16* prow_img = img + (size_t)(cm0 + wm * WTM + 16 * (4 * hh + ii) + r16) * ldc;
                         if constexpr (PERM) {
                             // blocks 2m, 2m + 1: 8 consecutive columns, one 16-B load per image
 #pragma unroll
@@ -1030,6 +1207,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                             for (int e = 0; e < 4; ++e)
                                 acc16[4 * hh + ii][j][e] = (acc16[4 * hh + ii][j][e] + bq[j][e]) +
                                                            ((float)rh0[ii][j][e] + (float)rl0[ii][j][e] * X3_DOWN);
+                }
                 }
                 // row partials over the wave's 64 columns (lanes l, l^16, l^32, l^48 share a row),
                 // then over the four waves of the row half through their slabs
@@ -1097,7 +1275,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         __hip_atomic_store((gu64*)g, tag | __float_as_uint(a), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                         __hip_atomic_store((gu64*)(g + 1), tag | __float_as_uint(b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
-                    float ps[2][4], pq[2][4];           // (diag 1: own partials only — no exchange)
+                    float ps[2][4], pq[2][4];
                     for (unsigned spins = 0;;) {
                         bool ok = true;
 #pragma unroll
@@ -1106,7 +1284,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                             for (int c = 0; c < 4; ++c) {
                                 ps[k][c] = os[k];
                                 pq[k][c] = oq[k];
-                                if (c < ntn && c != tcol && !(ep.diag & 1)) {
+                                if (c < ntn && c != tcol) {
                                     const u64* g = gx + ((size_t)c * BM + lane + 64 * k) * 2;
                                     const u64 va = __hip_atomic_load((const gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                                     const u64 vb = __hip_atomic_load((const gu64*)(g + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1125,17 +1303,16 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                     }
 #pragma unroll
                     for (int k = 0; k < 2; ++k) {
-                        const int c_lo = (ep.diag & 1) ? tcol : 0, c_hi = (ep.diag & 1) ? tcol + 1 : ntn;
-                        const float inv_n = (ep.diag & 1) ? 1.f / BM : 1.f / H;
+                        const float inv_n = 1.f / H;
                         float tot = 0.f;
 #pragma unroll
                         for (int c = 0; c < 4; ++c)
-                            if (c >= c_lo && c < c_hi) tot += ps[k][c];
+                            if (c < ntn) tot += ps[k][c];
                         const float mean = tot * inv_n;
                         float m2 = 0.f;
 #pragma unroll
                         for (int c = 0; c < 4; ++c) {
-                            if (c >= c_lo && c < c_hi) {
+                            if (c < ntn) {
                                 const float d = ps[k][c] * (1.f / BM) - mean;
                                 m2 += __builtin_fmaf((float)BM * d, d, pq[k][c]);
                             }
@@ -1144,12 +1321,13 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                     }
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-                f32x4 gq[4], bb[4];                      // LayerNorm weight / bias of the lane's columns
+                if constexpr (!(KRES && EARLYG)) {                   // (KRES: loaded with the bias)
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const int cj = PERM ? cn0 + wn * WTN + 32 * (j >> 1) + 8 * q4 + 4 * (j & 1) : c0 + 16 * j;
-                    gq[j] = *(const f32x4*)(ep.res_g + cj);
-                    bb[j] = *(const f32x4*)(ep.res_b + cj);
+                    for (int j = 0; j < 4; ++j) {
+                        const int cj = PERM ? cn0 + wn * WTN + 32 * (j >> 1) + 8 * q4 + 4 * (j & 1) : c0 + 16 * j;
+                        gq[j] = *(const f32x4*)(ep.res_g + cj);
+                        bb[j] = *(const f32x4*)(ep.res_b + cj);
+                    }
                 }
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
@@ -1235,6 +1413,9 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             par = last ^ 1;
             first = false;
     }
+    if constexpr (LNR) {
+        if (tid == 0) lnr_done(ep);
+    }
 }
 
 // Sequence number of a LayerNorm-epilogue launch (the granule tag), process-wide: never 0.
@@ -1269,7 +1450,7 @@ hipError_t smem_attr_once(const void* fn, int smem, std::atomic<unsigned>& devs)
 
 template <int EPI, int VAR = 0>
 hipError_t launch_x3s(const f16* A, const f16* W, int M_pad, int N_pad, int K, const EpiArgs& ep, hipStream_t st,
-                      int ldw = 0, bool coop = false) {
+                      int ldw = 0) {
     constexpr int smem = 2 * 65536;                  // ring (2 x 64 KiB); + 32 KiB static wave slabs
     if (K % 32 || K < 64 || M_pad % 256 || N_pad % 256) return hipErrorInvalidValue;
     static std::atomic<unsigned> attr_devs{0};      // devices whose LDS limit is raised
@@ -1279,7 +1460,7 @@ hipError_t launch_x3s(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
     int grid = n_tiles <= cus ? n_tiles : cus;
     if constexpr (EPI == EPI_LNRES_IMG) {
         // the image is rewritten in place over whole rows (N_pad = the hidden size, <= 4 column
-        // tiles); the claim / arrival words start at zero every launch
+        // tiles); the ticket words are zero at every launch (lnr_done)
         if (!ep.lnx || !ep.lncnt || !ep.lnerr || N_pad > 1024 || ep.nlog != N_pad || ep.ldc != 2 * N_pad)
             return hipErrorInvalidValue;
         // whole row panels per round: the first tiles form complete gangs (every workgroup
@@ -1295,28 +1476,10 @@ hipError_t launch_x3s(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
         // kernel (ln_tag_next): the O-projection and BertOutput instances share the granule buffer,
         // and per-instance counters would repeat each other's tags
         e2.ln_tag = ln_tag_next();
-        // the ticket counter is never reset: every workgroup of every ticket launch on it takes
-        // exactly one ticket, so this launch's first ticket is the sum of the earlier grids
-        if constexpr ((VAR & 134217728) == 0) {
-            if (!ep.ln_next) return hipErrorInvalidValue;
-            e2.ln_base = *ep.ln_next;
-            *ep.ln_next += (unsigned)grid;
-        }
     }
     const int ldw2 = ldw > 0 ? ldw : 2 * K;
-    if (coop) {
-        // the XCD-group gangs (VAR 134217728) take their membership from blockIdx, so every
-        // workgroup of the grid must be resident at once: a cooperative launch makes the runtime
-        // check the grid against the kernel's occupancy up front (hipErrorCooperativeLaunchTooLarge)
-        void* args[] = {(void*)&A, (void*)&W, (void*)&K, (void*)&ldw2, (void*)&ntn, (void*)&n_tiles, (void*)&e2};
-        return hipLaunchCooperativeKernel((const void*)gemm_x3s_kernel<EPI, VAR>, dim3(grid), dim3(512), args, smem, st);
-    }
     hipLaunchKernelGGL((gemm_x3s_kernel<EPI, VAR>), dim3(grid), dim3(512), smem, st, A, W, K, ldw2, ntn, n_tiles, e2);
-    const hipError_t e = hipGetLastError();
-    if constexpr (EPI == EPI_LNRES_IMG && (VAR & 134217728) == 0) {
-        if (e != hipSuccess) *ep.ln_next -= (unsigned)grid;     // no workgroup took a ticket
-    }
-    return e;
+    return hipGetLastError();
 }
 
 template <int EPI, int VAR = 0>
@@ -1405,6 +1568,8 @@ hipError_t launch_epi(const f16* A, const f16* W, int M_pad, int N_pad, int K, c
 
 int gemm_row_align() { return 256; }
 
+size_t lnres_counter_bytes() { return lnr_counter_bytes(); }
+
 // Workgroups of one fused residual + LayerNorm GEMM launch (EPI_LNRES_IMG): whole gangs of the
 // N_pad / 256 column tiles of a row panel, at one workgroup per CU.  A launch over P row panels
 // runs ceil(P / gangs) rounds of panels, so the host cuts its chunks at multiples of
@@ -1427,24 +1592,31 @@ hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_p
             // Output columns permuted inside 32-column groups (VAR 16777216: 16-B epilogue loads,
             // +1.1 % end to end, profiles/r3p2_lnperm_ab.txt); VAR 67108864 is a name tag only (the
             // BertOutput launch, K = 3072), so rocprofv3 reports the two instances separately.
-            // Gang formation (RS_LNGANG, read per call):
-            //   "ticket" (default): gangs of consecutive start-order tickets.  Deadlock-free at ANY
-            //       residency (a gang's members have all started before the next gang forms; complete
-            //       gangs finish and free their CUs), so a GPU shared with other kernels or processes
-            //       only slows the launch down.
-            //   "xcd": gangs inside XCD groups from blockIdx (VAR 134217728; a panel's column tiles
-            //       share one L2: BertOutput fetch 26.4 -> 20.0 KB per row, profiles/r3g2_lngang_xcd.txt).
-            //       Needs the whole grid resident; launched cooperatively, so the runtime refuses a
-            //       grid the occupancy does not admit.
+            // Gang formation (RS_LNGANG, read per call; lnr_gang_ticket): "ticket" = consecutive
+            // start-order tickets; "xcd" = start-order tickets inside each XCD (VAR 134217728; a
+            // panel's column tiles share one L2), the rest from an overflow ticket.  Either way a
+            // gang's members have all started before it exchanges statistics.  The exchange needs
+            // ntn (= N_pad / 256) workgroups of the gang co-resident — anywhere on the GPU for
+            // "ticket", on one XCD for "xcd" (or once the grid has started, anywhere): with fewer
+            // free slots the bounded wait ends the call in RS_EHIP instead of hanging.
             const char* g = getenv("RS_LNGANG");
             const bool xcd = g && !strcmp(g, "xcd");
-            constexpr int VL = 16777216;
+            // RS_LNKRES (A/B, read per call): 0 = residual read in the epilogue, 1 = during the K
+            // loop by row blocks (default), 2 = by half row blocks
+            const char* kr = getenv("RS_LNKRES");
+            const int kres = kr ? atoi(kr) : 1;
+            constexpr int VL = 16777216, KR1 = 268435456 | 1073741824, KR2 = 268435456 | 536870912 | 1073741824;
+#define RS_LNR(V_)                                                                                \
+    (kres == 0   ? launch_x3s<EPI_LNRES_IMG, (V_)>(A, W, M_pad, N_pad, K, ep, st, ldw)               \
+     : kres == 2 ? launch_x3s<EPI_LNRES_IMG, (V_) | KR2>(A, W, M_pad, N_pad, K, ep, st, ldw)         \
+                 : launch_x3s<EPI_LNRES_IMG, (V_) | KR1>(A, W, M_pad, N_pad, K, ep, st, ldw))
             if (xcd) {
-                if (K > 1024) return launch_x3s<EPI_LNRES_IMG, VL | 67108864 | 134217728>(A, W, M_pad, N_pad, K, ep, st, ldw, true);
-                return launch_x3s<EPI_LNRES_IMG, VL | 134217728>(A, W, M_pad, N_pad, K, ep, st, ldw, true);
+                if (K > 1024) return RS_LNR(VL | 67108864 | 134217728);
+                return RS_LNR(VL | 134217728);
             }
-            if (K > 1024) return launch_x3s<EPI_LNRES_IMG, VL | 67108864>(A, W, M_pad, N_pad, K, ep, st, ldw);
-            return launch_x3s<EPI_LNRES_IMG, VL>(A, W, M_pad, N_pad, K, ep, st, ldw);
+            if (K > 1024) return RS_LNR(VL | 67108864);
+            return RS_LNR(VL);
+#undef RS_LNR
         }
     }
     return hipErrorInvalidValue;
@@ -1477,8 +1649,7 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
     hipError_t e = hipErrorInvalidValue;
     if (M % 256 || N % 256 || K % 64) return -1;
     if (cfg == 31 || cfg == 32) {  // split-operand fp16x3 (A [M, 2K], W [N, 2K] images): 31 GELU image, 32 fp32
-        // dbg: 0 production, 60 the ping-pong kernel (k_gemm_pp.hip); timing diagnostics of
-        // gemm_x3s_kernel (wrong results): 1 no K-loop staging, 2 no epilogue stores (20 / 52:
+        // dbg: 0 production; timing diagnostics of gemm_x3s_kernel (wrong results): 1 no K-loop staging, 2 no epilogue stores (20 / 52:
         // the same, round-3 / round-4 probe numbering), 3 neither, 50 DMA never waited for (the
         // next tile never waits for this tile's stores), 51 stores onto row panel 0 (no HBM write
         // burst), 53 both
@@ -1489,12 +1660,6 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
     (cfg == 31 ? launch_x3s<EPI_GELU_F16, VAR_>(a, w, M, N, K, ep, st) : launch_x3s<EPI_BIAS_F32, VAR_>(a, w, M, N, K, ep, st))
         switch (dbg) {
             case 0: e = launch_gemm_x3s(epi, a, w, 2 * K, M, N, K, ep, st); break;
-            case 60: e = launch_gemm_pp(epi, a, w, 2 * K, M, N, K, ep, st); break;
-            // ping-pong timing diagnostics (fp32 output): 61 no epilogue stores, 62 halves in
-            // phase, 63 both, 64 no W loads, 65 no W loads + no stores, 69 no loads at all + no stores
-            case 61: case 62: case 63: case 64: case 65: case 69:
-                e = launch_gemm_pp(epi, a, w, 2 * K, M, N, K, ep, st, dbg == 69 ? 13 : dbg - 60);
-                break;
             case 1: e = RS_X3(1); break;
             case 2: case 20: case 52: e = RS_X3(2); break;
             case 3: e = RS_X3(3); break;

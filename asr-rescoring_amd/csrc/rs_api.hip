@@ -83,9 +83,8 @@ struct rs_model {
     int kx = 1;                 // fp16 operand image width (1: fp16, 3: fp16x3)
     DevBuf xst, h16, t32, qkv, ctx, inter;   // xst: (mean, rstd) of the pre-LN rows in t32
     DevBuf xst1;                // statistics of the post-attention stream (deferred residual)
-    DevBuf lnx, lncnt, lnerr;   // EPI_LNRES_IMG: per-tile row statistics, the monotonic ticket
-                                // counter, sticky statistics-wait timeout flag
-    unsigned ln_next = 0;       // first ticket of the next ticket-gang launch (host copy of lncnt[0])
+    DevBuf lnx, lncnt, lnerr;   // EPI_LNRES_IMG: per-tile row statistics, gang-ticket words (left
+                                // zeroed by every launch), sticky statistics-wait timeout flag
     DevBuf ctxq, resq, tq32, hq32, hq16, interq, lab, llog, part, rowlp_tmp;
     DevBuf meta, hypoff;
     f16* emb_dst = nullptr;     // MODE_EMB output (rs_token_embed / rs_bertscore_recall)
@@ -100,6 +99,11 @@ struct rs_model {
     int* pinned = nullptr;
     size_t pinned_cap = 0;
     hipEvent_t upload_done = nullptr;
+    // call ordering across streams: the end of the last call's work (any stream); a call on another
+    // stream first makes its stream wait for it (CallOrder)
+    hipEvent_t call_done = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool have_last = false;
     // profiling
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -222,6 +226,25 @@ int begin_call(rs_model* m, hipStream_t st) {
     return RS_OK;
 }
 
+// Calls on one model handle are ordered, whatever streams they come on: the handle's workspace,
+// LayerNorm gang tickets and flags are shared by every call, so a call on a different stream than the
+// previous call first makes its stream wait (device-side, hipStreamWaitEvent) for the previous call's
+// work, and every call records the end of its own work.  Host threads must still not share a handle.
+struct CallOrder {
+    rs_model* m;
+    hipStream_t st;
+    CallOrder(rs_model* m_, hipStream_t st_) : m(m_), st(st_) {
+        if (m->have_last && st != m->last_stream && m->call_done) (void)hipStreamWaitEvent(st, m->call_done, 0);
+    }
+    ~CallOrder() {
+        if (!m->call_done && hipEventCreateWithFlags(&m->call_done, hipEventDisableTiming) != hipSuccess) return;
+        if (hipEventRecord(m->call_done, st) == hipSuccess) {
+            m->last_stream = st;
+            m->have_last = true;
+        }
+    }
+};
+
 int reserve_impl(rs_model* m, int64_t max_rows) {
     const rs_bert_cfg& c = m->cfg;
     if (max_rows < 512) return fail(RS_EARG, "max_rows must be >= 512");
@@ -239,9 +262,8 @@ int reserve_impl(rs_model* m, int64_t max_rows) {
     HIPTRY(m->lnx.ensure(lnres_granules((int)M) * 8));
     HIPTRY(hipMemset(m->lnx.p, 0, m->lnx.bytes));               // granule tags start at 0 (never a launch's)
     if (!m->lncnt.p) {
-        HIPTRY(m->lncnt.ensure(16));
-        HIPTRY(hipMemset(m->lncnt.p, 0, 16));
-        m->ln_next = 0;
+        HIPTRY(m->lncnt.ensure(lnres_counter_bytes()));
+        HIPTRY(hipMemset(m->lncnt.p, 0, m->lncnt.bytes));
     }
     HIPTRY(m->lnerr.ensure(16));
     HIPTRY(hipMemset(m->lnerr.p, 0, 16));
@@ -373,13 +395,6 @@ bool x3s_imgres_on() {
 // RS_LNFUSE (image-held residual; default 1): the residual add + LayerNorm of both blocks run in
 // the O-projection / BertOutput GEMM epilogues (EPI_LNRES_IMG: full rows through an in-launch
 // exchange of row statistics) instead of as ln_res_img passes (RS_LNFUSE=0).  Read per call.
-// RS_PP (split-operand layers; read per call): 1 = the QKV and BertIntermediate projections on
-// the ping-pong kernel (k_gemm_pp.hip: the epilogue of one half of the workgroup overlapped by
-// the other half's K loop), 0 = gemm_x3s_kernel.  Bitwise equal results.
-bool pp_on() {
-    const char* e = getenv("RS_PP");
-    return e && !strcmp(e, "1");
-}
 bool lnfuse_on(const rs_bert_cfg& cf) {
     const char* e = getenv("RS_LNFUSE");
     return !(e && !strcmp(e, "0")) && cf.hidden % 256 == 0 && cf.hidden <= 1024;
@@ -426,10 +441,7 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
         e.m_valid = m_valid;
         ProfScope ps(m, st, kind, 2.0 * m_valid * (double)n_flop_cols * 3.0 * K);
         const int M_pad = (m_valid + al - 1) / al * al;
-        if ((epi == EPI_BIAS_F32 || epi == EPI_GELU_F16) && K % 64 == 0 && pp_on())
-            HIPTRY(launch_gemm_pp(epi, A, W, ldw, M_pad, N, K, e, st));
-        else
-            HIPTRY(launch_gemm_x3s(epi, A, W, ldw, M_pad, N, K, e, st));
+        HIPTRY(launch_gemm_x3s(epi, A, W, ldw, M_pad, N, K, e, st));
         return RS_OK;
     };
     auto gelu_ep = [&](const float* bias, f16* out) {
@@ -497,11 +509,10 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
                 EpiArgs e{};
                 e.bias = bias; e.out = h16; e.ldc = 2 * H; e.nlog = H; e.res_g = g; e.res_b = be;
                 e.ln_eps = cf.ln_eps; e.lnx = m->lnx.p; e.lncnt = m->lncnt.as<unsigned>();
-                e.ln_next = &m->ln_next;
                 e.lnerr = m->lnerr.as<unsigned>();
-                // RS_LNFUSE_DIAG (tests / timing only; read per call): 8 = the statistics wait
-                // times out at once (the RS_EHIP path)
-                e.diag = getenv("RS_LNFUSE_DIAG") ? atoi(getenv("RS_LNFUSE_DIAG")) : 0;
+                // RS_LNFUSE_DIAG=8 (tests; read per call): every statistics / gang wait times out at
+                // once (the RS_EHIP path); no other bit is honoured (no diagnostic changes scores)
+                e.diag = (getenv("RS_LNFUSE_DIAG") ? atoi(getenv("RS_LNFUSE_DIAG")) : 0) & 8;
                 return e;
             };
             if (lnfuse) {
@@ -920,6 +931,8 @@ int rs_pll_score(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, in
                  double* d_pll, float* d_row_lp, void* stream) {
     if (!m || !h_hyp_off || n_hyp < 0 || (n_hyp > 0 && (!d_tok || !d_pll))) return fail(RS_EARG, "null argument");
     hipStream_t st = (hipStream_t)stream;
+    if (n_hyp > 0) HIPTRY(hipSetDevice(m->device));
+    CallOrder order(m, st);
     SeqList sl;
     std::vector<int> hso(n_hyp + 1, 0);
     for (int h = 0; h < n_hyp; ++h) {
@@ -949,6 +962,8 @@ int rs_masked_logprob(rs_model* m, const int32_t* d_ids, const int32_t* h_seq_of
     if (!m || !h_seq_off || !h_query || n_seq < 0 || (n_seq > 0 && (!d_ids || !d_label || !d_out)))
         return fail(RS_EARG, "null argument");
     if (n_seq == 0) return RS_OK;
+    HIPTRY(hipSetDevice(m->device));
+    CallOrder order(m, (hipStream_t)stream);
     SeqList sl;
     for (int s = 0; s < n_seq; ++s) {
         const int o = h_seq_off[s], T = h_seq_off[s + 1] - o;
@@ -963,6 +978,8 @@ int rs_cls_score(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, in
                  float* d_out, void* stream) {
     if (!m || !h_hyp_off || n_hyp < 0 || (n_hyp > 0 && (!d_tok || !d_out))) return fail(RS_EARG, "null argument");
     if (n_hyp == 0) return RS_OK;
+    HIPTRY(hipSetDevice(m->device));
+    CallOrder order(m, (hipStream_t)stream);
     SeqList sl;
     for (int h = 0; h < n_hyp; ++h) {
         const int o = h_hyp_off[h], T = h_hyp_off[h + 1] - o;
@@ -977,6 +994,8 @@ int rs_token_embed(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, 
                    void* d_emb, void* stream) {
     if (!m || !h_hyp_off || n_hyp < 0 || (n_hyp > 0 && (!d_tok || !d_emb))) return fail(RS_EARG, "null argument");
     if (n_hyp == 0) return RS_OK;
+    HIPTRY(hipSetDevice(m->device));
+    CallOrder order(m, (hipStream_t)stream);
     SeqList sl;
     for (int h = 0; h < n_hyp; ++h) {
         const int o = h_hyp_off[h], T = h_hyp_off[h + 1] - o;
@@ -1008,6 +1027,7 @@ int rs_bertscore_recall(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_
             return fail(RS_EARG, "hypothesis " + std::to_string(h) + " has fewer than 2 tokens ([CLS] [SEP])");
     hipStream_t st = (hipStream_t)stream;
     HIPTRY(hipSetDevice(m->device));
+    CallOrder order(m, st);
     const int H = m->cfg.hidden;
     const size_t n_tok = (size_t)h_hyp_off[n_hyp];
     const bool two = m->kx == 3;                 // fp16x3: two-part embeddings, split-operand cosines
@@ -1067,6 +1087,7 @@ int rs_model_set_sync_check(rs_model* m, int on) {
 int rs_check(rs_model* m, void* stream) {
     if (!m) return fail(RS_EARG, "null model");
     HIPTRY(hipSetDevice(m->device));
+    CallOrder order(m, (hipStream_t)stream);
     return report_flags(m, (hipStream_t)stream, "scores");
 }
 
@@ -1102,6 +1123,7 @@ void rs_model_destroy(rs_model* m) {
     if (m->pinned_flag) (void)hipHostFree(m->pinned_flag);
     if (m->plan_done) (void)hipEventDestroy(m->plan_done);
     if (m->upload_done) (void)hipEventDestroy(m->upload_done);
+    if (m->call_done) (void)hipEventDestroy(m->call_done);
     for (hipEvent_t e : m->ev_pool) (void)hipEventDestroy(e);
     delete m;
 }

@@ -9,6 +9,9 @@ The corpus-CER numerators of the sweep (rs_ref_edit + rs_corpus_edits) depend on
 argmax and the fixed reference texts; they run once after the timed loop (the `rerank` block),
 as rescore.py computes them once per weight.
 Every rank scores its own U utterances (weak scaling; utterances are independent).
+``--workload c4``: BASELINE config C4 instead — the full 7176-utterance real-length set at N=100
+(alfred test length histogram), one fixed set split over the ranks (strong scaling).
+The default C3 run also reports ``c4_secondary``: one pass of that full C4 set on rank 0 at N=1.
 
 Prints ONE JSON line on rank 0.  Extra legs (not in the timed region): a HIP-event
 per-kernel-kind profile pass (roofline of the dominant kernel) and a bounded CPU
@@ -53,12 +56,72 @@ def _cpu_model() -> str:
     return "unknown"
 
 
+def c4_set():
+    """BASELINE config C4's input: 7176 utterances x N=100 at the alfred test set's real hypothesis
+    lengths (tests/golden/alfred_test_lengths.json, the length histogram of the reference's data)."""
+    lc = json.load(open(os.path.join(REPO, "tests", "golden", "alfred_test_lengths.json")))["length_counts"]
+    lengths = np.repeat(np.arange(len(lc)), lc).astype(np.int64)
+    return D.synthetic_nbest(7176, 100, seed=1, lengths=lengths, hard=True)
+
+
 def forward_flops(T: int, s=BERT_BASE) -> float:
     """Canonical algorithmic FLOPs of one MLM_PLL masked forward at length T."""
     H, F, V, nl = s.hidden, s.intermediate, s.vocab, s.layers
     dense = 2 * (4 * H * H + 2 * H * F)
     return float((nl - 1) * (T * dense + 4 * T * T * H) + 4 * T * H * H
                  + (2 * H * H + 4 * T * H + 2 * H * H + 4 * H * F) + 2 * (H * H + H * V))
+
+
+def c4_secondary(scorer, weights, device, cpu_model=None):
+    """One timed pass of the full C4 set (7176 x N=100, real lengths) through the headline scorer
+    (warm: the scorer has run the C3 steps), the 101-weight HIP fusion sweep and corpus CER on its
+    scores, and the rerank argmax over all 101 weights from the CPU reference's own lm (the oracle's
+    restatement of the reference work pattern) against the HIP lm on the two utterances nearest the
+    set's median utterance cost."""
+    from asr_rescoring_amd import shard
+    from oracle import rescore_ref as RR
+    import oracle.bert_ref as OB
+    t_gen = time.perf_counter()
+    nb4 = c4_set()
+    t_gen = time.perf_counter() - t_gen
+    d4 = torch.from_numpy(nb4.tokens).to(torch.device("cuda", device))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    lm4 = scorer.score_nbest(d4, nb4.hyp_off)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    lm_np = lm4.double().cpu().numpy()
+    Nb = 100
+    bw, bcer, _arg, cers = rerank.find_best_weight(nb4, lm_np, n_best=Nb, device=device)
+    # oracle-lm rerank check on two whole utterances
+    model = cpu_model if cpu_model is not None else OB.TorchBert(weights, BERT_BASE)
+    cost = shard.utterance_costs(nb4).astype(np.float64)
+    pick = [int(u) for u in np.argsort(np.abs(cost - np.median(cost)), kind="stable")[:2]]
+    idx = [nb4.utt_off[u] + i for u in pick for i in range(Nb)]
+    ref_lm, rel = [], []
+    for hh in idx:
+        sub_off = nb4.hyp_off[hh:hh + 2] - nb4.hyp_off[hh]
+        _, ref_pll = OB.pll_reference_pattern(model, nb4.tokens[nb4.hyp_off[hh]:nb4.hyp_off[hh + 1]], sub_off,
+                                              batch_size=32, full_head=True)
+        ref_lm.append(float(ref_pll[0]))
+        rel.append(abs(lm_np[hh] - ref_pll[0]) / abs(ref_pll[0]))
+    am_s = nb4.am[idx].reshape(2, Nb)
+    hyps_s = [[nb4.hyp_words(nb4.utt_off[u] + i) for i in range(Nb)] for u in pick]
+    refs_s = [nb4.refs[u] for u in pick]
+    _, _, arg_ref = RR.find_best_weight(am_s, np.asarray(ref_lm).reshape(2, Nb), hyps_s, refs_s, Nb)
+    _, _, arg_hip = RR.find_best_weight(am_s, lm_np[idx].reshape(2, Nb), hyps_s, refs_s, Nb)
+    lens = np.diff(nb4.hyp_off)
+    del d4
+    return {"workload": "C4 MLM_PLL full PLL, full 7176-utterance set x N=100, alfred real lengths, 1 GPU",
+            "value": round(nb4.n_forwards() / dt, 2), "unit": "masked fwd/s", "seconds": round(dt, 3),
+            "forwards": int(nb4.n_forwards()), "hypotheses": int(nb4.n_hyp),
+            "mean_T": round(float(np.average(lens, weights=lens - 2)), 2), "dtype": "fp16x3-split (fp32-accurate)",
+            "timing": "one pass, scorer warm from the C3 steps; input generation excluded",
+            "input_generation_seconds": round(t_gen, 1),
+            "rerank": {"best_weight": round(bw, 2), "cer": bcer, "am_only_cer": float(cers[0]),
+                       "oracle_check_utterances": pick,
+                       "argmax_equal_cpu_reference_lm_all_101_weights": bool(np.array_equal(arg_ref, arg_hip)),
+                       "pll_max_rel_err_vs_cpu_reference": float(max(rel))}}
 
 
 def main():
@@ -82,6 +145,11 @@ def main():
                     help="MLM fine-tuning steps on the synthetic set's reference sentences before scoring "
                          "(the reference's mlm_finetune_bert -> scoring -> fusion pipeline; 0 = random-init LM)")
     ap.add_argument("--finetune-lr", type=float, default=1e-4)
+    ap.add_argument("--workload", default="c3", choices=("c3", "c4"),
+                    help="c3 (default): U utterances x N=50 per rank (weak scaling); c4: the full 7176 x N=100 "
+                         "real-length set split over the ranks (strong scaling)")
+    ap.add_argument("--c4-secondary", type=int, default=1,
+                    help="C3 runs, rank 0 at N=1: one timed pass of the full C4 set (0 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -105,7 +173,11 @@ def main():
     # rank count (weak scaling: per-rank work ~ utts utterances).
     # hard: hypotheses permuted and AM scores unsorted, so the fused argmax moves with the weight
     # and the rerank check below is not the trivial AM-only case (same token counts)
-    nb_all = D.synthetic_nbest(args.utts * world, args.nbest, seed=1, hard=True)
+    if args.workload == "c4":
+        args.nbest = 100
+        nb_all = c4_set()
+    else:
+        nb_all = D.synthetic_nbest(args.utts * world, args.nbest, seed=1, hard=True)
 
     # The reference's pipeline: fine-tune BertForMaskedLM on in-domain text (MLM_PLL/main.py:117-161),
     # score with that checkpoint (:184-186), fuse (rescore.py:25-45).  Here the in-domain text is the
@@ -121,7 +193,10 @@ def main():
         ft = {"steps": args.finetune_steps, "lr": args.finetune_lr, "batch_rows": 64,
               "first_loss": round(losses[0], 4), "final_loss": round(losses[-1], 4),
               "seconds": round(time.perf_counter() - t_ft, 2),
-              "text": "the synthetic set's reference sentences (do_job rows, dropout off)"}
+              "text": ("the evaluation set's OWN reference sentences (do_job rows, dropout off): an oracle-style "
+                       "LM that makes the fused argmax depend on the LM; the rerank CER / best weight measure the "
+                       "fusion path, not LM quality (synthetic token sequences carry no structure a held-out "
+                       "fine-tune could learn)")}
     scorer = PLLScorer(weights, BERT_BASE, device=local, max_rows=args.max_rows, precision=args.precision)
     parts = shard.plan_shards(shard.utterance_costs(nb_all), world)
     u0, u1 = parts[rank]
@@ -220,17 +295,20 @@ def main():
                 "traffic": traffic, "traffic_source": tsrc, "algorithmic_bytes": alg_bytes,
                 "launches": n, "avg_launch_ms": round(ms / max(n, 1), 4),
                 "flops_per_launch": fl / max(n, 1), "algorithmic_flops_per_launch": fl / kx / max(n, 1)}
-        # MFMA busy of the same kernel kind from the committed rocprofv3 PMC pass
-        # (SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE over the CUs, tools/pmc_mfma.py)
+        # MFMA busy of the same kernel kind from a COMMITTED rocprofv3 PMC pass of an earlier run
+        # (SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE over the CUs, tools/pmc_mfma.py): not this run's
+        # measurement, so it sits under its own key with its source file
         mfma_files = sorted(f for f in os.listdir(os.path.join(REPO, "profiles")) if f.endswith("_pmc_mfma.json"))
         tag = {"qkv": "x3s:qkv", "oproj": "x3s:oproj", "ffn1": "x3s:ffn1", "ffn2": "x3s:ffn2"}.get(dom)
         if tag and kx == 3 and mfma_files:
             pm = json.load(open(os.path.join(REPO, "profiles", mfma_files[-1])))
             hit = [v for k, v in pm.items() if k.startswith(tag)]
             if hit:
-                roof["mfma_busy"] = hit[0].get("mfma_busy")
-                roof["mfma_busy_clock_GHz"] = hit[0].get("clock_GHz")
-                roof["mfma_busy_source"] = f"profiles/{mfma_files[-1]}"
+                roof["committed_pmc"] = {"mfma_busy": hit[0].get("mfma_busy"), "clock_GHz": hit[0].get("clock_GHz"),
+                                         "source": f"profiles/{mfma_files[-1]}",
+                                         "note": "committed profile of an earlier build; not measured in this run"}
+        if traffic is not None:
+            roof["traffic_note"] = "from a committed PMC profile (traffic_source), scaled to this run's rows per launch"
 
     # ---- reranked 1-best CER (second half of BASELINE.json's metric), rank-0 shard -------
     # HIP fusion over the 101-weight grid + corpus CER on this step's LM scores, checked
@@ -248,18 +326,20 @@ def main():
         # the fusion path; the scoring itself is checked against the CPU reference pattern in
         # cpu_baseline.pll_max_rel_err_vs_gpu and by tests/test_gpu_configs.py
         rr = {"best_weight": round(bw, 2), "cer": bcer, "am_only_cer": float(cers[0]),
+              "lm": ("fine-tuned on the evaluation references (lm_finetune.text)" if ft else "random-init"),
               "utterances": U, "fusion_cer_equal_oracle_same_lm": bool(bcer == obcer and bw == obw),
               "fusion_argmax_equal_oracle_same_lm": bool(np.array_equal(np.asarray(arg), oarg))}
 
     # ---- CPU baseline: oracle restatement of the reference work pattern ------------------
     # Also a scoring-parity spot check at bench scale: the PLL of every sampled hypothesis
     # (reference work pattern, fp32 CPU) against the HIP lm of the timed steps.
-    cpu = None
+    cpu, cpu_model = None, None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:       # the contract: rank 0 at N = 1 only
         from oracle.bert_ref import TorchBert, set_cpu_threads
         import oracle.bert_ref as OB
         threads = set_cpu_threads()
         model = TorchBert(weights, BERT_BASE)
+        cpu_model = model
         lm_np = lm.double().cpu().numpy()
         # whole utterances nearest the step's median utterance cost (sum_h L_h (L_h + 2), the cost
         # the sharding plan balances) first, until the time budget: a sample at the step's length
@@ -328,20 +408,35 @@ def main():
                 "steps": args.fp16_steps, "pll_max_rel_vs_headline": rel16}
         s16.close()
 
+    # ---- secondary leg: BASELINE config C4 (full 7176 x N=100 real-length set) at one GPU ------
+    c4 = None
+    if rank == 0 and world == 1 and args.workload == "c3" and args.c4_secondary and args.precision == "fp16x3":
+        c4 = c4_secondary(scorer, weights, local, cpu_model=cpu_model)
+
     if rank == 0:
         mean_T = float(np.average(lens, weights=lens - 2))
         rec = {"metric": "masked-token BERT forwards/sec (MLM_PLL, N=50, L~32)", "value": round(value, 2),
                "unit": "masked fwd/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-               "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
-               "vs_baseline": None, "dtype": DTYPE[args.precision], "data": "synthetic (PCG64 seed 1, permuted N-best with unsorted AM scores; random-init bert-base weights seed 1234)",
-               "config": {"workload": "C3 MLM_PLL full PLL", "model": "bert-base-chinese shape (12L/768/12H/3072/V21128)",
-                          "utts_per_rank": args.utts, "n_best": args.nbest, "utts_total": nb_all.n_utt,
+               "ms_per_step": round(dt / args.steps * 1e3, 3), "higher_is_better": True,
+               "scaling": "strong" if args.workload == "c4" else "weak",
+               "vs_baseline": None, "dtype": DTYPE[args.precision],
+               "data": ("synthetic (PCG64 seed 1, permuted N-best with unsorted AM scores"
+                        + ("; alfred test length histogram" if args.workload == "c4" else "")
+                        + "); bert-base weights: random init seed 1234"
+                        + (f", then MLM-fine-tuned {args.finetune_steps} steps on the set's reference sentences"
+                           if ft else "")),
+               "config": {"workload": ("C4 MLM_PLL full PLL, full 7176-utterance set, N=100, real lengths"
+                                       if args.workload == "c4" else "C3 MLM_PLL full PLL"),
+                          "model": "bert-base-chinese shape (12L/768/12H/3072/V21128)",
+                          "utts_per_rank": (None if args.workload == "c4" else args.utts), "n_best": args.nbest,
+                          "utts_total": nb_all.n_utt,
                           "forwards_per_step": n_fwd_all, "forwards_rank0_step": n_fwd,
                           "mean_T": round(mean_T, 2),
                           "parallelism": f"dp{world} (cost-balanced utterance shards of one global set + one RCCL all_gather"
                                          + (" in every step" if gather else "; none at one rank") + ")"},
                "achieved_tflops_canonical": round(flops_step * args.steps / dt / 1e12, 2),
                "roofline": roof, "cpu_baseline": cpu, "rerank": rr, "lm_finetune": ft, "fp16_secondary": fp16,
+               "c4_secondary": c4,
                "kinds_ms": {k: round(v[0], 3) for k, v in kinds.items()}}
         print(json.dumps(rec))
     scorer.close()

@@ -16,7 +16,15 @@
  *   - return 0 on success, a negative RS_E* code on failure; rs_last_error() gives a
  *     thread-local message.
  *   - A model handle is bound to one device and must not be used by two host threads
- *     at once.  Results are deterministic (no float atomics, fixed reduction orders).
+ *     at once.  Calls on one handle are ORDERED even across streams: they share the handle's
+ *     workspace, LayerNorm gang-ticket words and flags, so a call issued on a different stream
+ *     than the previous call first makes its stream wait (device-side) for the previous call's
+ *     work.  Results are deterministic (no float atomics, fixed reduction orders).
+ *   - The fused residual + LayerNorm GEMM (fp16x3 mode) exchanges row statistics between the
+ *     N_pad / 256 workgroups of a row panel inside one launch; those workgroups must be able to
+ *     run at the same time (3 free workgroup slots for bert-base: anywhere on the GPU with
+ *     RS_LNGANG=ticket, on one XCD with the default RS_LNGANG=xcd).  On a GPU so full of other
+ *     work that they cannot, the bounded wait ends the call in RS_EHIP instead of hanging.
  */
 #ifndef RESCORE_H_
 #define RESCORE_H_

@@ -143,24 +143,6 @@ def test_lnfuse_matches_separate_pass(w_base, monkeypatch, max_rows):
     assert rel_err(a, b).max() < 1e-6, rel_err(a, b).max()
 
 
-@pytest.mark.parametrize("max_rows", [4096, 262144])
-def test_pp_scores_bitwise(w_base, monkeypatch, max_rows):
-    """QKV and BertIntermediate on the ping-pong kernel (RS_PP=1) vs gemm_x3s_kernel (RS_PP=0):
-    the same MFMAs in the same order, so every PLL is bitwise equal; and the PP path still meets
-    the F1-class accuracy (checked through equality with the default path's fixture tests)."""
-    from asr_rescoring_amd.scorer import PLLScorer
-    nb = D.synthetic_nbest(10, 40, seed=13, vocab=BERT_BASE.vocab, len_lo=4, len_hi=60)
-    s = PLLScorer(w_base, BERT_BASE, device=0, max_rows=max_rows, precision="fp16x3")
-    try:
-        monkeypatch.setenv("RS_PP", "0")
-        a = s.score(nb)
-        monkeypatch.setenv("RS_PP", "1")
-        b = s.score(nb)
-    finally:
-        s.close()
-    assert np.array_equal(a, b), rel_err(b, a).max()
-
-
 def test_cls_golden(w_base, w_tiny, golden_dir):
     from asr_rescoring_amd.scorer import RescoreBertScorer
     for w, shape, name, key in ((w_base, BERT_BASE, "cls_base.npz", "cls"), (w_tiny, BERT_TINY, "pll_tiny.npz", "cls")):

@@ -1,4 +1,4 @@
-"""In-process A/B of launch switches that are read per call (RS_LNGANG, RS_PP, RS_CHUNK_ALIGN, ...)
+"""In-process A/B of launch switches that are read per call (RS_LNGANG, RS_CHUNK_ALIGN, ...)
 on the bench's C3 workload: one scorer, one synthetic set, the configurations interleaved
 round by round; prints masked forwards/s per configuration (median over rounds) and whether
 every configuration's PLL scores are bitwise equal to the first one's.
