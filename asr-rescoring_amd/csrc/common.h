@@ -60,7 +60,8 @@ struct EpiArgs {
     unsigned* lnerr;
     unsigned ln_tag;
     float ln_eps;
-    int diag;              // EPI_LNRES_IMG timing diagnostics (RS_LNFUSE_DIAG; 0 in production)
+    int diag;              // EPI_LNRES_IMG: 8 = every wait times out (RS_LNFUSE_DIAG, tests); 0 in production
+    unsigned long long* dbg;  // stamp builds only (rs_debug_stamps): per-workgroup phase cycle sums
 };
 inline size_t lnres_granules(int m_pad) { return (size_t)m_pad * 4 * 2; }     // <= 4 column tiles
 

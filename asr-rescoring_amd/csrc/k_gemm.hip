@@ -869,14 +869,23 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     constexpr int NSTORE = 32;                   // epilogue stores per wave per tile
     static_assert(EPI == EPI_BIAS_F32 || EPI == EPI_GELU_F16 || EPI == EPI_LNRES_IMG, "x3s epilogues");
     constexpr bool LNR = EPI == EPI_LNRES_IMG;
-    // VAR 268435456 (LayerNorm epilogue): the residual image is read during the K loop, one unit
-    // of NRU per K-step into RRU registers and added into the accumulators at the next step, so
-    // the epilogue no longer starts with a 256-KB read every CU issues at the same moment
-    constexpr bool KRES = LNR && (VAR & 268435456) != 0;
-    constexpr int NRU = (VAR & 536870912) ? 16 : 8;    // units: row blocks (8) or half blocks (16)
-    constexpr int RRU = NRU == 8 ? 4 : 2;               // uint4 registers per unit
-    constexpr bool EARLYG = (VAR & 1073741824) == 0;
     static_assert(!LNR || (VAR & 2) == 0, "the LayerNorm epilogue has no no-store diagnostic");
+    // VAR 268435456: stamp build (rs_debug_stamps; diagnostic only, never a production launch):
+    // s_memtime at the tile's phase boundaries, per-phase cycle sums in scalar registers, stored by
+    // thread 0 into ep.dbg[blockIdx.x * 16 + phase] (a buffer of its own: no output depends on it)
+    constexpr bool STAMP = (VAR & 268435456) != 0;
+    unsigned long long st_sum[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0;
+    auto stamp = [&](int ph) __attribute__((always_inline)) {
+        if constexpr (STAMP) {
+            unsigned long long tt;
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tt)::"memory");
+            __builtin_amdgcn_sched_barrier(0);
+            if (ph >= 0) st_sum[ph] += tt - st_prev;
+            st_prev = tt;
+        }
+    };
+    stamp(-1);
     static_assert((VAR & 16777216) == 0 || LNR, "the permuted-column layout is written for the LayerNorm epilogue");
     extern __shared__ __attribute__((aligned(16))) char smem[];        // the LDS-DMA ring (2 stages)
     // wave-private epilogue slabs: a separate LDS object, so the compiler can tell the slab
@@ -900,6 +909,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         __syncthreads();
         t = (int)*(const unsigned*)(slabs + 2048);
     }
+    stamp(8);
     if ((unsigned)t >= (unsigned)n_tiles) {
         if constexpr (LNR) {
             if (tid == 0) lnr_done(ep);
@@ -933,7 +943,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     const int pswz = ((lane & 3) ^ g16(prow >> 2)) * 8;
     const size_t ld2 = (size_t)2 * K;
     __amdgpu_buffer_rsrc_t rsA, rsW;
-    int voffA, voffW;                             // lane byte offsets of row half 0, hi part
+    int voffA[4], voffW[4];                       // lane byte offsets: (p & 1) row half x (r & 1) hi / lo
     // VAR 16777216: output columns permuted inside each 32-column group so that a lane's two
     // 16-column MFMA blocks 2m, 2m + 1 hold 8 CONSECUTIVE output columns (32 m + 8 q4 .. + 7)
     // instead of two runs of 4: W image row 32 m + 16 jj + 4 q + e is W row 32 m + 8 q + 4 jj + e.
@@ -942,10 +952,13 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     auto wperm = [](int L) {
         return PERM ? (L & ~31) | (((L >> 2) & 3) << 3) | (((L >> 4) & 1) << 2) | (L & 3) : L;
     };
-    // row half 1 (+128 rows: wperm keeps the row's 32-group) and the lo part (+K) are uniform
-    // byte offsets added in the scalar offset, so one lane offset per operand
-    voffA = (prow * (int)ld2 + pswz) * 2;
-    voffW = (wperm(prow) * ldw + pswz) * 2;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int l = 0; l < 2; ++l) {
+            voffA[2 * h + l] = ((prow + 128 * h) * (int)ld2 + l * K + pswz) * 2;
+            voffW[2 * h + l] = (wperm(prow + 128 * h) * ldw + l * K + pswz) * 2;
+        }
     auto set_rsrc = [&](int m0, int n0) {
         rsA = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * ld2), (short)0, (int)(256 * ld2 * 2), 0x00020000);
         rsW = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (size_t)n0 * ldw), (short)0, 256 * ldw * 2, 0x00020000);
@@ -954,8 +967,8 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         if constexpr ((VAR & 1) != 0) return;     // diagnostic: no K-loop staging (stale tiles)
         const int r = p >> 1;
         auto* dst = (__attribute__((address_space(3))) void*)(smem + buf * STAGE + r * REG + ((p & 1) * 8 + wave) * 1024);
-        const int so = ((p & 1) * 128 * (r < 2 ? (int)ld2 : ldw) + (r & 1) * K + k0) * 2;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 16, r < 2 ? voffA : voffW, so, 0, 0);
+        const int vo = (r < 2 ? voffA : voffW)[2 * (p & 1) + (r & 1)];
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 16, vo, k0 * 2, 0, 0);
     };
     auto stage = [&](int buf, int k0) {
 #pragma unroll
@@ -977,16 +990,15 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     // the next step's eight DMA pieces ride this step's first MFMA groups (one per group of four
     // MFMAs of row half 0); the last step of a tile passes k0n = 2^29 and issues none
     auto kstep16 = [&](int buf, int k0n) {
-        // k0n opaque: the pieces' scalar offsets are formed here, not hoisted out of the peeled
-        // steps as dozens of live SGPR constants
-        asm volatile("" : "+s"(k0n));
         const char* sb = smem + buf * STAGE;
-        half8 wh[4], wl[4];
+        half8 wh[4], wl[4], wd[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             wh[j] = *(const half8*)(sb + offW16 + j * 1024);
             wl[j] = *(const half8*)(sb + offW16 + REG + j * 1024);
         }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wd[j] = wh[j] * down;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             half8 ah[4], al[4];
@@ -1001,26 +1013,15 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
 #pragma unroll
                     for (int ii = 0; ii < 4; ++ii) ah[ii] *= down;              // A_hi / 64
                 }
-                // groups of four MFMAs: product 1 (W_hi / 64 . A_lo·64) by column block, its factor
-                // formed right there (opaque to CSE: no 16 registers of W_hi / 64 held across the
-                // step), products 0 and 2 by row block; per accumulator the order of the three
-                // products is unchanged
 #pragma unroll
-                for (int g = 0; g < 4; ++g) {
-                    if (pr == 1) {
-                        half8 wdj = wh[g];
-                        asm volatile("" : "+v"(wdj));
-                        wdj *= down;                                            // W_hi / 64
+                for (int ii = 0; ii < 4; ++ii) {
 #pragma unroll
-                        for (int ii = 0; ii < 4; ++ii)
-                            acc16[4 * h + ii][g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wdj, al[ii], acc16[4 * h + ii][g], 0, 0, 0);
-                    } else {
-#pragma unroll
-                        for (int j = 0; j < 4; ++j)
-                            acc16[4 * h + g][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(pr == 0 ? wh[j] : wl[j], ah[g],
-                                                                                         acc16[4 * h + g][j], 0, 0, 0);
+                    for (int j = 0; j < 4; ++j) {
+                        const half8 b = pr == 0 ? wh[j] : pr == 1 ? wd[j] : wl[j];
+                        const half8 a = pr == 1 ? al[ii] : ah[ii];
+                        acc16[4 * h + ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b, a, acc16[4 * h + ii][j], 0, 0, 0);
                     }
-                    const int grp = 12 * h + 4 * pr + g;
+                    const int grp = 12 * h + 4 * pr + ii;
                     if (grp < 8 && k0n < (1 << 29)) {
                         __builtin_amdgcn_sched_barrier(0);
                         piece(buf ^ 1, k0n, grp);
@@ -1037,72 +1038,42 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     stage(0, 0);
     int par = 0;                                                  // buffer of K-step 0
     bool first = true;
-    // KRES: residual image unit u of the tile (row block u of the wave tile, or half block u >> 1,
-    // column half u & 1) in the permuted-column accumulator layout: per row block ii and column half
-    // mm, 8 consecutive columns 32 mm + 8 q4 of the lane's row as one 16-B load per image (hi, lo·64)
-    uint4 rres[RRU];
-    auto res_load = [&](int u, int rm0, int rn0) __attribute__((always_inline)) {
-        const int ii = NRU == 8 ? u : u >> 1;
-        const f16* p = (const f16*)ep.out + (size_t)(rm0 + wm * WTM + 16 * ii + r16) * ep.ldc + rn0 + wn * WTN + 8 * q4;
-#pragma unroll
-        for (int k = 0; k < RRU / 2; ++k) {
-            const int mm = NRU == 8 ? k : (u & 1);
-            rres[2 * k] = *(const uint4*)(p + 32 * mm);
-            rres[2 * k + 1] = *(const uint4*)(p + 32 * mm + ep.nlog);
-        }
-    };
-    auto res_add = [&](int u) __attribute__((always_inline)) {      // u: a compile-time constant at every call
-        const int ii = NRU == 8 ? u : u >> 1;
-#pragma unroll
-        for (int k = 0; k < RRU / 2; ++k) {
-            const int mm = NRU == 8 ? k : (u & 1);
-            const half8 vh = __builtin_bit_cast(half8, rres[2 * k]);
-            const half8 vl = __builtin_bit_cast(half8, rres[2 * k + 1]);
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-                acc16[ii][2 * mm + (e >> 2)][e & 3] += __builtin_fmaf((float)vl[e], X3_DOWN, (float)vh[e]);
-        }
-    };
     for (;;) {
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc16[i][j] = (f32x4)(0.f);
-        auto kstep_full = [&](int kt) __attribute__((always_inline)) {
-            // step kt landed for this wave (at a tile's first step the previous tile's stores
-            // are younger and stay in flight); the barrier: landed for every wave, and every
-            // wave is done reading step kt-1's buffer, which now receives step kt+1
+        // step kt landed for this wave (at a tile's first step the previous tile's stores are
+        // younger and stay in flight); the barrier: landed for every wave, and every wave is done
+        // reading step kt-1's buffer, which now receives step kt+1.  (VAR 8, diagnostic: the DMA is
+        // never waited for — isolates its latency from its presence.)
+        int kt0 = 0;
+        if constexpr (LNR) {
+            // K-step 0 peeled with its next-step offset a constant (nk >= 2: launch_x3s): left to the
+            // compiler, the peeled step tested a hoisted loop-invariant flag that this build spilled,
+            // and the reload's vmcnt(0) drained the previous tile's 32 epilogue stores at every tile
+            // start (the fp32 / GELU builds keep the loop: peeled by hand they spill)
+            if constexpr ((VAR & 8) == 0) {
+                if (!first) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
+                else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            asm volatile("s_barrier" ::: "memory");
+            __builtin_amdgcn_sched_barrier(0);
+            kstep16(par, BK);
+            __builtin_amdgcn_sched_barrier(0);
+            kt0 = 1;
+        }
+        for (int kt = kt0; kt < nk; ++kt) {
+            const int cur = (par + kt) & 1;
             if constexpr ((VAR & 8) != 0) {
-                // diagnostic: the DMA is never waited for (isolates its latency from its presence)
             } else if (kt == 0 && !first) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             asm volatile("s_barrier" ::: "memory");
             __builtin_amdgcn_sched_barrier(0);
-        };
-        int kt0 = 0;
-        if constexpr (KRES) {
-            // the first NRU + 1 K-steps peeled (acc16 indices must be compile-time): step u adds
-            // unit u - 1 (landed with that step's vmcnt(0)) and issues unit u's loads; with fewer
-            // K-steps than units the rest of the residual is loaded and added without a step
-#pragma unroll
-            for (int u = 0; u <= NRU; ++u) {
-                const bool step = u < nk;
-                if (step) kstep_full(u);
-                if (u >= 1) res_add(u - 1);
-                if (u < NRU) res_load(u, m0, n0);
-                __builtin_amdgcn_sched_barrier(0);
-                if (step) {
-                    kstep16((par + u) & 1, u + 1 < nk ? (u + 1) * BK : (1 << 29));
-                    __builtin_amdgcn_sched_barrier(0);
-                }
-            }
-            kt0 = NRU + 1;
-        }
-        for (int kt = kt0; kt < nk; ++kt) {
-            kstep_full(kt);
-            kstep16((par + kt) & 1, kt + 1 < nk ? (kt + 1) * BK : (1 << 29));
+            kstep16(cur, kt + 1 < nk ? (kt + 1) * BK : (1 << 29));
             __builtin_amdgcn_sched_barrier(0);
         }
+        stamp(0);                                                 // K loop
         // ---- transition
         const int last = (par + nk - 1) & 1;                      // buffer of the last K-step
         const int cm0 = m0, cn0 = n0;
@@ -1110,25 +1081,13 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         // the wave's 64): only the bias loads are outstanding here (the last K-step issued no
         // DMA), so one vmcnt(0) waits for exactly them; inline asm keeps the compiler from placing
         // its own wait
-        f32x4 bq[4], gq[4], bb[4];               // bias; (KRES) LayerNorm weight / bias of the lane's columns
+        f32x4 bq[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            const int cj = cn0 + wn * WTN + (PERM ? 32 * (j >> 1) + 8 * q4 + 4 * (j & 1) : 16 * j + 4 * q4);
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bq[j]) : "v"(ep.bias + cj) : "memory");
-            if constexpr (KRES && EARLYG) {
-                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(gq[j]) : "v"(ep.res_g + cj) : "memory");
-                asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bb[j]) : "v"(ep.res_b + cj) : "memory");
-            }
+            const float* bp = ep.bias + cn0 + wn * WTN + (PERM ? 32 * (j >> 1) + 8 * q4 + 4 * (j & 1) : 16 * j + 4 * q4);
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bq[j]) : "v"(bp) : "memory");
         }
-        if constexpr (KRES && EARLYG) {
-            asm volatile("s_waitcnt vmcnt(0)"
-                         : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]), "+v"(gq[0]), "+v"(gq[1]), "+v"(gq[2]),
-                           "+v"(gq[3]), "+v"(bb[0]), "+v"(bb[1]), "+v"(bb[2]), "+v"(bb[3])
-                         :
-                         : "memory");
-        } else {
-            asm volatile("s_waitcnt vmcnt(0)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]) : : "memory");
-        }
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(bq[0]), "+v"(bq[1]), "+v"(bq[2]), "+v"(bq[3]) : : "memory");
         // the next tile's stage 0 (into the buffer step nk-2 used) lands while this epilogue runs
         // (issuing it after the LayerNorm epilogue's residual loads instead, so that their waits
         // need not cover this DMA, measured -2.7 %: profiles/r3p2_lnperm_ab.txt)
@@ -1140,6 +1099,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             set_rsrc(m0, n0);
             stage(last ^ 1, 0);
         }
+        stamp(1);                                                 // bias wait + next tile's stage 0
         // bias (+ GELU) of row blocks [i0, i1)
         auto finish = [&](int i0, int i1) {
 #pragma unroll
@@ -1161,24 +1121,21 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 const f16* img = (const f16*)ep.out;
                 const int c0 = cn0 + wn * WTN + 4 * q4;
                 // x = (acc + bias) + h, the residual image h = hi + lo/64 read in the accumulator
-                // layout.  KRES: h is already in the accumulators (added during the K loop).  Else
-                // read here, four row blocks at a time (as ln_res_img forms it) — every CU issues
-                // its 256 KB at the same moment (~3 % of the step at C3); the permuted-column layout
-                // (PERM) halves its load count: +1.1 % end to end
-                if constexpr (KRES) {
+                // layout, four row blocks at a time (as ln_res_img forms it); the permuted-column
+                // layout (PERM) halves its load count: +1.1 % end to end.  (Reading it during the K
+                // loop instead, one row block per K-step added into the accumulators, measured
+                // neutral — 63,277 vs 63,263 masked fwd/s, profiles/r5b_lnkres_ab.txt — and made a
+                // row's sum depend on its position in the tile, so it was removed.)
+                // (two row blocks per batch: four would hold 64 registers of residual beside the 128
+                // accumulators, and the spills that forced reloaded values whose waits drained the
+                // next tile's stage 0 inside the statistics publish)
+                constexpr int RB2 = 2;
 #pragma unroll
-                    for (int i = 0; i < 8; ++i)
+                for (int hh = 0; hh < 8 / RB2; ++hh) {
+                    half4 rh0[RB2][4], rl0[RB2][4];
 #pragma unroll
-                        for (int j = 0; j < 4; ++j)
-#pragma unroll
-                            for (int e = 0; e < 4; ++e) acc16[i][j][e] += bq[j][e];
-                } else {
-#pragma unroll
-                for (int hh = 0; hh < 2; ++hh) {
-                    half4 rh0[4][4], rl0[4][4];
-#pragma unroll
-                    for (int ii = 0; ii < 4; ++ii) {
-                        const f16* prow_img = img + (size_t)(cm0 + wm * WTM + 16 * (4 * hh + ii) + r16) * ldc;
+                    for (int ii = 0; ii < RB2; ++ii) {
+                        const f16* prow_img = img + (size_t)(cm0 + wm * WTM + 16 * (RB2 * hh + ii) + r16) * ldc;
                         if constexpr (PERM) {
                             // blocks 2m, 2m + 1: 8 consecutive columns, one 16-B load per image
 #pragma unroll
@@ -1200,15 +1157,15 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         }
                     }
 #pragma unroll
-                    for (int ii = 0; ii < 4; ++ii)
+                    for (int ii = 0; ii < RB2; ++ii)
 #pragma unroll
                         for (int j = 0; j < 4; ++j)
 #pragma unroll
                             for (int e = 0; e < 4; ++e)
-                                acc16[4 * hh + ii][j][e] = (acc16[4 * hh + ii][j][e] + bq[j][e]) +
-                                                           ((float)rh0[ii][j][e] + (float)rl0[ii][j][e] * X3_DOWN);
+                                acc16[RB2 * hh + ii][j][e] = (acc16[RB2 * hh + ii][j][e] + bq[j][e]) +
+                                                             ((float)rh0[ii][j][e] + (float)rl0[ii][j][e] * X3_DOWN);
                 }
-                }
+                stamp(2);                                         // residual read + add
                 // row partials over the wave's 64 columns (lanes l, l^16, l^32, l^48 share a row),
                 // then over the four waves of the row half through their slabs
                 float* red = (float*)(slabs + wave * 4096);
@@ -1259,10 +1216,15 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 if (wn == 0) {
                     typedef unsigned long long u64;
                     u64* gx = (u64*)ep.lnx + (size_t)panel * ntn * BM * 2 + wm * WTM * 2;   // [c][row][2]
+                    // the lane's granule offsets formed here, per tile (opaque lane index): hoisted out
+                    // of the tile loop they were a spilled 64-bit register whose reload waited for
+                    // the next tile's stage 0 before every publish
+                    int ln = lane;
+                    asm volatile("" : "+v"(ln));
                     float os[2], oq[2];
 #pragma unroll
                     for (int k = 0; k < 2; ++k) {
-                        const int rr = lane + 64 * k;
+                        const int rr = ln + 64 * k;
                         float a = 0.f, b = 0.f;
 #pragma unroll
                         for (int w2 = 0; w2 < WN; ++w2) {
@@ -1276,6 +1238,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         __hip_atomic_store((gu64*)(g + 1), tag | __float_as_uint(b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                     float ps[2][4], pq[2][4];
+                    stamp(3);                                     // tile statistics + publish (wave 0)
                     for (unsigned spins = 0;;) {
                         bool ok = true;
 #pragma unroll
@@ -1285,7 +1248,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                                 ps[k][c] = os[k];
                                 pq[k][c] = oq[k];
                                 if (c < ntn && c != tcol) {
-                                    const u64* g = gx + ((size_t)c * BM + lane + 64 * k) * 2;
+                                    const u64* g = gx + ((size_t)c * BM + ln + 64 * k) * 2;
                                     const u64 va = __hip_atomic_load((const gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                                     const u64 vb = __hip_atomic_load((const gu64*)(g + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                                     ok &= (va >> 32) == (tag >> 32) && (vb >> 32) == (tag >> 32);
@@ -1319,15 +1282,15 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         }
                         st2[lane + 64 * k] = make_float2(mean, 1.0f / sqrtf(__builtin_fmaf(m2, inv_n, ep.ln_eps)));
                     }
+                    stamp(4);                                     // peers' statistics (poll)
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-                if constexpr (!(KRES && EARLYG)) {                   // (KRES: loaded with the bias)
+                f32x4 gq[4], bb[4];                      // LayerNorm weight / bias of the lane's columns
 #pragma unroll
-                    for (int j = 0; j < 4; ++j) {
-                        const int cj = PERM ? cn0 + wn * WTN + 32 * (j >> 1) + 8 * q4 + 4 * (j & 1) : c0 + 16 * j;
-                        gq[j] = *(const f32x4*)(ep.res_g + cj);
-                        bb[j] = *(const f32x4*)(ep.res_b + cj);
-                    }
+                for (int j = 0; j < 4; ++j) {
+                    const int cj = PERM ? cn0 + wn * WTN + 32 * (j >> 1) + 8 * q4 + 4 * (j & 1) : c0 + 16 * j;
+                    gq[j] = *(const f32x4*)(ep.res_g + cj);
+                    bb[j] = *(const f32x4*)(ep.res_b + cj);
                 }
 #pragma unroll
                 for (int i = 0; i < 8; ++i) {
@@ -1337,6 +1300,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
 #pragma unroll
                         for (int e = 0; e < 4; ++e) acc16[i][j][e] = ln_apply(acc16[i][j][e], st, gq[j][e], bb[j][e]);
                 }
+                stamp(5);                                         // barrier, LN weights, LN apply
             };
             // the GELU image: each row-block pair's bias + GELU right before its slab pass, so that
             // VALU work overlaps the previous pair's LDS and global stores
@@ -1409,9 +1373,17 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                     }
                 }
             }
+            stamp(6);                                             // epilogue stores
+            if constexpr (STAMP) st_sum[7] += 1;
             if (!more) break;
             par = last ^ 1;
             first = false;
+    }
+    if constexpr (STAMP) {
+        if (tid == 0) {
+#pragma unroll
+            for (int ph = 0; ph < 10; ++ph) ep.dbg[blockIdx.x * 16 + ph] += st_sum[ph];
+        }
     }
     if constexpr (LNR) {
         if (tid == 0) lnr_done(ep);
@@ -1580,14 +1552,21 @@ int gemm_lnres_workgroups(int N_pad) {
 }
 
 // Production split-operand fp16x3 GEMM (gemm_x3s_kernel; tools/x3s_epi_probe.py).
-hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_pad, int N_pad, int K,
-                           const EpiArgs& ep, hipStream_t st) {
-    if (M_pad % 256 || N_pad % 256 || K % 32 || K < 64 || ldw < 2 * K || M_pad <= 0) return hipErrorInvalidValue;
-    // the buffer descriptors address one 256-row panel: 32-bit byte offsets
-    if ((long long)256 * ldw * 2 >= (1ll << 31) || (long long)256 * 2 * K * 2 >= (1ll << 31)) return hipErrorInvalidValue;
+// Stamp builds (rs_debug_stamps): while g_stamps is set, every split-operand GEMM launch runs the
+// VAR 268435456 build of its kernel and adds its per-workgroup phase cycles into the region of its
+// instance: 0 QKV / fp32 out, 1 BertIntermediate (GELU image), 2 O-projection + LayerNorm,
+// 3 BertOutput + LayerNorm (each [256 workgroups][16 words]).
+static unsigned long long* g_stamps = nullptr;
+constexpr int STAMP_WORDS = 4 * 256 * 16;
+
+template <int STV>
+hipError_t launch_gemm_x3s_v(int epi, const f16* A, const f16* W, int ldw, int M_pad, int N_pad, int K,
+                             const EpiArgs& ep_in, hipStream_t st) {
+    EpiArgs ep = ep_in;
+    if (STV) ep.dbg = g_stamps + (epi == EPI_BIAS_F32 ? 0 : epi == EPI_GELU_F16 ? 1 : K > 1024 ? 3 : 2) * 256 * 16;
     switch (epi) {
-        case EPI_BIAS_F32: return launch_x3s<EPI_BIAS_F32, 0>(A, W, M_pad, N_pad, K, ep, st, ldw);
-        case EPI_GELU_F16: return launch_x3s<EPI_GELU_F16, 0>(A, W, M_pad, N_pad, K, ep, st, ldw);
+        case EPI_BIAS_F32: return launch_x3s<EPI_BIAS_F32, STV>(A, W, M_pad, N_pad, K, ep, st, ldw);
+        case EPI_GELU_F16: return launch_x3s<EPI_GELU_F16, STV>(A, W, M_pad, N_pad, K, ep, st, ldw);
         case EPI_LNRES_IMG: {
             // Output columns permuted inside 32-column groups (VAR 16777216: 16-B epilogue loads,
             // +1.1 % end to end, profiles/r3p2_lnperm_ab.txt); VAR 67108864 is a name tag only (the
@@ -1601,25 +1580,43 @@ hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_p
             // free slots the bounded wait ends the call in RS_EHIP instead of hanging.
             const char* g = getenv("RS_LNGANG");
             const bool xcd = g && !strcmp(g, "xcd");
-            // RS_LNKRES (A/B, read per call): 0 = residual read in the epilogue, 1 = during the K
-            // loop by row blocks (default), 2 = by half row blocks
-            const char* kr = getenv("RS_LNKRES");
-            const int kres = kr ? atoi(kr) : 1;
-            constexpr int VL = 16777216, KR1 = 268435456 | 1073741824, KR2 = 268435456 | 536870912 | 1073741824;
-#define RS_LNR(V_)                                                                                \
-    (kres == 0   ? launch_x3s<EPI_LNRES_IMG, (V_)>(A, W, M_pad, N_pad, K, ep, st, ldw)               \
-     : kres == 2 ? launch_x3s<EPI_LNRES_IMG, (V_) | KR2>(A, W, M_pad, N_pad, K, ep, st, ldw)         \
-                 : launch_x3s<EPI_LNRES_IMG, (V_) | KR1>(A, W, M_pad, N_pad, K, ep, st, ldw))
+            constexpr int VL = 16777216 | STV;
             if (xcd) {
-                if (K > 1024) return RS_LNR(VL | 67108864 | 134217728);
-                return RS_LNR(VL | 134217728);
+                if (K > 1024) return launch_x3s<EPI_LNRES_IMG, VL | 67108864 | 134217728>(A, W, M_pad, N_pad, K, ep, st, ldw);
+                return launch_x3s<EPI_LNRES_IMG, VL | 134217728>(A, W, M_pad, N_pad, K, ep, st, ldw);
             }
-            if (K > 1024) return RS_LNR(VL | 67108864);
-            return RS_LNR(VL);
-#undef RS_LNR
+            if (K > 1024) return launch_x3s<EPI_LNRES_IMG, VL | 67108864>(A, W, M_pad, N_pad, K, ep, st, ldw);
+            return launch_x3s<EPI_LNRES_IMG, VL>(A, W, M_pad, N_pad, K, ep, st, ldw);
         }
     }
     return hipErrorInvalidValue;
+}
+
+hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_pad, int N_pad, int K,
+                           const EpiArgs& ep, hipStream_t st) {
+    if (M_pad % 256 || N_pad % 256 || K % 32 || K < 64 || ldw < 2 * K || M_pad <= 0) return hipErrorInvalidValue;
+    // the buffer descriptors address one 256-row panel: 32-bit byte offsets
+    if ((long long)256 * ldw * 2 >= (1ll << 31) || (long long)256 * 2 * K * 2 >= (1ll << 31)) return hipErrorInvalidValue;
+    if (g_stamps) return launch_gemm_x3s_v<268435456>(epi, A, W, ldw, M_pad, N_pad, K, ep, st);
+    return launch_gemm_x3s_v<0>(epi, A, W, ldw, M_pad, N_pad, K, ep, st);
+}
+
+// Diagnostic entry (not part of the scoring path): on = 1 allocates and zeroes the stamp buffer
+// and switches the split-operand GEMM launches to their stamp builds; on = 0 copies the buffer
+// (STAMP_WORDS u64: [instance][workgroup][phase], phases 0 K loop, 1 bias + next stage, 2 residual,
+// 3 statistics + publish, 4 poll, 5 LN apply, 6 stores, 7 tiles, 8 prologue) to host_out (may be
+// null), frees it and switches back.  Call on an idle device.
+extern "C" int rs_debug_stamps(int on, unsigned long long* host_out) {
+    if (on) {
+        if (!g_stamps && hipMalloc((void**)&g_stamps, STAMP_WORDS * 8) != hipSuccess) return -2;
+        return hipMemset(g_stamps, 0, STAMP_WORDS * 8) == hipSuccess ? 0 : -2;
+    }
+    if (!g_stamps) return -1;
+    if (hipDeviceSynchronize() != hipSuccess) return -2;
+    if (host_out && hipMemcpy(host_out, g_stamps, STAMP_WORDS * 8, hipMemcpyDeviceToHost) != hipSuccess) return -2;
+    (void)hipFree(g_stamps);
+    g_stamps = nullptr;
+    return 0;
 }
 
 hipError_t launch_gemm(int epi, const f16* A, const f16* W, int M_pad, int N_pad, int K,
