@@ -800,6 +800,7 @@ __device__ unsigned lnr_gang_ticket(const EpiArgs& ep, int ntn_) {
                 gid = (unsigned)v;
                 return true;
             }
+            if ((spins & 255) == 255 && lnr_ld(ep.lnerr, 0)) return false;
             __builtin_amdgcn_s_sleep(1);
         }
         return false;
@@ -832,6 +833,7 @@ __device__ unsigned lnr_gang_ticket(const EpiArgs& ep, int ntn_) {
                     ovf = ok = true;
                     break;
                 }
+                if ((spins & 255) == 255 && lnr_ld(ep.lnerr, 0)) break;
                 __builtin_amdgcn_s_sleep(1);
             }
         }
@@ -1213,6 +1215,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 // this tile's last K-step read (free until the next tile's first barrier; the
                 // slabs are rewritten by the store pass)
                 float2* st2 = (float2*)(smem + last * STAGE) + wm * WTM;
+                volatile unsigned* bailw = (volatile unsigned*)(smem + last * STAGE + 4096);   // per row half
                 if (wn == 0) {
                     typedef unsigned long long u64;
                     u64* gx = (u64*)ep.lnx + (size_t)panel * ntn * BM * 2 + wm * WTM * 2;   // [c][row][2]
@@ -1238,6 +1241,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         __hip_atomic_store((gu64*)(g + 1), tag | __float_as_uint(b), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     }
                     float ps[2][4], pq[2][4];
+                    bool failed = false;
                     stamp(3);                                     // tile statistics + publish (wave 0)
                     for (unsigned spins = 0;;) {
                         bool ok = true;
@@ -1259,8 +1263,14 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         if (ep.diag & 8) ok = false;        // diag 8 (tests): peers never arrive
                         if (__all(ok)) break;
                         __builtin_amdgcn_s_sleep(1);
-                        if (++spins == ((ep.diag & 8) ? (1u << 8) : (1u << 20))) {
+                        // bounded: a wait that cannot end (the gang's workgroups not co-resident)
+                        // sets the sticky error word; a wait that sees the word set (another
+                        // workgroup timed out) gives up too, so the launch drains fast
+                        ++spins;
+                        if (spins == ((ep.diag & 8) ? (1u << 8) : (1u << 20)) ||
+                            ((spins & 255) == 0 && __hip_atomic_load((const gu32*)ep.lnerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
                             if (lane == 0) __hip_atomic_store((gu32*)ep.lnerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                            failed = true;
                             break;
                         }
                     }
@@ -1282,9 +1292,11 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         }
                         st2[lane + 64 * k] = make_float2(mean, 1.0f / sqrtf(__builtin_fmaf(m2, inv_n, ep.ln_eps)));
                     }
+                    if (lane == 0) bailw[wm] = failed ? 1u : 0u;
                     stamp(4);                                     // peers' statistics (poll)
                 }
                 asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                if (bailw[0] | bailw[1]) return true;    // a wait gave up: the launch drains (RS_EHIP)
                 f32x4 gq[4], bb[4];                      // LayerNorm weight / bias of the lane's columns
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
@@ -1301,12 +1313,17 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         for (int e = 0; e < 4; ++e) acc16[i][j][e] = ln_apply(acc16[i][j][e], st, gq[j][e], bb[j][e]);
                 }
                 stamp(5);                                         // barrier, LN weights, LN apply
+                return false;
             };
             // the GELU image: each row-block pair's bias + GELU right before its slab pass, so that
             // VALU work overlaps the previous pair's LDS and global stores
             constexpr bool LATE = EPI == EPI_GELU_F16 && (VAR & 2) == 0;
-            if constexpr (LNR) lnres_epilogue();
-            else if constexpr (!LATE) finish(0, 8);
+            if constexpr (LNR) {
+                if (lnres_epilogue()) {
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile's stage 0 landed
+                    break;
+                }
+            } else if constexpr (!LATE) finish(0, 8);
             if constexpr ((VAR & 2) != 0) {      // diagnostic: no epilogue stores (acc kept alive)
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
@@ -1318,7 +1335,11 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 continue;
             }
             char* slb = slabs + wave * 4096;
-            const int rr0 = lane >> 3, c16 = lane & 7;
+            // (LayerNorm build: the store pass's lane offsets formed per tile — hoisted, they were a
+            // spilled register reloaded inside the residual wait)
+            int lns = lane;
+            if constexpr (LNR) asm volatile("" : "+v"(lns));
+            const int rr0 = lns >> 3, c16 = lns & 7;
             // VAR 33554432 (timing diagnostic, wrong results): every tile stores onto the rows of
             // row panel 0 (L2-resident lines), separating the store path from the HBM write burst
             const int sm0 = (VAR & 33554432) ? 0 : cm0;
@@ -1571,15 +1592,18 @@ hipError_t launch_gemm_x3s_v(int epi, const f16* A, const f16* W, int ldw, int M
             // Output columns permuted inside 32-column groups (VAR 16777216: 16-B epilogue loads,
             // +1.1 % end to end, profiles/r3p2_lnperm_ab.txt); VAR 67108864 is a name tag only (the
             // BertOutput launch, K = 3072), so rocprofv3 reports the two instances separately.
-            // Gang formation (RS_LNGANG, read per call; lnr_gang_ticket): "ticket" = consecutive
-            // start-order tickets; "xcd" = start-order tickets inside each XCD (VAR 134217728; a
-            // panel's column tiles share one L2), the rest from an overflow ticket.  Either way a
+            // Gang formation (RS_LNGANG, read per call; lnr_gang_ticket): "xcd" (default) = start-order
+            // tickets inside each XCD (VAR 134217728; a panel's column tiles share one L2), the rest
+            // from an overflow ticket; "ticket" = consecutive start-order tickets.  Either way a
             // gang's members have all started before it exchanges statistics.  The exchange needs
             // ntn (= N_pad / 256) workgroups of the gang co-resident — anywhere on the GPU for
             // "ticket", on one XCD for "xcd" (or once the grid has started, anywhere): with fewer
             // free slots the bounded wait ends the call in RS_EHIP instead of hanging.
+            // Default "xcd" (round 5: BertOutput fetch 25.0 -> 19.5 KB per row, O-projection 8.7 -> 7.2,
+            // throughput within noise, profiles/r5d_gangs_pmc.txt); "ticket" needs the gang's
+            // workgroups co-resident anywhere instead of on one XCD.
             const char* g = getenv("RS_LNGANG");
-            const bool xcd = g && !strcmp(g, "xcd");
+            const bool xcd = !(g && !strcmp(g, "ticket"));
             constexpr int VL = 16777216 | STV;
             if (xcd) {
                 if (K > 1024) return launch_x3s<EPI_LNRES_IMG, VL | 67108864 | 134217728>(A, W, M_pad, N_pad, K, ep, st, ldw);
@@ -1705,7 +1729,7 @@ __global__ void __launch_bounds__(64) occupy_kernel(long long ticks, int* out) {
 }  // namespace
 
 extern "C" int rs_debug_occupy(int blocks, int usec, int* d_out, void* stream) {
-    if (blocks <= 0 || blocks > 4096 || usec <= 0 || usec > 2000000) return -1;
+    if (blocks <= 0 || blocks > 4096 || usec <= 0 || usec > 5000000) return -1;
     constexpr int smem = 160 * 1024;
     static std::atomic<unsigned> attr_devs{0};
     if (smem_attr_once((const void*)occupy_kernel, smem, attr_devs) != hipSuccess) return -2;

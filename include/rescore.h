@@ -22,8 +22,8 @@
  *     work.  Results are deterministic (no float atomics, fixed reduction orders).
  *   - The fused residual + LayerNorm GEMM (fp16x3 mode) exchanges row statistics between the
  *     N_pad / 256 workgroups of a row panel inside one launch; those workgroups must be able to
- *     run at the same time (3 free workgroup slots for bert-base: anywhere on the GPU with the
- *     default RS_LNGANG=ticket, on one XCD with RS_LNGANG=xcd).  On a GPU so full of other work
+ *     run at the same time (3 free workgroup slots for bert-base: on one XCD with the default
+ *     RS_LNGANG=xcd, anywhere on the GPU with RS_LNGANG=ticket).  On a GPU so full of other work
  *     that they cannot, the bounded wait ends the call in RS_EHIP instead of hanging.
  */
 #ifndef RESCORE_H_

@@ -2,11 +2,16 @@
 contract around it, plus the RCCL exchange on one GPU.
 
 * gangs (the column tiles of a row panel exchanging row statistics inside the launch) are formed
-  by start-order tickets: with most CUs held by another stream's kernel the call still scores,
-  bitwise equal to an idle GPU, and never reaches the statistics-wait timeout;
+  by start-order tickets (per XCD by default, RS_LNGANG=xcd; chip-wide with RS_LNGANG=ticket): with
+  most CUs held by another stream's kernel the call still scores, bitwise equal to an idle GPU,
+  and never reaches the statistics-wait timeout;
 * the timeout path itself (forced by a diagnostic bit): RS_EHIP with a message, the flag cleared,
   the next call clean;
-* the XCD-group gang form (RS_LNGANG=xcd, cooperative launch) scores bitwise like the default;
+* the chip-wide ticket form (RS_LNGANG=ticket) scores bitwise like the XCD-local default;
+* the co-residency limit stated in include/rescore.h: with only two free workgroup slots (bert-base
+  gangs need three) the call fails fast with RS_EHIP instead of hanging, and the next call on a free
+  GPU scores bitwise (the gang-ticket words are reset by every launch); with three free slots the
+  ticket form scores;
 * chunks cut at whole LayerNorm-gang rounds score bitwise like max_rows chunks;
 * the deferred range check (rs_model_set_sync_check / rs_check);
 * a one-rank ``nccl`` (RCCL) process group: ``shard.score_sharded`` / ``gather_scores`` /
@@ -81,11 +86,59 @@ def test_lnfuse_forced_timeout_reports_and_clears(scorer, nb_mid, base_scores, m
     assert np.array_equal(scorer.score(nb_mid), base_scores)
 
 
-def test_lnfuse_xcd_gangs_match_ticket_gangs(scorer, nb_mid, base_scores, monkeypatch):
-    """The XCD-group gang form (blockIdx membership, cooperative launch) computes the same tiles
-    with the same statistics order: bitwise equal scores."""
-    monkeypatch.setenv("RS_LNGANG", "xcd")
+def test_lnfuse_ticket_gangs_match_xcd_gangs(scorer, nb_mid, base_scores, monkeypatch):
+    """The chip-wide ticket form computes the same tiles with the same statistics order as the
+    XCD-local default: bitwise equal scores, also with CUs held elsewhere."""
+    monkeypatch.setenv("RS_LNGANG", "ticket")
     assert np.array_equal(scorer.score(nb_mid), base_scores)
+    side = torch.cuda.Stream()
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    _occupy(n_cu // 2, 300_000, side)
+    got = scorer.score(nb_mid)
+    torch.cuda.synchronize()
+    assert np.array_equal(got, base_scores)
+
+
+@pytest.fixture(scope="module")
+def nb_small():
+    # one launch chunk, ~3k token rows: the kernels around the LayerNorm GEMMs stay short on 2-3 CUs
+    return D.synthetic_nbest(2, 6, seed=23, vocab=BERT_BASE.vocab, len_lo=10, len_hi=24)
+
+
+@pytest.mark.parametrize("gang", ["ticket", "xcd"])
+def test_lnfuse_too_few_free_slots_fails_fast_then_recovers(scorer, nb_small, monkeypatch, gang):
+    """Another stream's kernel holds all but two CUs (one 160 KiB-LDS workgroup each) for 4 s: a
+    bert-base gang (three column tiles) can never be co-resident, the first statistics wait runs
+    out, every other wait sees the error word and gives up, and the call fails with RS_EHIP well
+    before the CUs free up.  Once they have, the next call scores bitwise like an idle GPU."""
+    import time
+    from asr_rescoring_amd._lib import RescoreError
+    monkeypatch.setenv("RS_LNGANG", gang)
+    base = scorer.score(nb_small)
+    side = torch.cuda.Stream()
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    _occupy(n_cu - 2, 4_000_000, side)
+    t0 = time.perf_counter()
+    with pytest.raises(RescoreError, match="timed out"):
+        scorer.score(nb_small)
+    dt = time.perf_counter() - t0
+    side.synchronize()
+    print(f"RS_EHIP after {dt:.2f} s with 2 free CUs ({gang})")
+    assert dt < 3.5, dt
+    assert np.array_equal(scorer.score(nb_small), base)
+
+
+def test_lnfuse_three_free_slots_suffice(scorer, nb_small, monkeypatch):
+    """All but three CUs held: the ticket gangs (three start-order tickets anywhere) still form and
+    the call scores bitwise like an idle GPU."""
+    monkeypatch.setenv("RS_LNGANG", "ticket")
+    base = scorer.score(nb_small)
+    side = torch.cuda.Stream()
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    _occupy(n_cu - 3, 2_000_000, side)
+    got = scorer.score(nb_small)
+    torch.cuda.synchronize()
+    assert np.array_equal(got, base)
 
 
 def test_chunks_at_gang_rounds_match(w_base, nb_mid, monkeypatch):
