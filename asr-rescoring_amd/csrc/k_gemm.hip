@@ -762,6 +762,12 @@ enum : int {
 };
 constexpr size_t lnr_counter_bytes() { return (size_t)LNC_TAB * 8 + (size_t)LNC_TAB_N * 8; }
 
+// Bound of every wait in a LayerNorm-GEMM launch, in ticks of the constant 100 MHz s_memrealtime
+// clock: 1 s (RS_LNFUSE_DIAG=8, tests: 10 us).  A wait whose peers are co-resident ends in
+// microseconds; one that runs out means they are not (or another workgroup gave up first).
+__device__ __forceinline__ unsigned long long lnr_wait_ticks(int diag) { return (diag & 8) ? 1000ull : 100000000ull; }
+__device__ __forceinline__ unsigned long long lnr_now() { return __builtin_amdgcn_s_memrealtime(); }
+
 typedef __attribute__((address_space(1))) unsigned lgu32;
 typedef __attribute__((address_space(1))) unsigned long long lgu64;
 __device__ __forceinline__ unsigned lnr_add(unsigned* c, int w, unsigned v = 1u) {
@@ -787,23 +793,22 @@ __device__ unsigned lnr_gang_ticket(const EpiArgs& ep, int ntn_) {
     const unsigned ntn = (unsigned)ntn_, G = gridDim.x;
     const unsigned long long tag = (unsigned long long)ep.ln_tag << 32;
     unsigned long long* tab = (unsigned long long*)c + LNC_TAB;
-    const unsigned spin_max = (ep.diag & 8) ? (1u << 8) : (1u << 20);
+    const unsigned long long t_lim = lnr_wait_ticks(ep.diag), t_start = lnr_now();
     auto join = [&](unsigned long long* slot, bool completes, unsigned& gid) -> bool {   // false: timed out
         if (completes) {
             gid = lnr_add(c, LNC_GANGS);
             __hip_atomic_store((lgu64*)slot, tag | gid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             return true;
         }
-        for (unsigned spins = 0; spins < spin_max; ++spins) {
+        for (unsigned spins = 1;; ++spins) {
             const unsigned long long v = __hip_atomic_load((const lgu64*)slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if ((v >> 32) == (tag >> 32)) {
                 gid = (unsigned)v;
                 return true;
             }
-            if ((spins & 255) == 255 && lnr_ld(ep.lnerr, 0)) return false;
+            if ((spins & 63) == 0 && (lnr_now() - t_start > t_lim || lnr_ld(ep.lnerr, 0))) return false;
             __builtin_amdgcn_s_sleep(1);
         }
-        return false;
     };
     unsigned x;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
@@ -821,7 +826,7 @@ __device__ unsigned lnr_gang_ticket(const EpiArgs& ep, int ntn_) {
             ok = join(slot, true, gid);
         } else {
             ok = false;
-            for (unsigned spins = 0; spins < spin_max; ++spins) {
+            for (unsigned spins = 1;; ++spins) {
                 const unsigned long long v = __hip_atomic_load((const lgu64*)slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 if ((v >> 32) == (tag >> 32)) {
                     gid = (unsigned)v;
@@ -833,7 +838,7 @@ __device__ unsigned lnr_gang_ticket(const EpiArgs& ep, int ntn_) {
                     ovf = ok = true;
                     break;
                 }
-                if ((spins & 255) == 255 && lnr_ld(ep.lnerr, 0)) break;
+                if ((spins & 63) == 0 && (lnr_now() - t_start > t_lim || lnr_ld(ep.lnerr, 0))) break;
                 __builtin_amdgcn_s_sleep(1);
             }
         }
@@ -1243,6 +1248,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                     float ps[2][4], pq[2][4];
                     bool failed = false;
                     stamp(3);                                     // tile statistics + publish (wave 0)
+                    const unsigned long long t_lim = lnr_wait_ticks(ep.diag), t_start = lnr_now();
                     for (unsigned spins = 0;;) {
                         bool ok = true;
 #pragma unroll
@@ -1266,9 +1272,9 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         // bounded: a wait that cannot end (the gang's workgroups not co-resident)
                         // sets the sticky error word; a wait that sees the word set (another
                         // workgroup timed out) gives up too, so the launch drains fast
-                        ++spins;
-                        if (spins == ((ep.diag & 8) ? (1u << 8) : (1u << 20)) ||
-                            ((spins & 255) == 0 && __hip_atomic_load((const gu32*)ep.lnerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
+                        if ((++spins & 63) == 0 &&
+                            (lnr_now() - t_start > t_lim ||
+                             __hip_atomic_load((const gu32*)ep.lnerr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))) {
                             if (lane == 0) __hip_atomic_store((gu32*)ep.lnerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                             failed = true;
                             break;
