@@ -51,7 +51,8 @@ struct EpiArgs {
     const float* res_g0;
     const float* res_b0;
     // EPI_LNRES_IMG: LN = (res_g, res_b, ln_eps) over nlog columns; lnx: lnres_granules(M)
-    // 8-B granules [M/256][N/256][256][2] {ln_tag, sum | M2} (zeroed once by the owner); lncnt:
+    // 8-B granules [M/256][N/256][256][2] {ln_tag, sum | M2}, then [M/256] {ln_tag, panel list}
+    // (zeroed once by the owner); lncnt:
     // lnres_counter_bytes() of gang-ticket words and gang-id slots (zeroed once by the owner, left
     // zeroed by every launch); lnerr (sticky, the caller's): set to 1 when a statistics or gang wait
     // timed out; ln_tag: set by the launch
@@ -63,7 +64,8 @@ struct EpiArgs {
     int diag;              // EPI_LNRES_IMG: 8 = every wait times out (RS_LNFUSE_DIAG, tests); 0 in production
     unsigned long long* dbg;  // stamp builds only (rs_debug_stamps): per-workgroup phase cycle sums
 };
-inline size_t lnres_granules(int m_pad) { return (size_t)m_pad * 4 * 2; }     // <= 4 column tiles
+// <= 4 column tiles of 256 rows x 2 statistics granules, then one list-claim granule per row panel
+inline size_t lnres_granules(int m_pad) { return (size_t)m_pad * 4 * 2 + (size_t)m_pad / 256 + 1; }
 
 // fp16 operand image of an fp32 activation row with logical width K:
 //   kx == 1: [hi]                          (RS_PREC_FP16)

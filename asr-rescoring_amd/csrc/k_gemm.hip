@@ -750,22 +750,24 @@ gemm_persist_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K,
 // Counter words of ep.lncnt (zeroed once by the owner; the last workgroup to finish a launch zeroes
 // them again, lnr_done, so each launch on the stream starts from zero — no host-side ticket state):
 enum : int {
-    LNC_TICKET = 0,        // global start-order ticket
     LNC_DONE = 16,         // workgroups finished
     LNC_LOCAL = 32,        // + 16 x: XCD x's local ticket (own 64-B line each)
-    LNC_STARTED = 160,     // workgroups that took their local ticket
-    LNC_OVF = 176,         // overflow ticket
-    LNC_GANGS = 192,       // gang ids handed out
+    LNC_OVF = 176,         // overflow ticket (every gang of RS_LNGANG=ticket)
+    LNC_GANGS = 192,       // panel lists taken
     LNC_WORDS = 256,
-    LNC_TAB = 128,         // u64 index of the gang-id slots {ln_tag, id}: [8][128] local, then [256] overflow
+    LNC_TAB = 128,         // u64 index of the gang slots {ln_tag, state}: [8][128] local, then [256] overflow
     LNC_TAB_N = 8 * 128 + 256,
 };
 constexpr size_t lnr_counter_bytes() { return (size_t)LNC_TAB * 8 + (size_t)LNC_TAB_N * 8; }
 
-// Bound of every wait in a LayerNorm-GEMM launch, in ticks of the constant 100 MHz s_memrealtime
-// clock: 1 s (RS_LNFUSE_DIAG=8, tests: 10 us).  A wait whose peers are co-resident ends in
-// microseconds; one that runs out means they are not (or another workgroup gave up first).
+// Bounds of the waits in a LayerNorm-GEMM launch, in ticks of the constant 100 MHz s_memrealtime
+// clock.  Statistics (between members of a formed gang, which have all started): 1 s.  Gang
+// formation (a member waiting for workgroups that have not started — under another tenant's
+// kernels they start when a CU frees up in their shader engine): 10 s, a hang guard only.
+// RS_LNFUSE_DIAG=8 (tests): 10 us.  A wait that runs out sets the sticky error word; every other
+// wait that sees it gives up, so the launch drains and the call returns RS_EHIP.
 __device__ __forceinline__ unsigned long long lnr_wait_ticks(int diag) { return (diag & 8) ? 1000ull : 100000000ull; }
+__device__ __forceinline__ unsigned long long lnr_form_ticks(int diag) { return (diag & 8) ? 1000ull : 1000000000ull; }
 __device__ __forceinline__ unsigned long long lnr_now() { return __builtin_amdgcn_s_memrealtime(); }
 
 typedef __attribute__((address_space(1))) unsigned lgu32;
@@ -777,82 +779,144 @@ __device__ __forceinline__ unsigned lnr_ld(const unsigned* c, int w) {
     return __hip_atomic_load((const lgu32*)(c + w), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// XCD: gangs inside one XCD (its column tiles then read their shared A panel through one L2) —
-// XCD x's workgroups take local tickets in start order; every n_tiles_n consecutive local tickets
-// below cap = floor(floor(G / 8) / ntn) * ntn form a gang, the rest (and the members of a local gang
-// that can never fill: its XCD received fewer workgroups, seen once every workgroup of the grid has
-// taken its local ticket) form gangs from a global overflow ticket, again in start order.  With the
-// observed round-robin placement no workgroup waits for the grid to start; the protocol does not
-// depend on placement (HIP promises none).  Otherwise: gangs of consecutive global tickets.
-// A gang's member that completes it takes the gang id and publishes it tagged with ln_tag; the
-// others poll (bounded: a timeout sets the sticky error word and returns an id past the tiles).
+// Gangs (thread 0 of every workgroup, once at its start).  A gang = the ntn workgroups computing
+// the column tiles of the same row panels, formed only from workgroups that have STARTED (the
+// hardware dispatches a grid's workgroups round-robin over the 32 shader engines, and one whose
+// engine is full waits there however many CUs are free elsewhere: blockIdx says nothing about
+// co-residency).  XCD (RS_LNGANG=xcd): gangs inside one XCD (its column tiles then read their
+// shared A panel through one L2) — XCD x's workgroups take local tickets in start order, and every
+// ntn consecutive local tickets below cap = floor(floor(G / 8) / ntn) * ntn form a local gang.
+// Otherwise, and for the local tickets past cap and the members of cancelled local gangs: gangs of
+// ntn consecutive overflow tickets, in start order.  A gang is settled exactly once in its slot
+// {ln_tag, state} by compare-and-swap: its completing member claims it (PENDING), takes the next
+// panel list and publishes its id; a waiting member cancels it instead when every list has been
+// taken (no work is left for it), or, for a local gang, after LNR_CANCEL_TICKS (its XCD has fewer
+// than ntn free slots: the members regroup chip-wide).  Whoever wins decides for every member,
+// present or arriving later.  Panel lists: list l of NL = min(G / ntn, panels) holds the row panels
+// l, l + G / ntn, ...; a gang walks its list (member m keeps column tile m), then takes the next
+// untaken list (lnr: the list counter; in the normal case none is left, every gang having formed
+// with its own), so the lists of gangs that never formed — workgroups held off by another tenant
+// — are computed by the gangs that did, and nothing waits for a workgroup that has not started.
+// Returns l * ntn + m (l >= NL: no work) or ~0u after a timeout (the launch drains).
+constexpr unsigned LNR_PENDING = 0xfffffffeu, LNR_CANCELLED = 0xffffffffu;
+constexpr unsigned long long LNR_CANCEL_TICKS = 5000ull;      // 50 us of the 100 MHz clock
 template <bool XCD>
-__device__ unsigned lnr_gang_ticket(const EpiArgs& ep, int ntn_) {
+__device__ unsigned lnr_gang_ticket(const EpiArgs& ep, int ntn_, int n_panels) {
     unsigned* c = ep.lncnt;
-    if constexpr (!XCD) return lnr_add(c, LNC_TICKET);
     const unsigned ntn = (unsigned)ntn_, G = gridDim.x;
     const unsigned long long tag = (unsigned long long)ep.ln_tag << 32;
     unsigned long long* tab = (unsigned long long*)c + LNC_TAB;
-    const unsigned long long t_lim = lnr_wait_ticks(ep.diag), t_start = lnr_now();
-    auto join = [&](unsigned long long* slot, bool completes, unsigned& gid) -> bool {   // false: timed out
-        if (completes) {
-            gid = lnr_add(c, LNC_GANGS);
-            __hip_atomic_store((lgu64*)slot, tag | gid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            return true;
+    const unsigned long long t_lim = lnr_form_ticks(ep.diag), t_start = lnr_now();
+    auto ld64 = [](unsigned long long* p) {
+        return __hip_atomic_load((const lgu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
+    auto cas64 = [](unsigned long long* p, unsigned long long& expect, unsigned long long want) {
+        return __hip_atomic_compare_exchange_strong((lgu64*)p, &expect, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT);
+    };
+    const unsigned NL = min(G / ntn, (unsigned)n_panels);
+    auto exhausted = [&]() { return lnr_ld(c, LNC_GANGS) >= NL; };
+    // the completing member: claim the slot (unless cancelled), take a panel list, publish its id
+    auto complete = [&](unsigned long long* slot, unsigned& gid) -> bool {
+        unsigned long long v = ld64(slot);
+        for (;;) {
+            if ((v >> 32) == (tag >> 32)) return false;                // cancelled (no one else claims)
+            if (cas64(slot, v, tag | LNR_PENDING)) break;
         }
+        gid = lnr_add(c, LNC_GANGS);
+        __hip_atomic_store((lgu64*)slot, tag | gid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return true;
+    };
+    // a waiting member: 1 published (gid), -1 cancelled, 0 timed out / the error word set
+    auto await_id = [&](unsigned long long* slot, bool local, unsigned& gid) -> int {
+        const unsigned long long t0 = lnr_now();
         for (unsigned spins = 1;; ++spins) {
-            const unsigned long long v = __hip_atomic_load((const lgu64*)slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            unsigned long long v = ld64(slot);
             if ((v >> 32) == (tag >> 32)) {
-                gid = (unsigned)v;
-                return true;
+                const unsigned st = (unsigned)v;
+                if (st == LNR_CANCELLED) return -1;
+                if (st != LNR_PENDING) {
+                    gid = st;
+                    return 1;
+                }
+            } else if ((local && lnr_now() - t0 > ((ep.diag & 8) ? 0ull : LNR_CANCEL_TICKS)) || exhausted()) {
+                if (cas64(slot, v, tag | LNR_CANCELLED)) return -1;
+                continue;                                          // settled meanwhile: read it again
             }
-            if ((spins & 63) == 0 && (lnr_now() - t_start > t_lim || lnr_ld(ep.lnerr, 0))) return false;
+            if ((spins & 63) == 0 && (lnr_now() - t_start > t_lim || lnr_ld(ep.lnerr, 0))) return 0;
             __builtin_amdgcn_s_sleep(1);
         }
     };
-    unsigned x;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-    x &= 7;
-    const unsigned cap = (G / 8) / ntn * ntn;
-    const unsigned lc = lnr_add(c, LNC_LOCAL + 16 * (int)x);
-    lnr_add(c, LNC_STARTED);                                  // after the local ticket
     unsigned gid = 0, mem = 0;
-    bool ovf = lc >= cap, ok = true;
-    if (!ovf) {
-        const unsigned k = lc / ntn;
-        mem = lc - k * ntn;
-        unsigned long long* slot = tab + x * 128 + k;
-        if (mem + 1 == ntn) {
-            ok = join(slot, true, gid);
-        } else {
-            ok = false;
-            for (unsigned spins = 1;; ++spins) {
-                const unsigned long long v = __hip_atomic_load((const lgu64*)slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((v >> 32) == (tag >> 32)) {
-                    gid = (unsigned)v;
-                    ok = true;
-                    break;
-                }
-                // every workgroup has its local ticket: XCD x's count is final
-                if (lnr_ld(c, LNC_STARTED) == G && lnr_ld(c, LNC_LOCAL + 16 * (int)x) < ntn * (k + 1)) {
-                    ovf = ok = true;
-                    break;
-                }
-                if ((spins & 63) == 0 && (lnr_now() - t_start > t_lim || lnr_ld(ep.lnerr, 0))) break;
-                __builtin_amdgcn_s_sleep(1);
+    bool ovf = !XCD, ok = true;
+    if constexpr (XCD) {
+        unsigned x;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+        x &= 7;
+        const unsigned cap = (G / 8) / ntn * ntn;
+        const unsigned lc = lnr_add(c, LNC_LOCAL + 16 * (int)x);
+        ovf = lc >= cap;
+        if (!ovf) {
+            const unsigned k = lc / ntn;
+            mem = lc - k * ntn;
+            unsigned long long* slot = tab + x * 128 + k;
+            if (mem + 1 == ntn) {
+                ovf = !complete(slot, gid);
+            } else {
+                const int r = await_id(slot, true, gid);
+                ok = r != 0;
+                ovf = r < 0;
             }
         }
     }
     if (ovf && ok) {
         const unsigned o = lnr_add(c, LNC_OVF), k = o / ntn;
         mem = o - k * ntn;
-        ok = k < 256 && join(tab + 8 * 128 + k, mem + 1 == ntn, gid);
+        unsigned long long* slot = tab + 8 * 128 + k;
+        if (k >= 256) {
+            ok = false;
+        } else if (mem + 1 == ntn) {
+            if (!complete(slot, gid)) gid = NL;                        // cancelled: no work left
+        } else {
+            const int r = await_id(slot, false, gid);
+            ok = r != 0;
+            if (r < 0) gid = NL;
+        }
     }
     if (!ok) {
         __hip_atomic_store((lgu32*)ep.lnerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         return 0xffffffffu;
     }
-    return gid * ntn + mem;
+    return gid >= NL ? 0xfffffffeu : gid * ntn + mem;
+}
+
+// The transition after the last tile of a gang's panel list (panel p, column tile tcol): column tile
+// 0's wave 0 publishes the list it took (nlist, its lane 0) in the claim granule of panel p, after
+// the launch's statistics granules; every wave of every member reads it there.  t = the new list's
+// first tile, or past the tiles.  false: the wait ran out or the error word is set (the launch
+// drains; the sticky word is set).
+__device__ __forceinline__ bool lnr_next_list(const EpiArgs& ep, int& t, unsigned nlist, int p, int tcol, int ntn,
+                                              int n_tiles, int wave, int lane) {
+    const int n_panels = n_tiles / ntn;
+    const unsigned NL = min((unsigned)(gridDim.x / ntn), (unsigned)n_panels);
+    const unsigned long long tag = (unsigned long long)ep.ln_tag << 32;
+    unsigned long long* clm = (unsigned long long*)ep.lnx + (size_t)n_panels * ntn * 512 + p;
+    if (tcol == 0 && wave == 0 && lane == 0)
+        __hip_atomic_store((lgu64*)clm, tag | nlist, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long t_lim = lnr_wait_ticks(ep.diag), t_start = lnr_now();
+    for (unsigned spins = 1;; ++spins) {
+        const unsigned long long v = __hip_atomic_load((const lgu64*)clm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((v >> 32) == (tag >> 32) && !(ep.diag & 8)) {
+            const unsigned l = (unsigned)v;
+            t = l < NL ? (int)l * ntn + tcol : n_tiles;
+            return true;
+        }
+        if ((spins & 63) == 0 && (lnr_now() - t_start > t_lim || lnr_ld(ep.lnerr, 0))) {
+            if (lane == 0) __hip_atomic_store((lgu32*)ep.lnerr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+    }
 }
 
 // End of a workgroup (thread 0): the last of the grid zeroes the counters for the next launch
@@ -860,9 +924,9 @@ __device__ unsigned lnr_gang_ticket(const EpiArgs& ep, int ntn_) {
 __device__ __forceinline__ void lnr_done(const EpiArgs& ep) {
     unsigned* c = ep.lncnt;
     if (lnr_add(c, LNC_DONE) + 1 != gridDim.x) return;
-    const int w[] = {LNC_TICKET, LNC_STARTED, LNC_OVF, LNC_GANGS, LNC_DONE};
+    const int w[] = {LNC_OVF, LNC_GANGS, LNC_DONE};
     for (int x = 0; x < 8; ++x) __hip_atomic_store((lgu32*)(c + LNC_LOCAL + 16 * x), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    for (int i = 0; i < 5; ++i) __hip_atomic_store((lgu32*)(c + w[i]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = 0; i < 3; ++i) __hip_atomic_store((lgu32*)(c + w[i]), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <int EPI, int VAR>
@@ -910,9 +974,10 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         // Gangs: a row panel's n_tiles_n column tiles are computed by n_tiles_n workgroups that
         // exchange row statistics (lnres_epilogue), so a gang must consist of workgroups that have
         // all STARTED: gangs are formed from tickets taken at start, never from blockIdx.  A gang
-        // (id g of G / ntn) walks the panels g, g + G / ntn, ...; member m keeps column tile m:
-        // first tile g * ntn + m, then t += gridDim.x.  lnr_gang_ticket (thread 0) returns g * ntn + m.
-        if (tid == 0) *(unsigned*)(slabs + 2048) = lnr_gang_ticket<(VAR & 134217728) != 0>(ep, n_tiles_n);
+        // walks panel list l (panels l, l + G / ntn, ...; member m keeps column tile m: first tile
+        // l * ntn + m, then t += gridDim.x), then the next untaken list.  lnr_gang_ticket (thread 0)
+        // returns l * ntn + m.
+        if (tid == 0) *(unsigned*)(slabs + 2048) = lnr_gang_ticket<(VAR & 134217728) != 0>(ep, n_tiles_n, n_tiles / n_tiles_n);
         __syncthreads();
         t = (int)*(const unsigned*)(slabs + 2048);
     }
@@ -1046,6 +1111,14 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     int par = 0;                                                  // buffer of K-step 0
     bool first = true;
     for (;;) {
+        // LNR, the last tile of the gang's panel list: column tile 0's wave 0 takes the next list
+        // now (the youngest memory operation here: its return is waited for by K-step 1, a step
+        // later) and hands it over at the transition
+        unsigned nlist = 0;
+        if constexpr (LNR) {
+            if (m0 / BM + (int)gridDim.x / n_tiles_n >= n_tiles / n_tiles_n && n0 == 0 && wave == 0 && lane == 0)
+                nlist = lnr_add(ep.lncnt, LNC_GANGS);
+        }
 #pragma unroll
         for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -1100,6 +1173,9 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         // need not cover this DMA, measured -2.7 %: profiles/r3p2_lnperm_ab.txt)
         bool more = false;
         t += gridDim.x;
+        if constexpr (LNR) {
+            if (t >= n_tiles && !lnr_next_list(ep, t, nlist, cm0 / BM, cn0 / BM, n_tiles_n, n_tiles, wave, lane)) break;
+        }
         more = t < n_tiles;
         if (more) {
             tile_of(t, m0, n0);
@@ -1718,11 +1794,17 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
 // Test utility (not part of the scoring path): keeps `blocks` workgroups resident for `usec`
 // microseconds, one per CU (each declares the whole 160 KiB of LDS), on `stream` — a kernel of
 // another stream (or process) holding CUs while the scorer runs.  Bounded by the constant-rate
-// s_memrealtime clock (100 MHz): every wave exits once the time is up.
+// s_memrealtime clock (100 MHz): every wave exits once the time is up.  d_out (may be null,
+// 3 x blocks ints): [0, blocks) spins, [blocks, 2 blocks) where the workgroup ran (XCC_ID << 24 |
+// HW_ID bits 23:0: CU_ID 11:8, SH_ID 12, SE_ID 15:13), [2 blocks, 3 blocks) its start time
+// (s_memrealtime, low 32 bits).
 namespace {
 __global__ void __launch_bounds__(64) occupy_kernel(long long ticks, int* out) {
     extern __shared__ int lds_hold[];
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    unsigned hw, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)\n\ts_getreg_b32 %1, hwreg(HW_REG_XCC_ID)"
+                 : "=s"(hw), "=s"(xcc));
     int spins = 0;
     while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < ticks) {
         __builtin_amdgcn_s_sleep(8);
@@ -1730,12 +1812,16 @@ __global__ void __launch_bounds__(64) occupy_kernel(long long ticks, int* out) {
     }
     lds_hold[threadIdx.x] = spins;
     __syncthreads();
-    if (threadIdx.x == 0 && out) out[blockIdx.x] = lds_hold[0];     // vector store
+    if (threadIdx.x == 0 && out) {                                 // vector stores
+        out[blockIdx.x] = lds_hold[0];
+        out[gridDim.x + blockIdx.x] = (int)(((xcc & 15u) << 24) | (hw & 0xffffffu));
+        out[2 * gridDim.x + blockIdx.x] = (int)(unsigned)t0;
+    }
 }
 }  // namespace
 
 extern "C" int rs_debug_occupy(int blocks, int usec, int* d_out, void* stream) {
-    if (blocks <= 0 || blocks > 4096 || usec <= 0 || usec > 5000000) return -1;
+    if (blocks <= 0 || blocks > 1365 || usec <= 0 || usec > 5000000) return -1;
     constexpr int smem = 160 * 1024;
     static std::atomic<unsigned> attr_devs{0};
     if (smem_attr_once((const void*)occupy_kernel, smem, attr_devs) != hipSuccess) return -2;

@@ -21,10 +21,15 @@
  *     than the previous call first makes its stream wait (device-side) for the previous call's
  *     work.  Results are deterministic (no float atomics, fixed reduction orders).
  *   - The fused residual + LayerNorm GEMM (fp16x3 mode) exchanges row statistics between the
- *     N_pad / 256 workgroups of a row panel inside one launch; those workgroups must be able to
- *     run at the same time (3 free workgroup slots for bert-base: on one XCD with the default
- *     RS_LNGANG=xcd, anywhere on the GPU with RS_LNGANG=ticket).  On a GPU so full of other work
- *     that they cannot, the bounded wait ends the call in RS_EHIP instead of hanging.
+ *     N_pad / 256 workgroups of a row panel inside one launch (a gang).  Gangs are formed only
+ *     from workgroups that have started, and the row panels come in lists that a gang takes from a
+ *     counter, so the lists of gangs that never formed (workgroups held off by another tenant) are
+ *     computed by those that did: the launch completes on whatever CUs it gets, with 3 free
+ *     workgroup slots anywhere on the GPU for bert-base.  The hardware dispatches a grid's
+ *     workgroups round-robin over the 32 shader engines (8 XCDs x 4); while another tenant fills a
+ *     whole engine, the workgroups dispatched to it (of this kernel or any other) wait for it.
+ *     Every wait inside a launch is bounded (statistics 1 s, gang formation 10 s): one that runs
+ *     out ends the call in RS_EHIP instead of hanging.
  */
 #ifndef RESCORE_H_
 #define RESCORE_H_
