@@ -71,7 +71,7 @@ inline size_t lnres_granules(int m_pad) { return (size_t)m_pad * 4 * 2 + (size_t
 //   kx == 1: [hi]                          (RS_PREC_FP16)
 //   kx == 3: [hi | hi/64 | (x - hi)*64]    (RS_PREC_FP16X3, K-concatenated GEMM form)
 //   kx == 2: [hi | (x - hi)*64]            (RS_PREC_FP16X3, split-operand GEMM form: the
-//            x3s kernel forms hi/64 in registers; weights use the first two parts of their
+//            x3s kernel forms 64 W_hi in registers; weights use the first two parts of their
 //            three-part image, [W_hi | W_lo*64])
 // paired with the weight image [W_hi | W_lo*64 | W_hi/64] the K-concatenated MFMA product is
 // A_hi.W_hi + A_hi.W_lo + A_lo.W_hi (the power-of-two factors cancel exactly): fp32-level

@@ -6,6 +6,8 @@ Variants of gemm_x3s_kernel through rs_debug_gemm (cfg 32 fp32 out, cfg 31 GELU 
   alias    every tile stores onto row panel 0 (no HBM write burst; L2-resident lines)
   nw+al    both
   noepi    no stores (bias / GELU math kept)
+PROBE=scale: prod / noscale (no in-register operand scaling in the K loop: 64 W_hi since round 5,
+W_hi/64 and A_hi/64 before) / noepi / bare (no staging, no stores) / bare-noscale.
 Rounds interleaved in one process; medians.  TF/s of MFMA work (3 x 2MNK).
 Usage: python tools/x3s_epi_probe.py [M] [rounds]
 """
@@ -42,21 +44,12 @@ def main():
         out32 = torch.empty(M, N, device=dev)
         img = torch.empty(M, 2 * N, device=dev, dtype=torch.float16)
         fl = 3 * 2.0 * M * N * K
-        var = {"f32": (32, out32, {"prod": 0, "pp": 60, "nowait": 50, "alias": 51, "nw+al": 53, "noepi": 20}),
-               "gelu2": (31, img, {"prod": 0, "pp": 60, "nowait": 50, "alias": 51, "nw+al": 53, "noepi": 52})}
-        if os.environ.get("PROBE") == "pp":
-            # the ping-pong kernel's costs (fp32 output): without stores, halves in phase, without
-            # W loads, with no loads at all; against gemm_x3s_kernel's no-epilogue / bare loop
-            var = {"f32": (32, out32, {"x3s": 0, "x3s-noepi": 20, "x3s-bare": 3, "pp": 60, "pp-noepi": 61,
-                                       "pp-inphase": 62, "pp-noepi-inphase": 63, "pp-noW": 64,
-                                       "pp-noW-noepi": 65, "pp-bare": 69})}
-        # the ping-pong kernel is bitwise equal to the production kernel (same MFMA order)
-        for cfg, o in ((32, out32), (31, img)) if os.environ.get("PROBE") != "pp" else ():
-            o2 = torch.empty_like(o)
-            assert fn(cfg, 0, A2.data_ptr(), W2.data_ptr(), b.data_ptr(), o.data_ptr(), M, N, K, st) == 0
-            assert fn(cfg, 60, A2.data_ptr(), W2.data_ptr(), b.data_ptr(), o2.data_ptr(), M, N, K, st) == 0
-            torch.cuda.synchronize()
-            print(f"pp == prod (cfg {cfg}, N={N}, K={K}): {torch.equal(o, o2)}", flush=True)
+        var = {"f32": (32, out32, {"prod": 0, "nowait": 50, "alias": 51, "nw+al": 53, "noepi": 20}),
+               "gelu2": (31, img, {"prod": 0, "nowait": 50, "alias": 51, "nw+al": 53, "noepi": 52})}
+        if os.environ.get("PROBE") == "scale":
+            # the K loop's in-register operand scaling: production, without it (dbg 4), and both
+            # against the bare loop (no staging, no stores: 3, 7)
+            var = {"f32": (32, out32, {"prod": 0, "noscale": 4, "noepi": 20, "bare": 3, "bare-noscale": 7})}
         times = {}
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for _ in range(rounds):
