@@ -21,6 +21,9 @@ def short(n):
     m = re.search(r"gemm_persist_kernelILi(\d+)ELi(\d+)E", n)
     if m:
         return f"persist<{m.group(1)},{m.group(2)}>"
+    m = re.search(r"attn16x3v2_kernelILb(\d)ELi(\d+)E", n)
+    if m:
+        return f"attn16x3v2<dedup{m.group(1)},R{m.group(2)}>"
     m = re.search(r"gemm_f16_kernelILi(\d+)ELi(\d+)E.*?ELi(\d+)ELi(\d+)EEEv", n)
     if m:
         return f"plain<{m.group(1)}x{m.group(2)},epi{m.group(3)},var{m.group(4)}>"
