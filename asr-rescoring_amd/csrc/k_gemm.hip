@@ -1181,10 +1181,16 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             if (t >= n_tiles && !lnr_next_list(ep, t, nlist, cm0 / BM, cn0 / BM, n_tiles_n, n_tiles, wave, lane)) break;
         }
         more = t < n_tiles;
+        // VAR 1073741824 (the LayerNorm build's default): the next tile's stage 0 issued after the
+        // row statistics instead (lnres_epilogue's caller) — its eight back-to-back DMA issues cost
+        // this phase ~6k cycles per tile here, where nothing hides them (the residual phase is
+        // unchanged either way; profiles/r5late0_stage0_after_stats.txt).  It still lands before the
+        // next tile's K-step 0, whose vmcnt(NSTORE) leaves only the younger epilogue stores in flight.
+        constexpr bool LATE0 = LNR && (VAR & 1073741824) != 0;
         if (more) {
             tile_of(t, m0, n0);
             set_rsrc(m0, n0);
-            stage(last ^ 1, 0);
+            if constexpr (!LATE0) stage(last ^ 1, 0);
         }
         stamp(1);                                                 // bias wait + next tile's stage 0
         // bias (+ GELU) of row blocks [i0, i1)
@@ -1224,7 +1230,10 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                     half4 rh0[RB2][4], rl0[RB2][4];
 #pragma unroll
                     for (int ii = 0; ii < RB2; ++ii) {
-                        const f16* prow_img = img + (size_t)(cm0 + wm * WTM + 16 * (RB2 * hh + ii) + r16) * ldc;
+                        // VAR 536870912 (timing diagnostic, wrong results): the residual is read
+                        // from row panel 0 (L2-resident lines) — the read without its HBM traffic
+                        const int rm0 = (VAR & 536870912) ? 0 : cm0;
+                        const f16* prow_img = img + (size_t)(rm0 + wm * WTM + 16 * (RB2 * hh + ii) + r16) * ldc;
                         if constexpr (PERM) {
                             // blocks 2m, 2m + 1: 8 consecutive columns, one 16-B load per image
 #pragma unroll
@@ -1410,6 +1419,9 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 if (lnres_epilogue()) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile's stage 0 landed
                     break;
+                }
+                if constexpr (LATE0) {
+                    if (more) stage(last ^ 1, 0);
                 }
             } else if constexpr (!LATE) finish(0, 8);
             if constexpr ((VAR & 2) != 0) {      // diagnostic: no epilogue stores (acc kept alive)
@@ -1692,7 +1704,9 @@ hipError_t launch_gemm_x3s_v(int epi, const f16* A, const f16* W, int ldw, int M
             // workgroups co-resident anywhere instead of on one XCD.
             const char* g = getenv("RS_LNGANG");
             const bool xcd = !(g && !strcmp(g, "ticket"));
-            constexpr int VL = 16777216 | STV;
+            // VAR 1073741824: the next tile's stage 0 issued after the row statistics (O-projection
+            // -1.1 %, BertOutput -0.7 %, profiles/r5late0_stage0_after_stats.txt)
+            constexpr int VL = 16777216 | 1073741824 | STV;
             if (xcd) {
                 if (K > 1024) return launch_x3s<EPI_LNRES_IMG, VL | 67108864 | 134217728>(A, W, M_pad, N_pad, K, ep, st, ldw);
                 return launch_x3s<EPI_LNRES_IMG, VL | 134217728>(A, W, M_pad, N_pad, K, ep, st, ldw);
