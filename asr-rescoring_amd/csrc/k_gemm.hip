@@ -1030,6 +1030,14 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         for (int l = 0; l < 2; ++l) {
             voffA[2 * h + l] = ((prow + 128 * h) * (int)ld2 + l * K + pswz) * 2;
             voffW[2 * h + l] = (wperm(prow + 128 * h) * ldw + l * K + pswz) * 2;
+            if constexpr ((VAR & 4096) != 0) {
+                // VAR 4096 (timing diagnostic, wrong results): each DMA piece covers 8 rows x 128 B
+                // (K-step t: bytes [128 t, 128 t + 128) of the row) instead of 16 rows x 64 B — the
+                // same rows and bytes per K loop, full-line requests
+                const int drow = wave * 16 + (lane >> 3) + 8 * l + 128 * h;
+                voffA[2 * h + l] = (drow * (int)ld2 + (lane & 7) * 8) * 2;
+                voffW[2 * h + l] = (wperm(drow) * ldw + (lane & 7) * 8) * 2;
+            }
         }
     auto set_rsrc = [&](int m0, int n0) {
         rsA = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * ld2), (short)0, (int)(256 * ld2 * 2), 0x00020000);
@@ -1040,7 +1048,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         const int r = p >> 1;
         auto* dst = (__attribute__((address_space(3))) void*)(smem + buf * STAGE + r * REG + ((p & 1) * 8 + wave) * 1024);
         const int vo = (r < 2 ? voffA : voffW)[2 * (p & 1) + (r & 1)];
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 16, vo, k0 * 2, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 16, vo, (VAR & 4096) ? k0 * 4 : k0 * 2, 0, 0);
     };
     auto stage = [&](int buf, int k0) {
 #pragma unroll
@@ -1225,11 +1233,28 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 // accumulators, and the spills that forced reloaded values whose waits drained the
                 // next tile's stage 0 inside the statistics publish)
                 constexpr int RB2 = 2;
+                // VAR 8388608 (timing diagnostic, wrong results): the residual add skipped
 #pragma unroll
                 for (int hh = 0; hh < 8 / RB2; ++hh) {
+                    if constexpr ((VAR & 8388608) != 0) break;
                     half4 rh0[RB2][4], rl0[RB2][4];
 #pragma unroll
                     for (int ii = 0; ii < RB2; ++ii) {
+                        if constexpr ((VAR & 2097152) != 0) {
+                            // VAR 2097152 (timing diagnostic, wrong results): the same rows, bytes and
+                            // lines, but each load covers 8 rows x 128 B instead of 16 rows x 64 B
+#pragma unroll
+                            for (int m = 0; m < 2; ++m) {
+                                const f16* p = img + (size_t)(cm0 + wm * WTM + 16 * (RB2 * hh + ii) + (r16 >> 1) + 8 * m) * ldc +
+                                               cn0 + wn * WTN + 8 * (4 * (r16 & 1) + q4);
+                                const half8 vh = *(const half8*)p, vl = *(const half8*)(p + H);
+                                rh0[ii][2 * m] = (half4){vh[0], vh[1], vh[2], vh[3]};
+                                rh0[ii][2 * m + 1] = (half4){vh[4], vh[5], vh[6], vh[7]};
+                                rl0[ii][2 * m] = (half4){vl[0], vl[1], vl[2], vl[3]};
+                                rl0[ii][2 * m + 1] = (half4){vl[4], vl[5], vl[6], vl[7]};
+                            }
+                            continue;
+                        }
                         // VAR 536870912 (timing diagnostic, wrong results): the residual is read
                         // from row panel 0 (L2-resident lines) — the read without its HBM traffic
                         const int rm0 = (VAR & 536870912) ? 0 : cm0;
