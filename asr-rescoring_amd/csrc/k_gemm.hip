@@ -1033,10 +1033,11 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             if constexpr ((VAR & 4096) != 0) {
                 // VAR 4096 (timing diagnostic, wrong results): each DMA piece covers 8 rows x 128 B
                 // (K-step t: bytes [128 t, 128 t + 128) of the row) instead of 16 rows x 64 B — the
-                // same rows and bytes per K loop, full-line requests
+                // same rows and bytes per K loop, full-line requests (+ 16: W side only, + 32: A
+                // side only)
                 const int drow = wave * 16 + (lane >> 3) + 8 * l + 128 * h;
-                voffA[2 * h + l] = (drow * (int)ld2 + (lane & 7) * 8) * 2;
-                voffW[2 * h + l] = (wperm(drow) * ldw + (lane & 7) * 8) * 2;
+                if constexpr ((VAR & 16) == 0) voffA[2 * h + l] = (drow * (int)ld2 + (lane & 7) * 8) * 2;
+                if constexpr ((VAR & 32) == 0) voffW[2 * h + l] = (wperm(drow) * ldw + (lane & 7) * 8) * 2;
             }
         }
     auto set_rsrc = [&](int m0, int n0) {
@@ -1048,7 +1049,9 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         const int r = p >> 1;
         auto* dst = (__attribute__((address_space(3))) void*)(smem + buf * STAGE + r * REG + ((p & 1) * 8 + wave) * 1024);
         const int vo = (r < 2 ? voffA : voffW)[2 * (p & 1) + (r & 1)];
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 16, vo, (VAR & 4096) ? k0 * 4 : k0 * 2, 0, 0);
+        constexpr bool FLA = (VAR & 4096) && !(VAR & 16), FLW = (VAR & 4096) && !(VAR & 32);
+        const int so = (r < 2 ? FLA : FLW) ? k0 * 4 : k0 * 2;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 16, vo, so, 0, 0);
     };
     auto stage = [&](int buf, int k0) {
 #pragma unroll
