@@ -1021,6 +1021,13 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     // instead of two runs of 4: W image row 32 m + 16 jj + 4 q + e is W row 32 m + 8 q + 4 jj + e.
     // The epilogue's per-lane loads (bias, residual image, LayerNorm weights) become 16-B loads.
     constexpr bool PERM = (VAR & 16777216) != 0;
+    // VAR 64 (NOT instantiated — no launch path): the W image interleaved [hi 32 | lo 32] per
+    // 32-column K-step (one 128-B line per row and K-step: full-line DMA requests,
+    // profiles/r5kline2_per_operand.txt); W rows in LDS at a 128-B pitch, chunk c of row n at
+    // c ^ ((n >> 1) & 7).  Bitwise equal to production and 2.0-3.5 % faster at M = 262144, but one
+    // 1024-row call faulted (illegal address, cause not found): profiles/r5wil_w_interleaved.txt
+    constexpr bool WIL = (VAR & 64) != 0;
+    static_assert(!(WIL && (VAR & 4096)), "the interleaved W layout and the full-line diagnostic");
     auto wperm = [](int L) {
         return PERM ? (L & ~31) | (((L >> 2) & 3) << 3) | (((L >> 4) & 1) << 2) | (L & 3) : L;
     };
@@ -1030,6 +1037,13 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         for (int l = 0; l < 2; ++l) {
             voffA[2 * h + l] = ((prow + 128 * h) * (int)ld2 + l * K + pswz) * 2;
             voffW[2 * h + l] = (wperm(prow + 128 * h) * ldw + l * K + pswz) * 2;
+            if constexpr (WIL) {
+                // W image interleaved per K-step (VAR 64): piece (h, l) = LDS rows n = 128 h + 16 wave
+                // + 8 l + (lane >> 3), one 128-B line each ([hi 32 | lo 32] of the K-step); lane
+                // slot s = lane & 7 holds logical chunk s ^ ((n >> 1) & 7) (0-3 hi, 4-7 lo)
+                const int n = 128 * h + wave * 16 + 8 * l + (lane >> 3);
+                voffW[2 * h + l] = (wperm(n) * ldw + (((lane & 7) ^ ((n >> 1) & 7)) * 8)) * 2;
+            }
             if constexpr ((VAR & 4096) != 0) {
                 // VAR 4096 (timing diagnostic, wrong results): each DMA piece covers 8 rows x 128 B
                 // (K-step t: bytes [128 t, 128 t + 128) of the row) instead of 16 rows x 64 B — the
@@ -1047,10 +1061,12 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     auto piece = [&](int buf, int k0, int p) {
         if constexpr ((VAR & 1) != 0) return;     // diagnostic: no K-loop staging (stale tiles)
         const int r = p >> 1;
-        auto* dst = (__attribute__((address_space(3))) void*)(smem + buf * STAGE + r * REG + ((p & 1) * 8 + wave) * 1024);
+        const int dofs = (WIL && r >= 2) ? 2 * REG + ((p & 1) * 128 + wave * 16 + 8 * (r & 1)) * 128
+                                         : r * REG + ((p & 1) * 8 + wave) * 1024;
+        auto* dst = (__attribute__((address_space(3))) void*)(smem + buf * STAGE + dofs);
         const int vo = (r < 2 ? voffA : voffW)[2 * (p & 1) + (r & 1)];
         constexpr bool FLA = (VAR & 4096) && !(VAR & 16), FLW = (VAR & 4096) && !(VAR & 32);
-        const int so = (r < 2 ? FLA : FLW) ? k0 * 4 : k0 * 2;
+        const int so = (r < 2 ? FLA : (FLW || WIL)) ? k0 * 4 : k0 * 2;
         __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 16, vo, so, 0, 0);
     };
     auto stage = [&](int buf, int k0) {
@@ -1074,7 +1090,8 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     // down toward the fp16 subnormals the MFMA flushes.
     const int r16 = lane & 15, q4 = lane >> 4;
     const int offA16 = (wm * WTM + r16) * RB + ((q4 ^ g16(r16 >> 2)) << 4);
-    const int offW16 = 2 * REG + (wn * WTN + r16) * RB + ((q4 ^ g16(r16 >> 2)) << 4);
+    const int offW16 = WIL ? 2 * REG + (wn * WTN + r16) * 128 + ((q4 ^ ((r16 >> 1) & 7)) << 4)
+                           : 2 * REG + (wn * WTN + r16) * RB + ((q4 ^ g16(r16 >> 2)) << 4);
     f32x4 acc16[8][4];
     // the next step's eight DMA pieces ride this step's first MFMA groups (one per group of four
     // MFMAs of row half 0); the last step of a tile passes k0n = 2^29 and issues none (the same
@@ -1085,8 +1102,13 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         half8 wh[4], wl[4], wu[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            wh[j] = *(const half8*)(sb + offW16 + j * 1024);
-            wl[j] = *(const half8*)(sb + offW16 + REG + j * 1024);
+            if constexpr (WIL) {                                  // 16 rows of 128 B; lo = chunk ^ 4
+                wh[j] = *(const half8*)(sb + offW16 + j * 2048);
+                wl[j] = *(const half8*)(sb + (offW16 ^ 64) + j * 2048);
+            } else {
+                wh[j] = *(const half8*)(sb + offW16 + j * 1024);
+                wl[j] = *(const half8*)(sb + offW16 + REG + j * 1024);
+            }
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) wu[j] = (VAR & 4) ? wh[j] : wh[j] * up;       // VAR 4: timing diagnostic
