@@ -152,7 +152,16 @@ def main():
                     help="C3 runs, rank 0 at N=1: one timed pass of the full C4 set (0 = skip)")
     args = ap.parse_args()
 
+    # --gpus N without a launcher: N fresh rank processes (one per GPU) before any GPU call here;
+    # the parent only relays rank 0's JSON line (asr_rescoring_amd/launch.py)
+    from asr_rescoring_amd import launch
+    if launch.need_spawn(args.gpus):
+        rc = launch.spawn_ranks(args.gpus, sys.argv[1:], script=os.path.abspath(__file__))
+        sys.exit(rc if rc >= 0 else 128 - rc)
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus != world and int(os.environ.get("RANK", "0")) == 0:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: running {world} rank(s)", file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
