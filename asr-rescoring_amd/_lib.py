@@ -15,7 +15,7 @@ import torch  # noqa: F401  (must load torch's HIP runtime before librescore.so)
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 # RS_LIBRESCORE: another in-tree build of the same library (A/B timing of two builds in one GPU
-# session, tools/lib_ab.sh); default the library build.py writes
+# session); default the library build.py writes.  The override is announced on stderr.
 LIB_PATH = os.environ.get("RS_LIBRESCORE") or os.path.join(PKG_DIR, "librescore.so")
 
 RS_HEAD_MLM, RS_HEAD_CLS, RS_HEAD_EMB = 1, 2, 4
@@ -96,7 +96,23 @@ _SIGS = {
                                             ctypes.POINTER(ctypes.c_char_p), P]),
 }
 
-EXPORTED = tuple(_SIGS)
+# Diagnostic / test entries (not declared in include/rescore.h, not part of the scoring path).
+# Typed here so that every caller passes 64-bit pointers: an untyped ctypes call converts a Python
+# int to a 32-bit C int, and a truncated device pointer faults the kernel that dereferences it
+# (the round-5 "interleaved-W" illegal address: a test called rs_debug_gemm untyped).
+CI = ctypes.c_int
+_DEBUG_SIGS = {
+    "rs_debug_gemm": (CI, [CI, CI, P, P, P, P, CI, CI, CI, P]),
+    "rs_debug_attention": (CI, [CI, P, P, P, CI, CI, CI, P, P]),
+    "rs_debug_ln": (CI, [CI, CI] + [P] * 9),
+    "rs_debug_stamps": (CI, [CI, P]),
+    "rs_debug_occupy": (CI, [CI, CI, P, P]),
+    "rs_debug_sgemm_cfg": (CI, [CI] * 4 + [P, CI, CI, P, CI, CI, P, CI, CI, P]),
+    "rs_debug_sgemm": (CI, [CI] * 3 + [P, CI, CI, P, CI, CI, P, CI, CI, P]),
+    "rs_debug_sgemm_pick": (CI, [CI] * 5),
+}
+EXPORTED = tuple(_SIGS)          # the shipped library's entries (include/rescore.h)
+_SIGS.update(_DEBUG_SIGS)
 
 
 def load(path: str = LIB_PATH):
@@ -106,8 +122,15 @@ def load(path: str = LIB_PATH):
         return _lib
     if not os.path.exists(path):
         raise ImportError(f"{path} not found: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    if os.environ.get("RS_LIBRESCORE"):
+        import sys
+        print(f"librescore: RS_LIBRESCORE override {path}", file=sys.stderr)
     lib = ctypes.CDLL(path)
+    if not hasattr(lib, "rs_version"):
+        raise ImportError(f"{path} is not a librescore build (no rs_version)")
     for name, (res, args) in _SIGS.items():
+        if name in _DEBUG_SIGS and not hasattr(lib, name):
+            continue                          # RS_DIAG-only entry (rs_debug_stamps) in the shipped build
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args

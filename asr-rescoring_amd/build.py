@@ -50,13 +50,15 @@ def _stamp(target: str, deps, cmd) -> None:
         f.write(_digest(deps, cmd))
 
 
-def _compile(src: str) -> str:
+def _compile(src: str, csrc: str = CSRC, objdir: str = OBJ, include: str = os.path.join(REPO, "include"),
+             defines=()) -> str:
     host = src.endswith(".cpp")                     # host-only C++ (tokenizer / JSON front end)
-    obj = os.path.join(OBJ, os.path.basename(src).rsplit(".", 1)[0] + ".o")
-    deps = [src] + glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.inc")) \
-        + glob.glob(os.path.join(REPO, "include", "*.h"))
-    cmd = ([CXX, "-O2", "-std=c++17", "-fPIC", "-Wall", "-I", os.path.join(REPO, "include")] if host
-           else [HIPCC] + FLAGS) + ["-c", src, "-o", obj]
+    obj = os.path.join(objdir, os.path.basename(src).rsplit(".", 1)[0] + ".o")
+    deps = [src] + glob.glob(os.path.join(csrc, "*.h")) + glob.glob(os.path.join(csrc, "*.inc")) \
+        + glob.glob(os.path.join(include, "*.h"))
+    flags = [f if f != os.path.join(REPO, "include") else include for f in FLAGS]
+    cmd = ([CXX, "-O2", "-std=c++17", "-fPIC", "-Wall", "-I", include] if host
+           else [HIPCC] + flags + [f"-D{d}" for d in defines]) + ["-c", src, "-o", obj]
     if _needs(obj, deps, cmd):
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
@@ -65,23 +67,33 @@ def _compile(src: str) -> str:
     return obj
 
 
-def build_library(verbose: bool = False) -> str:
-    os.makedirs(OBJ, exist_ok=True)
-    srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
+def build_library(verbose: bool = False, diag: bool = False, csrc: str = CSRC, out: str = None,
+                  include: str = None) -> str:
+    """The shipped library (default), or with ``diag`` the timing-diagnostic build
+    ``librescore_diag.so`` (-DRS_DIAG=1: the wrong-results GEMM variants and the stamp build the
+    probe tools under tools/ use; never loaded by the scoring path, tests or bench).  ``csrc`` /
+    ``out`` / ``include``: build another source tree (an A/B of two revisions, tools/build_rev.py)."""
+    include = include or os.path.join(REPO, "include")
+    lib = out or (os.path.join(PKG, "librescore_diag.so") if diag else LIB)
+    objdir = os.path.join(os.path.dirname(lib), "build_" + os.path.basename(lib).split(".")[0]) \
+        if (out or diag) else OBJ
+    os.makedirs(objdir, exist_ok=True)
+    defines = ("RS_DIAG=1",) if diag else ()
+    srcs = sorted(glob.glob(os.path.join(csrc, "*.hip")) + glob.glob(os.path.join(csrc, "*.cpp")))
     with cf.ThreadPoolExecutor(max_workers=min(8, len(srcs))) as ex:
-        objs = list(ex.map(_compile, srcs))
+        objs = list(ex.map(lambda f: _compile(f, csrc, objdir, include, defines), srcs))
     # rocBLAS: the trainer's RS_TRAIN_ROCBLAS=1 baseline GEMMs (its soname matches the copy torch loads first)
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB] + objs + \
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + objs + \
         ["-L/opt/rocm/lib", "-lrocblas", "-lpthread"]
-    if _needs(LIB, objs, cmd):
+    if _needs(lib, objs, cmd):
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"link failed:\n{r.stderr[-4000:]}")
-        _stamp(LIB, objs, cmd)
+        _stamp(lib, objs, cmd)
     if verbose:
-        print("built", LIB, file=sys.stderr)
-    return LIB
+        print("built", lib, file=sys.stderr)
+    return lib
 
 
 if __name__ == "__main__":
-    build_library(verbose=True)
+    build_library(verbose=True, diag="--diag" in sys.argv)

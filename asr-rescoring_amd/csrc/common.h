@@ -70,38 +70,52 @@ inline size_t lnres_granules(int m_pad) { return (size_t)m_pad * 4 * 2 + (size_t
 // fp16 operand image of an fp32 activation row with logical width K:
 //   kx == 1: [hi]                          (RS_PREC_FP16)
 //   kx == 3: [hi | hi/64 | (x - hi)*64]    (RS_PREC_FP16X3, K-concatenated GEMM form)
-//   kx == 2: [hi | (x - hi)*64]            (RS_PREC_FP16X3, split-operand GEMM form: the
-//            x3s kernel forms 64 W_hi in registers; weights use the first two parts of their
-//            three-part image, [W_hi | W_lo*64])
+//   kx == 2: hi and lo = (x - hi)*64 INTERLEAVED per 32-column K-step (RS_PREC_FP16X3,
+//            split-operand GEMM form): [hi 0..31 | lo 0..31 | hi 32..63 | lo 32..63 | ...], so
+//            one K-step of a row is one 128-B line and the x3s kernel's LDS-DMA requests whole
+//            lines (round 6; the planar [hi | lo] form requested two 64-B halves per row and
+//            K-step, and that kernel's K loop is request-rate bound: profiles/r5kline_*).
+//            Column c's hi part sits at il_hi(c), its lo part 32 halves later.  The x3s kernel
+//            forms 64 W_hi in registers; its weights are the same interleaved [W_hi | W_lo*64].
 // paired with the weight image [W_hi | W_lo*64 | W_hi/64] the K-concatenated MFMA product is
 // A_hi.W_hi + A_hi.W_lo + A_lo.W_hi (the power-of-two factors cancel exactly): fp32-level
 // accuracy from fp16 MFMA in one accumulator.  The factors keep the lo parts out of the fp16
 // subnormal range, which the f16 MFMA flushes: lo = x - hi is subnormal for |x| < 0.25, and
 // weights of |W| ~ 0.05 have W_lo ~ 1e-5 (unscaled, those products were lost).
 constexpr float X3_UP = 64.f, X3_DOWN = 1.f / 64.f;
+__host__ __device__ __forceinline__ int il_hi(int c) { return ((c & ~31) << 1) | (c & 31); }
 __device__ __forceinline__ f16 x3_mid(f16 hi) { return (f16)((float)hi * X3_DOWN); }
 __device__ __forceinline__ f16 x3_lo(float v, f16 hi) { return (f16)((v - (float)hi) * X3_UP); }
 __device__ __forceinline__ void put_split(f16* row, int c, int K, int kx, float v) {
     const f16 hi = (f16)v;
+    if (kx == 2) {
+        row[il_hi(c)] = hi;
+        row[il_hi(c) + 32] = x3_lo(v, hi);
+        return;
+    }
     row[c] = hi;
     if (kx == 3) {
         row[K + c] = x3_mid(hi);
         row[2 * K + c] = x3_lo(v, hi);
-    } else if (kx == 2) {
-        row[K + c] = x3_lo(v, hi);
     }
 }
+// c % 4 == 0 (the four columns lie in one 32-column K-step)
 __device__ __forceinline__ void put_split4(f16* row, int c, int K, int kx, float4 v) {
     const half4 hi = {(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
-    *(half4*)(row + c) = hi;
+    const int ch = kx == 2 ? il_hi(c) : c;
+    *(half4*)(row + ch) = hi;
     if (kx >= 2) {
         const half4 lo = {x3_lo(v.x, hi[0]), x3_lo(v.y, hi[1]), x3_lo(v.z, hi[2]), x3_lo(v.w, hi[3])};
-        *(half4*)(row + (kx - 1) * K + c) = lo;
+        *(half4*)(row + (kx == 2 ? ch + 32 : 2 * K + c)) = lo;
     }
     if (kx == 3) {
         const half4 mid = {x3_mid(hi[0]), x3_mid(hi[1]), x3_mid(hi[2]), x3_mid(hi[3])};
         *(half4*)(row + K + c) = mid;
     }
+}
+// value of column c of a kx == 2 image row: hi + lo/64
+__device__ __forceinline__ float2 il_parts(const f16* row, int c) {
+    return make_float2((float)row[il_hi(c)], (float)row[il_hi(c) + 32]);
 }
 
 // Per-sequence metadata of a scoring call (structure of arrays, device).  A "sequence"
@@ -135,9 +149,10 @@ __device__ __forceinline__ float wave_max(float v) {
 // launches of the same epilogue
 hipError_t launch_gemm(int epi, const f16* A, const f16* W, int M_pad, int N_pad, int K,
                        const EpiArgs& ep, hipStream_t st, int tag = 0);
-// split-operand fp16x3 GEMM (gemm_x3s_kernel): A two-part image [M_pad, 2K], W rows of ldw
-// halfs starting [W_hi | W_lo*64] (the three-part weight image, ldw = 3K); epi EPI_BIAS_F32 or
-// EPI_GELU_F16 (two-part image out, ep.nlog = N apart).  N_pad % 256 == 0, K % 32 == 0, K >= 64.
+// split-operand fp16x3 GEMM (gemm_x3s_kernel): A the interleaved two-part image [M_pad, 2K]
+// (kx == 2 above), W rows of ldw >= 2K halfs starting with the interleaved [W_hi | W_lo*64] image
+// (ldw = 2K: the packed split-operand weights); epi EPI_BIAS_F32, EPI_GELU_F16 (interleaved
+// two-part image out) or EPI_LNRES_IMG.  N_pad % 256 == 0, K % 32 == 0, K >= 64.
 hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_pad, int N_pad, int K,
                            const EpiArgs& ep, hipStream_t st);
 int gemm_row_align();   // M padding granularity required by launch_gemm

@@ -13,8 +13,8 @@
 //  cls_linear      RescoreBert Linear(H, 1) on the CLS state (RescoreBert/model.py:19-20)
 //  segsum_f64      per-hypothesis PLL, float64, in row order (MLM_PLL/main.py:106-107)
 //
-// Every producer of a GEMM operand writes the fp16 operand image (put_split: [hi] or
-// [hi | hi/64 | lo*64]).  The residual stream stays PRE-LayerNorm in fp32 (x32) with per-row
+// Every producer of a GEMM operand writes the fp16 operand image (put_split: [hi],
+// [hi | hi/64 | lo*64], or the split-operand form's per-K-step interleaved [hi 32 | lo 32]).  The residual stream stays PRE-LayerNorm in fp32 (x32) with per-row
 // (mean, rstd): its consumers (the next residual GEMM's accumulator init, attention_query)
 // rebuild LN(x) with ln_apply, so no LN kernel writes an fp32 copy of its output.
 #include <type_traits>
@@ -231,7 +231,7 @@ ln_res_img_kernel(f16* __restrict__ h16, const float* __restrict__ o32, int rows
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         const int c = v * 256 + lane * 4;
-        const half4 hi = *(const half4*)(hr + c), lo = *(const half4*)(hr + H + c);
+        const half4 hi = *(const half4*)(hr + il_hi(c)), lo = *(const half4*)(hr + il_hi(c) + 32);
         const float4 o = *(const float4*)(o32 + (size_t)row * H + c);
         x[v] = make_float4(o.x + ((float)hi[0] + (float)lo[0] * X3_DOWN), o.y + ((float)hi[1] + (float)lo[1] * X3_DOWN),
                            o.z + ((float)hi[2] + (float)lo[2] * X3_DOWN), o.w + ((float)hi[3] + (float)lo[3] * X3_DOWN));
@@ -866,8 +866,8 @@ attn_query_kernel(const QT* __restrict__ qkv, const QT* __restrict__ qd, const f
     {   // residual of the scored row: LN of its pre-LN sum, or the normalised state's image
         const int c = h * 64 + lane;
         const size_t r = (size_t)(rs + qi);
-        resq[(size_t)s_loc * H + c] = himg ? (float)himg[r * 2 * H + c] + (float)himg[r * 2 * H + H + c] * X3_DOWN
-                                           : ln_apply(x32[r * H + c], stats[r], lg[c], lb[c]);
+        const float2 hl = himg ? il_parts(himg + r * 2 * H, c) : make_float2(0.f, 0.f);
+        resq[(size_t)s_loc * H + c] = himg ? hl.x + hl.y * X3_DOWN : ln_apply(x32[r * H + c], stats[r], lg[c], lb[c]);
     }
 }
 
@@ -988,8 +988,8 @@ embed_out_kernel(const float* __restrict__ x32, const float2* __restrict__ stats
 #pragma unroll
         for (int v = 0; v < NV; ++v) {
             const int c = v * 256 + lane * 4;
-            if (himg) {                       // the normalised state's two-part image
-                const half4 hi = *(const half4*)(himg + r * 2 * H + c), lo = *(const half4*)(himg + r * 2 * H + H + c);
+            if (himg) {                       // the normalised state's (interleaved) two-part image
+                const half4 hi = *(const half4*)(himg + r * 2 * H + il_hi(c)), lo = *(const half4*)(himg + r * 2 * H + il_hi(c) + 32);
                 y[v] = make_float4((float)hi[0] + (float)lo[0] * X3_DOWN, (float)hi[1] + (float)lo[1] * X3_DOWN,
                                    (float)hi[2] + (float)lo[2] * X3_DOWN, (float)hi[3] + (float)lo[3] * X3_DOWN);
             } else {
@@ -1007,8 +1007,11 @@ embed_out_kernel(const float* __restrict__ x32, const float2* __restrict__ stats
         for (int v = 0; v < NV; ++v) {
             const int c = v * 256 + lane * 4;
             const float4 e = make_float4(y[v].x / nrm, y[v].y / nrm, y[v].z / nrm, y[v].w / nrm);
-            if constexpr (TWO) put_split4(o, c, H, 2, e);
-            else *(half4*)(o + c) = half4{(f16)e.x, (f16)e.y, (f16)e.z, (f16)e.w};
+            if constexpr (TWO) {              // the caller's planar [hi | lo*64] layout (rs_token_embed)
+                const half4 hi = {(f16)e.x, (f16)e.y, (f16)e.z, (f16)e.w};
+                *(half4*)(o + c) = hi;
+                *(half4*)(o + H + c) = half4{x3_lo(e.x, hi[0]), x3_lo(e.y, hi[1]), x3_lo(e.z, hi[2]), x3_lo(e.w, hi[3])};
+            } else *(half4*)(o + c) = half4{(f16)e.x, (f16)e.y, (f16)e.z, (f16)e.w};
         }
     }
 }

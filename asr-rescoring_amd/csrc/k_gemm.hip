@@ -21,6 +21,11 @@
 //  * Bijective XCD-aware block remap: consecutive tiles (same A row panel) share an XCD L2.
 #include "common.h"
 #include "gemm_dev.h"
+
+// RS_DIAG=1: the timing-diagnostic build (librescore_diag.so, build.py diag=True; tools/ only)
+#ifndef RS_DIAG
+#define RS_DIAG 0
+#endif
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -149,7 +154,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
 #pragma unroll
             for (int g = 0; g < NQ; ++g) {
                 const int col = acol + MS * j + qcol<MS>(g, lane);
-                const float4 b4 = (VAR & 2) ? make_float4(0.f, 0.f, 0.f, 0.f) : *(const float4*)(ep.bias + col);
+                const float4 b4 = *(const float4*)(ep.bias + col);
                 float4 lg4, lb4, lg04, lb04;
                 if constexpr (EPI == EPI_RESLN_F32) {
                     lg4 = *(const float4*)(ep.res_g + col);
@@ -162,7 +167,7 @@ gemm_f16_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
 #pragma unroll
                 for (int i = 0; i < TM; ++i) {
                     float4 v = b4;
-                    if constexpr ((EPI == EPI_RES_F32 || EPI == EPI_RESLN_F32) && !(VAR & 2)) {
+                    if constexpr (EPI == EPI_RES_F32 || EPI == EPI_RESLN_F32) {
                         float4 r4 = *(const float4*)(ep.res + (size_t)(arow + MS * i) * ep.ldc + col);
                         if constexpr (EPI == EPI_RESLN_F32) {
                             if (defer) {   // post-attention stream: LN0(res) + o16 (ln_res_rows' x)
@@ -940,11 +945,15 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     constexpr int NSTORE = 32;                   // epilogue stores per wave per tile
     static_assert(EPI == EPI_BIAS_F32 || EPI == EPI_GELU_F16 || EPI == EPI_LNRES_IMG, "x3s epilogues");
     constexpr bool LNR = EPI == EPI_LNRES_IMG;
-    static_assert(!LNR || (VAR & 2) == 0, "the LayerNorm epilogue has no no-store diagnostic");
-    // VAR 268435456: stamp build (rs_debug_stamps; diagnostic only, never a production launch):
-    // s_memtime at the tile's phase boundaries, per-phase cycle sums in scalar registers, stored by
-    // thread 0 into ep.dbg[blockIdx.x * 16 + phase] (a buffer of its own: no output depends on it)
-    constexpr bool STAMP = (VAR & 268435456) != 0;
+    // Timing diagnostics (wrong results; compiled only into the RS_DIAG build, librescore_diag.so,
+    // never into the shipped library): DV 1 no K-loop staging, 2 no epilogue stores, 8 the DMA
+    // never waited for, 33554432 every tile stores onto row panel 0 (no HBM write burst),
+    // 268435456 the stamp build (rs_debug_stamps): s_memtime at the tile's phase boundaries,
+    // per-phase cycle sums in scalar registers, stored by thread 0 into
+    // ep.dbg[blockIdx.x * 16 + phase] (a buffer of its own: no output depends on it)
+    constexpr int DV = RS_DIAG ? VAR & (1 | 2 | 8 | 33554432 | 268435456) : 0;
+    static_assert(!LNR || (DV & 2) == 0, "the LayerNorm epilogue has no no-store diagnostic");
+    constexpr bool STAMP = (DV & 268435456) != 0;
     unsigned long long st_sum[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0}, st_prev = 0;
     auto stamp = [&](int ph) __attribute__((always_inline)) {
         if constexpr (STAMP) {
@@ -1008,26 +1017,22 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         n0 = tn * BM;
     };
     // LDS-DMA: buffer_load_dwordx4 ... lds (32-bit lane offsets into a per-tile panel buffer
-    // descriptor, k0 in the scalar offset), 1 KiB pieces of 16 rows x 64 B; wave w stages pieces
-    // p = 0..7 of region p >> 1, rows (p & 1) * 128 + w * 16 + lane / 4 (16-B chunk lane & 3,
-    // g16-swizzled on the source address)
-    const int prow = wave * 16 + (lane >> 2);
-    const int pswz = ((lane & 3) ^ g16(prow >> 2)) * 8;
+    // descriptor, k0 in the scalar offset).  Both operands are interleaved two-part images
+    // (common.h, kx == 2): one K-step of a row is one 128-B line [hi 32 | lo 32], so a 1 KiB piece
+    // is 8 rows x 128 B — whole-line requests (round 6: the planar images took 16 rows x 64 B
+    // per piece, two half-line requests per row and K-step; the K loop is request-rate bound,
+    // profiles/r5kline_fullline_dma.txt).  In LDS each operand is 256 rows at a 128-B pitch, chunk
+    // c (0-3 hi, 4-7 lo) of row n at slot c ^ ((n >> 1) & 7).  Wave w stages pieces p = 0..7:
+    // operand p >> 2 (A, W), rows n = 128 (p & 1) + 16 w + 8 ((p >> 1) & 1) + (lane >> 3), lane
+    // slot lane & 7 (its logical chunk swizzled on the source address).
     const size_t ld2 = (size_t)2 * K;
     __amdgpu_buffer_rsrc_t rsA, rsW;
-    int voffA[4], voffW[4];                       // lane byte offsets: (p & 1) row half x (r & 1) hi / lo
+    int voffA[4], voffW[4];                       // lane byte offsets: (p & 1) row half x 8-row half
     // VAR 16777216: output columns permuted inside each 32-column group so that a lane's two
     // 16-column MFMA blocks 2m, 2m + 1 hold 8 CONSECUTIVE output columns (32 m + 8 q4 .. + 7)
     // instead of two runs of 4: W image row 32 m + 16 jj + 4 q + e is W row 32 m + 8 q + 4 jj + e.
     // The epilogue's per-lane loads (bias, residual image, LayerNorm weights) become 16-B loads.
     constexpr bool PERM = (VAR & 16777216) != 0;
-    // VAR 64 (NOT instantiated — no launch path): the W image interleaved [hi 32 | lo 32] per
-    // 32-column K-step (one 128-B line per row and K-step: full-line DMA requests,
-    // profiles/r5kline2_per_operand.txt); W rows in LDS at a 128-B pitch, chunk c of row n at
-    // c ^ ((n >> 1) & 7).  Bitwise equal to production and 2.0-3.5 % faster at M = 262144, but one
-    // 1024-row call faulted (illegal address, cause not found): profiles/r5wil_w_interleaved.txt
-    constexpr bool WIL = (VAR & 64) != 0;
-    static_assert(!(WIL && (VAR & 4096)), "the interleaved W layout and the full-line diagnostic");
     auto wperm = [](int L) {
         return PERM ? (L & ~31) | (((L >> 2) & 3) << 3) | (((L >> 4) & 1) << 2) | (L & 3) : L;
     };
@@ -1035,39 +1040,25 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     for (int h = 0; h < 2; ++h)
 #pragma unroll
         for (int l = 0; l < 2; ++l) {
-            voffA[2 * h + l] = ((prow + 128 * h) * (int)ld2 + l * K + pswz) * 2;
-            voffW[2 * h + l] = (wperm(prow + 128 * h) * ldw + l * K + pswz) * 2;
-            if constexpr (WIL) {
-                // W image interleaved per K-step (VAR 64): piece (h, l) = LDS rows n = 128 h + 16 wave
-                // + 8 l + (lane >> 3), one 128-B line each ([hi 32 | lo 32] of the K-step); lane
-                // slot s = lane & 7 holds logical chunk s ^ ((n >> 1) & 7) (0-3 hi, 4-7 lo)
-                const int n = 128 * h + wave * 16 + 8 * l + (lane >> 3);
-                voffW[2 * h + l] = (wperm(n) * ldw + (((lane & 7) ^ ((n >> 1) & 7)) * 8)) * 2;
-            }
-            if constexpr ((VAR & 4096) != 0) {
-                // VAR 4096 (timing diagnostic, wrong results): each DMA piece covers 8 rows x 128 B
-                // (K-step t: bytes [128 t, 128 t + 128) of the row) instead of 16 rows x 64 B — the
-                // same rows and bytes per K loop, full-line requests (+ 16: W side only, + 32: A
-                // side only)
-                const int drow = wave * 16 + (lane >> 3) + 8 * l + 128 * h;
-                if constexpr ((VAR & 16) == 0) voffA[2 * h + l] = (drow * (int)ld2 + (lane & 7) * 8) * 2;
-                if constexpr ((VAR & 32) == 0) voffW[2 * h + l] = (wperm(drow) * ldw + (lane & 7) * 8) * 2;
-            }
+            const int n = 128 * h + wave * 16 + 8 * l + (lane >> 3);
+            const int sl = ((lane & 7) ^ ((n >> 1) & 7)) * 8;
+            voffA[2 * h + l] = (n * (int)ld2 + sl) * 2;
+            voffW[2 * h + l] = (wperm(n) * ldw + sl) * 2;
         }
     auto set_rsrc = [&](int m0, int n0) {
         rsA = __builtin_amdgcn_make_buffer_rsrc((void*)(A + (size_t)m0 * ld2), (short)0, (int)(256 * ld2 * 2), 0x00020000);
         rsW = __builtin_amdgcn_make_buffer_rsrc((void*)(W + (size_t)n0 * ldw), (short)0, 256 * ldw * 2, 0x00020000);
     };
     auto piece = [&](int buf, int k0, int p) {
-        if constexpr ((VAR & 1) != 0) return;     // diagnostic: no K-loop staging (stale tiles)
+        if constexpr ((DV & 1) != 0) return;      // diagnostic: no K-loop staging (stale tiles)
         const int r = p >> 1;
-        const int dofs = (WIL && r >= 2) ? 2 * REG + ((p & 1) * 128 + wave * 16 + 8 * (r & 1)) * 128
-                                         : r * REG + ((p & 1) * 8 + wave) * 1024;
+        const int dofs = (r >> 1) * 2 * REG + ((p & 1) * 128 + wave * 16 + 8 * (r & 1)) * 128;
         auto* dst = (__attribute__((address_space(3))) void*)(smem + buf * STAGE + dofs);
         const int vo = (r < 2 ? voffA : voffW)[2 * (p & 1) + (r & 1)];
-        constexpr bool FLA = (VAR & 4096) && !(VAR & 16), FLW = (VAR & 4096) && !(VAR & 32);
-        const int so = (r < 2 ? FLA : (FLW || WIL)) ? k0 * 4 : k0 * 2;
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 16, vo, so, 0, 0);
+        // k0 halves of logical K = 2 k0 halves of the image = 4 k0 bytes.  The scalar offset is
+        // outside the descriptor's range check (only the lane offset is checked): the host
+        // guarantees K-step k0 lies inside every row (launch_gemm_x3s: ldw >= 2K)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(r < 2 ? rsA : rsW, dst, 16, vo, k0 * 4, 0, 0);
     };
     auto stage = [&](int buf, int k0) {
 #pragma unroll
@@ -1076,8 +1067,8 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     const half8 up = (half8)(f16)X3_UP;
 
     // v_mfma_f32_16x16x32_f16, one MFMA per BK = 32 step.  Lane l supplies row (l & 15) of a
-    // 16-row block at 16-B k-chunk (l >> 4): a wave reads 16 whole 64-B rows per ds_read_b128,
-    // which the g16 chunk swizzle keeps conflict-free.  The chip holds a higher clock under the
+    // 16-row block at 16-B k-chunk (l >> 4): a wave reads the hi (or lo) halves of 16 rows per
+    // ds_read_b128.  The chip holds a higher clock under the
     // 16x16 shape at equal MFMA cycles (MI355X_MICROARCH 'DVFS give-back' 7; +6-8 % over
     // 32x32x16 here).  acc16[i][j]: rows 16 i + (l & 15) of the wave tile, columns
     // 16 j + 4 (l >> 4) .. +3.  Per K-step: W_hi, W_lo of the wave's 64 columns once (+ 64 W_hi
@@ -1085,13 +1076,16 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     // The three products at one scale, 64x the value: (64 W_hi) A_hi + W_hi (64 A_lo) + (64 W_lo) A_hi
     // (the images hold the lo parts x64), so the accumulators carry 64 C and the epilogue scales
     // by 1/64 with its bias add.  One operand scaled in registers per K-step (16 v_pk_mul_f16 per
-    // wave) instead of W_hi/64 and A_hi/64 (48; dbg 4, no scaling at all: the round-5 probe put
-    // those 48 at 2.4-2.9 % of the GEMM, profiles/r5t_x3s_scale.txt) — and no operand is divided
-    // down toward the fp16 subnormals the MFMA flushes.
+    // wave) instead of W_hi/64 and A_hi/64 (48; no scaling at all: the round-5 probe put those 48
+    // at 2.4-2.9 % of the GEMM, profiles/r5t_x3s_scale.txt) — and no operand is divided down
+    // toward the fp16 subnormals the MFMA flushes.  64 W_hi must stay finite: |W_hi| <= 1023.5,
+    // which rs_model_finalize checks before it packs a model's split-operand weights.
     const int r16 = lane & 15, q4 = lane >> 4;
-    const int offA16 = (wm * WTM + r16) * RB + ((q4 ^ g16(r16 >> 2)) << 4);
-    const int offW16 = WIL ? 2 * REG + (wn * WTN + r16) * 128 + ((q4 ^ ((r16 >> 1) & 7)) << 4)
-                           : 2 * REG + (wn * WTN + r16) * RB + ((q4 ^ g16(r16 >> 2)) << 4);
+    // fragment rows at a 128-B pitch: lane (r16, q4) reads hi chunk q4 of its row at slot
+    // q4 ^ ((r16 >> 1) & 7); its lo chunk q4 + 4 is that slot ^ 4 (offset ^ 64).  The 16 lanes of a
+    // ds_read_b128 group cover rows r16 = 0..15 at bank offsets 32 (r16 & 1) + 4 slot: conflict-free
+    const int offA16 = (wm * WTM + r16) * 128 + ((q4 ^ ((r16 >> 1) & 7)) << 4);
+    const int offW16 = 2 * REG + (wn * WTN + r16) * 128 + ((q4 ^ ((r16 >> 1) & 7)) << 4);
     f32x4 acc16[8][4];
     // the next step's eight DMA pieces ride this step's first MFMA groups (one per group of four
     // MFMAs of row half 0); the last step of a tile passes k0n = 2^29 and issues none (the same
@@ -1102,23 +1096,18 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         half8 wh[4], wl[4], wu[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-            if constexpr (WIL) {                                  // 16 rows of 128 B; lo = chunk ^ 4
-                wh[j] = *(const half8*)(sb + offW16 + j * 2048);
-                wl[j] = *(const half8*)(sb + (offW16 ^ 64) + j * 2048);
-            } else {
-                wh[j] = *(const half8*)(sb + offW16 + j * 1024);
-                wl[j] = *(const half8*)(sb + offW16 + REG + j * 1024);
-            }
+            wh[j] = *(const half8*)(sb + offW16 + j * 2048);
+            wl[j] = *(const half8*)(sb + (offW16 ^ 64) + j * 2048);
         }
 #pragma unroll
-        for (int j = 0; j < 4; ++j) wu[j] = (VAR & 4) ? wh[j] : wh[j] * up;       // VAR 4: timing diagnostic
+        for (int j = 0; j < 4; ++j) wu[j] = wh[j] * up;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             half8 ah[4], al[4];
 #pragma unroll
             for (int ii = 0; ii < 4; ++ii) {
-                ah[ii] = *(const half8*)(sb + offA16 + (4 * h + ii) * 1024);
-                al[ii] = *(const half8*)(sb + offA16 + REG + (4 * h + ii) * 1024);
+                ah[ii] = *(const half8*)(sb + offA16 + (4 * h + ii) * 2048);
+                al[ii] = *(const half8*)(sb + (offA16 ^ 64) + (4 * h + ii) * 2048);
             }
 #pragma unroll
             for (int pr = 0; pr < 3; ++pr) {
@@ -1162,7 +1151,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             for (int j = 0; j < 4; ++j) acc16[i][j] = (f32x4)(0.f);
         // step kt landed for this wave (at a tile's first step the previous tile's stores are
         // younger and stay in flight); the barrier: landed for every wave, and every wave is done
-        // reading step kt-1's buffer, which now receives step kt+1.  (VAR 8, diagnostic: the DMA is
+        // reading step kt-1's buffer, which now receives step kt+1.  (DV 8, diagnostic: the DMA is
         // never waited for — isolates its latency from its presence.)
         int kt0 = 0;
         if constexpr (LNR) {
@@ -1170,7 +1159,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             // compiler, the peeled step tested a hoisted loop-invariant flag that this build spilled,
             // and the reload's vmcnt(0) drained the previous tile's 32 epilogue stores at every tile
             // start (the fp32 / GELU builds keep the loop: peeled by hand they spill)
-            if constexpr ((VAR & 8) == 0) {
+            if constexpr ((DV & 8) == 0) {
                 if (!first) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
                 else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
@@ -1182,7 +1171,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         }
         for (int kt = kt0; kt < nk; ++kt) {
             const int cur = (par + kt) & 1;
-            if constexpr ((VAR & 8) != 0) {
+            if constexpr ((DV & 8) != 0) {
             } else if (kt == 0 && !first) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
             else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             asm volatile("s_barrier" ::: "memory");
@@ -1258,38 +1247,20 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 // accumulators, and the spills that forced reloaded values whose waits drained the
                 // next tile's stage 0 inside the statistics publish)
                 constexpr int RB2 = 2;
-                // VAR 8388608 (timing diagnostic, wrong results): the residual add skipped
 #pragma unroll
                 for (int hh = 0; hh < 8 / RB2; ++hh) {
-                    if constexpr ((VAR & 8388608) != 0) break;
                     half4 rh0[RB2][4], rl0[RB2][4];
 #pragma unroll
                     for (int ii = 0; ii < RB2; ++ii) {
-                        if constexpr ((VAR & 2097152) != 0) {
-                            // VAR 2097152 (timing diagnostic, wrong results): the same rows, bytes and
-                            // lines, but each load covers 8 rows x 128 B instead of 16 rows x 64 B
-#pragma unroll
-                            for (int m = 0; m < 2; ++m) {
-                                const f16* p = img + (size_t)(cm0 + wm * WTM + 16 * (RB2 * hh + ii) + (r16 >> 1) + 8 * m) * ldc +
-                                               cn0 + wn * WTN + 8 * (4 * (r16 & 1) + q4);
-                                const half8 vh = *(const half8*)p, vl = *(const half8*)(p + H);
-                                rh0[ii][2 * m] = (half4){vh[0], vh[1], vh[2], vh[3]};
-                                rh0[ii][2 * m + 1] = (half4){vh[4], vh[5], vh[6], vh[7]};
-                                rl0[ii][2 * m] = (half4){vl[0], vl[1], vl[2], vl[3]};
-                                rl0[ii][2 * m + 1] = (half4){vl[4], vl[5], vl[6], vl[7]};
-                            }
-                            continue;
-                        }
-                        // VAR 536870912 (timing diagnostic, wrong results): the residual is read
-                        // from row panel 0 (L2-resident lines) — the read without its HBM traffic
-                        const int rm0 = (VAR & 536870912) ? 0 : cm0;
-                        const f16* prow_img = img + (size_t)(rm0 + wm * WTM + 16 * (RB2 * hh + ii) + r16) * ldc;
+                        // the interleaved image row: column c's hi at il_hi(c), its lo 32 halves on
+                        const f16* prow_img = img + (size_t)(cm0 + wm * WTM + 16 * (RB2 * hh + ii) + r16) * ldc;
                         if constexpr (PERM) {
-                            // blocks 2m, 2m + 1: 8 consecutive columns, one 16-B load per image
+                            // blocks 2m, 2m + 1: 8 consecutive columns (32-column group m of the
+                            // wave's 64), one 16-B load per part
 #pragma unroll
                             for (int m = 0; m < 2; ++m) {
-                                const f16* p = prow_img + cn0 + wn * WTN + 32 * m + 8 * q4;
-                                const half8 vh = *(const half8*)p, vl = *(const half8*)(p + H);
+                                const f16* p = prow_img + 2 * (cn0 + wn * WTN) + 64 * m + 8 * q4;
+                                const half8 vh = *(const half8*)p, vl = *(const half8*)(p + 32);
                                 rh0[ii][2 * m] = (half4){vh[0], vh[1], vh[2], vh[3]};
                                 rh0[ii][2 * m + 1] = (half4){vh[4], vh[5], vh[6], vh[7]};
                                 rl0[ii][2 * m] = (half4){vl[0], vl[1], vl[2], vl[3]};
@@ -1298,9 +1269,9 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         } else {
 #pragma unroll
                             for (int j = 0; j < 4; ++j) {
-                                const f16* p = prow_img + c0 + 16 * j;
+                                const f16* p = prow_img + il_hi(c0 + 16 * j);
                                 rh0[ii][j] = *(const half4*)p;
-                                rl0[ii][j] = *(const half4*)(p + H);
+                                rl0[ii][j] = *(const half4*)(p + 32);
                             }
                         }
                     }
@@ -1464,7 +1435,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             };
             // the GELU image: each row-block pair's bias + GELU right before its slab pass, so that
             // VALU work overlaps the previous pair's LDS and global stores
-            constexpr bool LATE = EPI == EPI_GELU_F16 && (VAR & 2) == 0;
+            constexpr bool LATE = EPI == EPI_GELU_F16 && (DV & 2) == 0;
             if constexpr (LNR) {
                 if (lnres_epilogue()) {
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the next tile's stage 0 landed
@@ -1474,7 +1445,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                     if (more) stage(last ^ 1, 0);
                 }
             } else if constexpr (!LATE) finish(0, 8);
-            if constexpr ((VAR & 2) != 0) {      // diagnostic: no epilogue stores (acc kept alive)
+            if constexpr ((DV & 2) != 0) {       // diagnostic: no epilogue stores (acc kept alive)
 #pragma unroll
                 for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -1490,9 +1461,8 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             int lns = lane;
             if constexpr (LNR) asm volatile("" : "+v"(lns));
             const int rr0 = lns >> 3, c16 = lns & 7;
-            // VAR 33554432 (timing diagnostic, wrong results): every tile stores onto the rows of
-            // row panel 0 (L2-resident lines), separating the store path from the HBM write burst
-            const int sm0 = (VAR & 33554432) ? 0 : cm0;
+            // DV 33554432 (diagnostic): every tile stores onto the rows of row panel 0
+            const int sm0 = (DV & 33554432) ? 0 : cm0;
             if constexpr (EPI == EPI_BIAS_F32) {
                 // 32 x 32 fp32 slab blocks: row blocks 2 i2 + a, column blocks 2 j2 + b
 #pragma unroll
@@ -1513,30 +1483,32 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         for (int it = 0; it < 4; ++it) st16<64>((uint4*)(ob + (size_t)(it * 8 + rr0) * ep.ldc), v[it]);
                     }
             } else {
-                // two-part images in 32 x 64 slab blocks (row blocks 2 i2 + a, all four column
-                // blocks): image 0 = hi, image 1 = lo*64
-                // row-block pair outermost: its accumulators die after both images are out
+                // the interleaved two-part image in 32 x 64 slab blocks: row blocks 2 i2 + a, one
+                // 32-column group g of the wave's 64 per block, each slab row its 128-B line
+                // [hi 32 | lo*64 32] (column blocks 2 g, 2 g + 1)
+                // row-block pair outermost: its accumulators die after both groups are out
 #pragma unroll
                 for (int i2 = 0; i2 < 4; ++i2) {
                     if constexpr (LATE) finish(2 * i2, 2 * i2 + 2);
 #pragma unroll
-                    for (int img = 0; img < 2; ++img) {
+                    for (int g = 0; g < 2; ++g) {
 #pragma unroll
                         for (int a = 0; a < 2; ++a)
 #pragma unroll
-                            for (int j = 0; j < 4; ++j) {
-                                half4 h;
+                            for (int jj = 0; jj < 2; ++jj) {
+                                half4 hh, hl;
 #pragma unroll
                                 for (int e = 0; e < 4; ++e) {
-                                    const float x = acc16[2 * i2 + a][j][e];
+                                    const float x = acc16[2 * i2 + a][2 * g + jj][e];
                                     const f16 hi = (f16)x;
-                                    h[e] = img == 0 ? hi : x3_lo(x, hi);
+                                    hh[e] = hi;
+                                    hl[e] = x3_lo(x, hi);
                                 }
-                                const int row = 16 * a + r16,
-                                          byte = PERM ? 64 * (j >> 1) + 16 * q4 + 8 * (j & 1) : 32 * j + 8 * q4;
-                                *(half4*)(slb + row * 128 + (((byte >> 4) ^ (row & 7)) << 4) + (byte & 8)) = h;
+                                const int row = 16 * a + r16, byte = PERM ? 16 * q4 + 8 * jj : 32 * jj + 8 * q4;
+                                *(half4*)(slb + row * 128 + (((byte >> 4) ^ (row & 7)) << 4) + (byte & 8)) = hh;
+                                *(half4*)(slb + row * 128 + ((((byte >> 4) + 4) ^ (row & 7)) << 4) + (byte & 8)) = hl;
                             }
-                        f16* ob = (f16*)ep.out + (size_t)(sm0 + wm * WTM + 32 * i2) * ep.ldc + img * ep.nlog + cn0 + wn * WTN + 8 * c16;
+                        f16* ob = (f16*)ep.out + (size_t)(sm0 + wm * WTM + 32 * i2) * ep.ldc + 2 * (cn0 + wn * WTN) + 64 * g + 8 * c16;
                         uint4 v[4];
                         slab_read4(slb, rr0, c16, v);
 #pragma unroll
@@ -1723,18 +1695,22 @@ int gemm_lnres_workgroups(int N_pad) {
 }
 
 // Production split-operand fp16x3 GEMM (gemm_x3s_kernel; tools/x3s_epi_probe.py).
-// Stamp builds (rs_debug_stamps): while g_stamps is set, every split-operand GEMM launch runs the
-// VAR 268435456 build of its kernel and adds its per-workgroup phase cycles into the region of its
-// instance: 0 QKV / fp32 out, 1 BertIntermediate (GELU image), 2 O-projection + LayerNorm,
-// 3 BertOutput + LayerNorm (each [256 workgroups][16 words]).
+// Stamp builds (RS_DIAG only, rs_debug_stamps): while g_stamps is set, every split-operand GEMM
+// launch runs the VAR 268435456 build of its kernel and adds its per-workgroup phase cycles into
+// the region of its instance: 0 QKV / fp32 out, 1 BertIntermediate (GELU image), 2 O-projection +
+// LayerNorm, 3 BertOutput + LayerNorm (each [256 workgroups][16 words]).
+#if RS_DIAG
 static unsigned long long* g_stamps = nullptr;
 constexpr int STAMP_WORDS = 4 * 256 * 16;
+#endif
 
 template <int STV>
 hipError_t launch_gemm_x3s_v(int epi, const f16* A, const f16* W, int ldw, int M_pad, int N_pad, int K,
                              const EpiArgs& ep_in, hipStream_t st) {
     EpiArgs ep = ep_in;
+#if RS_DIAG
     if (STV) ep.dbg = g_stamps + (epi == EPI_BIAS_F32 ? 0 : epi == EPI_GELU_F16 ? 1 : K > 1024 ? 3 : 2) * 256 * 16;
+#endif
     switch (epi) {
         case EPI_BIAS_F32: return launch_x3s<EPI_BIAS_F32, STV>(A, W, M_pad, N_pad, K, ep, st, ldw);
         case EPI_GELU_F16: return launch_x3s<EPI_GELU_F16, STV>(A, W, M_pad, N_pad, K, ep, st, ldw);
@@ -1773,10 +1749,13 @@ hipError_t launch_gemm_x3s(int epi, const f16* A, const f16* W, int ldw, int M_p
     if (M_pad % 256 || N_pad % 256 || K % 32 || K < 64 || ldw < 2 * K || M_pad <= 0) return hipErrorInvalidValue;
     // the buffer descriptors address one 256-row panel: 32-bit byte offsets
     if ((long long)256 * ldw * 2 >= (1ll << 31) || (long long)256 * 2 * K * 2 >= (1ll << 31)) return hipErrorInvalidValue;
+#if RS_DIAG
     if (g_stamps) return launch_gemm_x3s_v<268435456>(epi, A, W, ldw, M_pad, N_pad, K, ep, st);
+#endif
     return launch_gemm_x3s_v<0>(epi, A, W, ldw, M_pad, N_pad, K, ep, st);
 }
 
+#if RS_DIAG
 // Diagnostic entry (not part of the scoring path): on = 1 allocates and zeroes the stamp buffer
 // and switches the split-operand GEMM launches to their stamp builds; on = 0 copies the buffer
 // (STAMP_WORDS u64: [instance][workgroup][phase], phases 0 K loop, 1 bias + next stage, 2 residual,
@@ -1794,6 +1773,7 @@ extern "C" int rs_debug_stamps(int on, unsigned long long* host_out) {
     g_stamps = nullptr;
     return 0;
 }
+#endif
 
 hipError_t launch_gemm(int epi, const f16* A, const f16* W, int M_pad, int N_pad, int K,
                        const EpiArgs& ep, hipStream_t st, int tag) {
@@ -1821,29 +1801,31 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
     const f16* w = (const f16*)W;
     hipError_t e = hipErrorInvalidValue;
     if (M % 256 || N % 256 || K % 64) return -1;
-    if (cfg == 31 || cfg == 32) {  // split-operand fp16x3 (A [M, 2K], W [N, 2K] images): 31 GELU image, 32 fp32
-        // dbg: 0 production; timing diagnostics of gemm_x3s_kernel (wrong results): 1 no K-loop staging, 2 no epilogue stores (20 / 52:
-        // the same, round-3 / round-4 probe numbering), 3 neither, 50 DMA never waited for (the
-        // next tile never waits for this tile's stores), 51 stores onto row panel 0 (no HBM write
-        // burst), 53 both
+    if (cfg == 31 || cfg == 32) {  // split-operand fp16x3 (A [M, 2K], W [N, 2K] interleaved images): 31 GELU image, 32 fp32
+        // dbg 0: the production kernel.  The RS_DIAG build adds the timing diagnostics of
+        // gemm_x3s_kernel (wrong results; tools/x3s_epi_probe.py): 1 no K-loop staging, 2 no
+        // epilogue stores (20 / 52: the same, older probe numbering), 3 neither, 50 DMA never
+        // waited for, 51 stores onto row panel 0 (no HBM write burst), 53 both
         ep.nlog = N;
         const int epi = cfg == 31 ? EPI_GELU_F16 : EPI_BIAS_F32;
         if (cfg == 31) ep.ldc = 2 * N;
+        if (dbg == 0) e = launch_gemm_x3s(epi, a, w, 2 * K, M, N, K, ep, st);
+#if RS_DIAG
 #define RS_X3(VAR_)                                                                        \
     (cfg == 31 ? launch_x3s<EPI_GELU_F16, VAR_>(a, w, M, N, K, ep, st) : launch_x3s<EPI_BIAS_F32, VAR_>(a, w, M, N, K, ep, st))
-        switch (dbg) {
-            case 0: e = launch_gemm_x3s(epi, a, w, 2 * K, M, N, K, ep, st); break;
+        else switch (dbg) {
             case 1: e = RS_X3(1); break;
             case 2: case 20: case 52: e = RS_X3(2); break;
             case 3: e = RS_X3(3); break;
-            case 4: e = RS_X3(4); break;                      // no 64 W_hi scaling in the K loop (wrong results)
-            case 7: e = RS_X3(7); break;
             case 50: e = RS_X3(8); break;
             case 51: e = RS_X3(33554432); break;
             case 53: e = RS_X3(8 | 33554432); break;
             default: return -1;
         }
 #undef RS_X3
+#else
+        else return -1;
+#endif
         return e == hipSuccess ? 0 : -2;
     }
     // fp16 kernels: 9 / 11 persistent bias / GELU with the plain schedule (the bitwise reference

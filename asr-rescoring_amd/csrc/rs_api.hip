@@ -53,7 +53,9 @@ struct DevBuf {
 };
 
 struct Layer {
-    f16 *wqkv, *wo, *w1, *w2;
+    f16 *wqkv, *wo, *w1, *w2;       // operand images of the precision mode (kx parts, planar)
+    f16 *iqkv = nullptr, *io = nullptr, *i1 = nullptr, *i2 = nullptr;   // fp16x3: interleaved two-part
+                                    // images [W_hi | W_lo*64] of the split-operand GEMMs (ldw = 2K)
     float *bqkv, *bo, *b1, *b2, *g1, *be1, *g2, *be2;
 };
 
@@ -81,6 +83,8 @@ struct rs_model {
     int64_t max_rows = 0;
     int s_cap = 0, r_pad = 0, m_pad = 0;
     int kx = 1;                 // fp16 operand image width (1: fp16, 3: fp16x3)
+    bool x3s_w = false;         // the split-operand weight images exist (fp16x3, every projection
+                                // weight |w| < 1023.75 so that 64 W_hi is finite in the x3s K loop)
     DevBuf xst, h16, t32, qkv, ctx, inter;   // xst: (mean, rstd) of the pre-LN rows in t32
     DevBuf xst1;                // statistics of the post-attention stream (deferred residual)
     DevBuf lnx, lncnt, lnerr;   // EPI_LNRES_IMG: per-tile row statistics, gang-ticket words (left
@@ -141,6 +145,37 @@ f16* upload_f16(rs_model* m, const std::vector<float>& src, size_t rows_pad, siz
     m->allocs.push_back(p);
     *err = hipMemcpy(p, tmp.data(), tmp.size() * sizeof(f16), hipMemcpyHostToDevice);
     return (f16*)p;
+}
+
+// Weight W [rows, cols] -> the split-operand GEMM's interleaved two-part image [rows, 2 cols]
+// (common.h, kx == 2): per 32-column K-step [hi 32 | lo*64 32], the same hi / lo*64 values as the
+// planar three-part image's first two parts.
+f16* upload_il(rs_model* m, const std::vector<float>& src, size_t cols, hipError_t* err) {
+    const size_t rows = src.size() / cols;
+    std::vector<f16> tmp(rows * cols * 2, (f16)0.0f);
+    for (size_t r = 0; r < rows; ++r)
+        for (size_t c = 0; c < cols; ++c) {
+            const float v = src[r * cols + c];
+            const f16 hi = (f16)v;
+            f16* row = tmp.data() + r * cols * 2;
+            row[il_hi((int)c)] = hi;
+            row[il_hi((int)c) + 32] = (f16)((v - (float)hi) * 64.f);
+        }
+    void* p = nullptr;
+    *err = hipMalloc(&p, tmp.size() * sizeof(f16));
+    if (*err != hipSuccess) return nullptr;
+    m->allocs.push_back(p);
+    *err = hipMemcpy(p, tmp.data(), tmp.size() * sizeof(f16), hipMemcpyHostToDevice);
+    return (f16*)p;
+}
+
+// The split-operand K loop forms 64 W_hi in fp16 (k_gemm.hip kstep16): finite only for
+// |W_hi| <= 1023.5, i.e. |w| < 1023.75.  A model with a larger projection weight runs its fp16x3
+// layers in the K-concatenated form instead (no 64x factor on W_hi), which holds |w| <= 65504.
+bool x3s_range_ok(const std::vector<float>& v) {
+    for (float x : v)
+        if (!(std::fabs(x) < 1023.75f)) return false;
+    return true;
 }
 
 float* upload_f32(rs_model* m, const std::vector<float>& src, size_t n_pad, hipError_t* err) {
@@ -381,9 +416,9 @@ bool ffn2_f16() {
 // (gemm_x3s_kernel: two-part activation images, three fp16 products formed in registers, fp32
 // outputs + ln_res32 rows for the residual blocks); 0 = the K-concatenated three-part form.
 // Read per call (tests flip it in-process).
-bool x3s_on(const rs_bert_cfg& cf) {
+bool x3s_on(const rs_model* m) {
     const char* e = getenv("RS_X3S");
-    return !(e && !strcmp(e, "0")) && cf.hidden % 256 == 0 && cf.intermediate % 256 == 0;
+    return !(e && !strcmp(e, "0")) && m->x3s_w && m->cfg.hidden % 256 == 0 && m->cfg.intermediate % 256 == 0;
 }
 // RS_X3S_IMGRES (split-operand layers, default 1): the residual stream is held only as the
 // two-part image of the normalised hidden state (ln_res_img: 12 B per element per residual
@@ -409,7 +444,7 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
     const int qkv_epi = q32 ? EPI_BIAS_F32 : EPI_BIAS_F16;
     const int rows = c.rows, ns = c.s1 - c.s0;
     const bool dedup = c.urows > 0;           // layer-0 Q/K/V over unique rows (MLM; fp16, or fp16x3 split)
-    const bool x3s = kx == 3 && x3s_on(cf);   // split-operand GEMMs: full-row images are two-part
+    const bool x3s = kx == 3 && x3s_on(m);    // split-operand GEMMs: full-row images are two-part
     const int kxf = x3s ? 2 : kx;             // width factor of the full-row operand images
     const bool imgres = x3s && x3s_imgres_on();  // residual stream = the two-part image in h16
     const bool lnfuse = imgres && lnfuse_on(cf);  // ... closed in the residual GEMMs' epilogues
@@ -475,7 +510,7 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
             ep.bias = L.bqkv + H;
             ep.out = (char*)qkv + H * esz;
             if (x3s) {
-                if (int r = gx(RS_K_QKV, EPI_BIAS_F32, h16, L.wqkv + (size_t)H * 3 * H, 3 * H, rows, 2 * H, H, ep, 2 * H))
+                if (int r = gx(RS_K_QKV, EPI_BIAS_F32, h16, L.iqkv + (size_t)H * 2 * H, 2 * H, rows, 2 * H, H, ep, 2 * H))
                     return r;
             } else if (int r = gemm(m, st, RS_K_QKV, qkv_epi, h16, L.wqkv + (size_t)H * kx * H, rows, 2 * H, kx * H, ep,
                                     2 * H)) return r;
@@ -487,11 +522,11 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
             EpiArgs eq{};
             eq.bias = L.bqkv; eq.out = m->tq32.p; eq.ldc = H;
             if (x3s) {
-                if (int r = gx(RS_K_QKV, EPI_BIAS_F32, hq16g, L.wqkv, 3 * H, ns, H, H, eq, H)) return r;
+                if (int r = gx(RS_K_QKV, EPI_BIAS_F32, hq16g, L.iqkv, 2 * H, ns, H, H, eq, H)) return r;
             } else if (int r = gemm(m, st, RS_K_QKV, qkv_epi, hq16g, L.wqkv, ns, H, kx * H, eq, H)) return r;
             qdense = m->tq32.p;
         } else if (x3s) {
-            if (int r = gx(RS_K_QKV, EPI_BIAS_F32, uq ? inter : h16, L.wqkv, 3 * H, uq ? c.urows : rows, 3 * H, H, ep,
+            if (int r = gx(RS_K_QKV, EPI_BIAS_F32, uq ? inter : h16, L.iqkv, 2 * H, uq ? c.urows : rows, 3 * H, H, ep,
                            last ? 2 * H : 3 * H)) return r;
         } else if (int r = gemm(m, st, RS_K_QKV, qkv_epi, h16, L.wqkv, uq ? c.urows : rows, 3 * H, kx * H, ep,
                                 last ? 2 * H : 3 * H)) return r;
@@ -516,23 +551,23 @@ int run_chunk(rs_model* m, hipStream_t st, const int* d_tok, const SeqMeta& sm, 
                 return e;
             };
             if (lnfuse) {
-                if (int r = gx(RS_K_OPROJ, EPI_LNRES_IMG, ctx, L.wo, 3 * H, rows, H, H, lnres_ep(L.bo, L.g1, L.be1), H))
+                if (int r = gx(RS_K_OPROJ, EPI_LNRES_IMG, ctx, L.io, 2 * H, rows, H, H, lnres_ep(L.bo, L.g1, L.be1), H))
                     return r;
             } else {
                 ep = EpiArgs{}; ep.bias = L.bo; ep.out = o32; ep.ldc = H;
-                if (int r = gx(RS_K_OPROJ, EPI_BIAS_F32, ctx, L.wo, 3 * H, rows, H, H, ep, H)) return r;
+                if (int r = gx(RS_K_OPROJ, EPI_BIAS_F32, ctx, L.io, 2 * H, rows, H, H, ep, H)) return r;
                 ProfScope ps(m, st, RS_K_OTHER, 0);
                 if (imgres) HIPTRY(launch_ln_res_img(h16, o32, rows, L.g1, L.be1, cf.ln_eps, H, st));
                 else HIPTRY(launch_ln_res32(t32, xst, xst, pg, pb, o32, rows, L.g1, L.be1, cf.ln_eps, H, h16, 2, st));
             }
             ep = EpiArgs{}; ep.bias = L.b1; ep.out = inter; ep.ldc = 2 * F; ep.kx = 2; ep.nlog = F;
-            if (int r = gx(RS_K_FFN1, EPI_GELU_F16, h16, L.w1, 3 * H, rows, F, H, ep, F)) return r;
+            if (int r = gx(RS_K_FFN1, EPI_GELU_F16, h16, L.i1, 2 * H, rows, F, H, ep, F)) return r;
             if (lnfuse) {
-                if (int r = gx(RS_K_FFN2, EPI_LNRES_IMG, inter, L.w2, 3 * F, rows, H, F, lnres_ep(L.b2, L.g2, L.be2), H))
+                if (int r = gx(RS_K_FFN2, EPI_LNRES_IMG, inter, L.i2, 2 * F, rows, H, F, lnres_ep(L.b2, L.g2, L.be2), H))
                     return r;
             } else {
                 ep = EpiArgs{}; ep.bias = L.b2; ep.out = o32; ep.ldc = H;
-                if (int r = gx(RS_K_FFN2, EPI_BIAS_F32, inter, L.w2, 3 * F, rows, H, F, ep, H)) return r;
+                if (int r = gx(RS_K_FFN2, EPI_BIAS_F32, inter, L.i2, 2 * F, rows, H, F, ep, H)) return r;
                 ProfScope ps(m, st, RS_K_OTHER, 0);
                 if (imgres) HIPTRY(launch_ln_res_img(h16, o32, rows, L.g2, L.be2, cf.ln_eps, H, st));
                 else HIPTRY(launch_ln_res32(t32, xst, xst, L.g1, L.be1, o32, rows, L.g2, L.be2, cf.ln_eps, H, h16, 2, st));
@@ -690,7 +725,7 @@ int run_all(rs_model* m, hipStream_t st, const int* d_tok, SeqList& sl, int mode
     int64_t cap = m->max_rows;
     {
         const char* ca = getenv("RS_CHUNK_ALIGN");
-        const bool lnf = m->kx == 3 && x3s_on(m->cfg) && x3s_imgres_on() && lnfuse_on(m->cfg);
+        const bool lnf = m->kx == 3 && x3s_on(m) && x3s_imgres_on() && lnfuse_on(m->cfg);
         const int ntn = m->cfg.hidden / 256;
         if (lnf && !(ca && !strcmp(ca, "0")) && ntn > 0) {
             const int64_t unit = (int64_t)256 * (gemm_lnres_workgroups(m->cfg.hidden) / ntn);
@@ -719,7 +754,7 @@ int run_all(rs_model* m, hipStream_t st, const int* d_tok, SeqList& sl, int mode
     const int dedup_env = dedup_s ? atoi(dedup_s) : 1;
     // fp16x3: the split-operand layer with the image-held residual (its attention kernel reads
     // the unique rows for chunks with T <= 64)
-    const bool x3_dedup = m->kx == 3 && x3s_on(m->cfg) && x3s_imgres_on();
+    const bool x3_dedup = m->kx == 3 && x3s_on(m) && x3s_imgres_on();
     if (dedup_env && mode == MODE_MLM && (m->kx == 1 || x3_dedup) && m->cfg.layers >= 2)
         for (Chunk& c : chunks)
             if (m->kx == 1 || c.max_len <= 64) c.urows = plan_unique_rows(sl, c.s0, c.s1);
@@ -846,6 +881,18 @@ int rs_model_finalize(rs_model* m) {
     UP32(m->eg, eg, H);
     UP32(m->eb, eb, H);
     m->layers.resize(c.layers);
+    // fp16x3: the split-operand GEMMs' interleaved weight images, when every projection weight
+    // keeps 64 W_hi finite (x3s_range_ok); else the K-concatenated form runs every layer
+    bool x3s_w = m->kx == 3;
+    for (int i = 0; i < c.layers && x3s_w; ++i) {
+        const std::string p = "bert.encoder.layer." + std::to_string(i) + ".";
+        for (const char* k : {"attention.self.query.weight", "attention.self.key.weight", "attention.self.value.weight",
+                              "attention.output.dense.weight", "intermediate.dense.weight", "output.dense.weight"}) {
+            auto it = m->host.find(p + k);
+            if (it != m->host.end() && !x3s_range_ok(it->second)) x3s_w = false;
+        }
+    }
+#define UPIL(dst, src, cols) do { dst = upload_il(m, *(src), (cols), &err); if (err != hipSuccess) return fail(RS_EHIP, "upload"); } while (0)
     for (int i = 0; i < c.layers; ++i) {
         const std::string p = "bert.encoder.layer." + std::to_string(i) + ".";
         auto* wq = need(m, p + "attention.self.query.weight", H * H, &miss);
@@ -882,7 +929,15 @@ int rs_model_finalize(rs_model* m) {
         UP32(L.b2, b2, H);
         UP32(L.g2, g2, H);
         UP32(L.be2, be2, H);
+        if (x3s_w) {
+            UPIL(L.iqkv, &wqkv, H);
+            UPIL(L.io, wo, H);
+            UPIL(L.i1, w1, H);
+            UPIL(L.i2, w2, F);
+        }
     }
+#undef UPIL
+    m->x3s_w = x3s_w;
     if (c.heads_mask & RS_HEAD_MLM) {
         const std::string p = "cls.predictions.";
         auto* wt = need(m, p + "transform.dense.weight", H * H, &miss);

@@ -29,8 +29,9 @@ def gemm():
     fn.argtypes = [ctypes.c_int, ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_int] * 3 + [ctypes.c_void_p]
     st = torch.cuda.current_stream().cuda_stream
 
-    def run(cfg, dbg, A, W, b, out):
-        M, K = A.shape
+    def run(cfg, dbg, A, W, b, out, K=None):
+        M = A.shape[0]
+        K = A.shape[1] if K is None else K          # split-operand cfg 31/32: the logical K
         N = W.shape[0]
         assert fn(cfg, dbg, A.data_ptr(), W.data_ptr(), b.data_ptr(), out.data_ptr(), M, N, K, st) == 0
         torch.cuda.synchronize()
@@ -73,30 +74,70 @@ def test_persistent_schedule_bitwise(gemm, name, N, K, gelu):
 
 
 def _split2(x):
+    """The split-operand GEMM's two-part image of fp32 x [R, K] (common.h kx == 2): hi and
+    lo = (x - hi) * 64 interleaved per 32-column K-step, [hi 0..31 | lo 0..31 | hi 32..63 | ...]."""
     hi = x.half()
-    return torch.cat([hi, ((x - hi.float()) * 64.0).half()], dim=1).contiguous()
+    lo = ((x - hi.float()) * 64.0).half()
+    R, K = x.shape
+    return torch.stack([hi.view(R, K // 32, 32), lo.view(R, K // 32, 32)], dim=2).reshape(R, 2 * K).contiguous()
+
+
+def _unsplit2(img):
+    """hi + lo / 64 of an interleaved two-part image [R, 2N] -> fp32 [R, N]."""
+    R, N2 = img.shape
+    v = img.float().view(R, N2 // 64, 2, 32)
+    return (v[:, :, 0] + v[:, :, 1] / 64.0).reshape(R, N2 // 2)
+
+
+def test_split2_layout():
+    x = torch.arange(2 * 64, dtype=torch.float32).view(2, 64) + 0.25
+    img = _split2(x)
+    assert torch.equal(img[0, :32].float(), x[0, :32].half().float())          # hi of columns 0..31
+    assert torch.equal(img[0, 64:96].float(), x[0, 32:].half().float())        # hi of columns 32..63
+    assert torch.allclose(_unsplit2(img), x)
 
 
 @pytest.mark.parametrize("dbg,M", [(0, 1024), (0, 40960)])
 @pytest.mark.parametrize("name,N,K,gelu", SHAPES)
 def test_x3s_vs_torch_fp32(gemm, name, N, K, gelu, dbg, M):
-    """Split-operand fp16x3 GEMM (cfg 31/32 of rs_debug_gemm, dbg 0 = gemm_x3s_kernel): fp32 output and the two-part GELU image vs an fp32 torch matmul, at
+    """Split-operand fp16x3 GEMM (cfg 31/32 of rs_debug_gemm, dbg 0 = gemm_x3s_kernel) on the
+    interleaved two-part images: fp32 output and the GELU image vs an fp32 torch matmul, at
     fp32-level accuracy (3 fp16 products; measured ~2e-6 of max |C|).  M = 40960 gives every
-    persistent workgroup several tiles (tile transitions, the last tile of each workgroup)."""
+    persistent workgroup several tiles (tile transitions, the last tile of each workgroup);
+    M = 1024 one tile per workgroup (the first tile is the last)."""
     g = torch.Generator(device="cuda").manual_seed(11)
     A = torch.randn(M, K, device="cuda", generator=g)
     W = torch.randn(N, K, device="cuda", generator=g) * 0.05
     b = torch.randn(N, device="cuda", generator=g) * 0.1
     A2, W2 = _split2(A), _split2(W)
     ref = A @ W.t() + b
-    lib = _lib.load()          # direct call: the logical K (the fixture passes A's width)
-    st = torch.cuda.current_stream().cuda_stream
     for cfg, o in ((32, torch.empty(M, N, device="cuda")), (31, torch.empty(M, 2 * N, device="cuda", dtype=torch.float16))):
-        assert lib.rs_debug_gemm(cfg, dbg, A2.data_ptr(), W2.data_ptr(), b.data_ptr(), o.data_ptr(), M, N, K, st) == 0
-        torch.cuda.synchronize()
+        gemm(cfg, dbg, A2, W2, b, o, K=K)
         if cfg == 32:
             err = (o - ref).abs().max() / ref.abs().max()
         else:
             gl = torch.nn.functional.gelu(ref)
-            err = (o[:, :N].float() + o[:, N:].float() / 64.0 - gl).abs().max() / gl.abs().max()
+            err = (_unsplit2(o) - gl).abs().max() / gl.abs().max()
         assert err < 1e-5, (cfg, float(err))
+
+
+@pytest.mark.parametrize("M", [1024, 40960, 262144])
+@pytest.mark.parametrize("name,N,K,gelu", SHAPES[:3])
+def test_x3s_deterministic_at_tile_counts(gemm, name, N, K, gelu, M):
+    """Interleaved split-operand GEMM: bitwise run-to-run determinism at M = 1024 (36 / 12 workgroups
+    of one tile each: the first tile is the last — the round-5 fault case, whose cause was an untyped
+    ctypes call truncating the pointers, not the kernel), 40960 and 262144 (many tiles per workgroup),
+    and fp32-level agreement with torch on the first rows."""
+    g = torch.Generator(device="cuda").manual_seed(17)
+    A = torch.randn(M, K, device="cuda", generator=g)
+    W = torch.randn(N, K, device="cuda", generator=g) * 0.05
+    b = torch.randn(N, device="cuda", generator=g) * 0.1
+    A2, W2 = _split2(A), _split2(W)
+    outs = []
+    for _ in range(2):
+        o = torch.full((M, N), float("nan"), device="cuda")
+        gemm(32, 0, A2, W2, b, o, K=K)
+        outs.append(o)
+    assert torch.equal(outs[0].view(torch.int32), outs[1].view(torch.int32))
+    ref = A[:4096] @ W.t() + b
+    assert (outs[0][:4096] - ref).abs().max() / ref.abs().max() < 1e-5
