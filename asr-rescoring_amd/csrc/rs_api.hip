@@ -108,6 +108,7 @@ struct rs_model {
     hipEvent_t call_done = nullptr;
     hipStream_t last_stream = nullptr;
     bool have_last = false;
+    bool order_lost = false;     // a call could not record call_done (order_begin reports it)
     // profiling
     bool prof = false;
     std::vector<hipEvent_t> ev_pool;
@@ -264,21 +265,37 @@ int begin_call(rs_model* m, hipStream_t st) {
 // Calls on one model handle are ordered, whatever streams they come on: the handle's workspace,
 // LayerNorm gang tickets and flags are shared by every call, so a call on a different stream than the
 // previous call first makes its stream wait (device-side, hipStreamWaitEvent) for the previous call's
-// work, and every call records the end of its own work.  Host threads must still not share a handle.
+// work, and every call records the end of its own work in call_done (created at finalize on the
+// model's device).  Host threads must still not share a handle.  A failed wait fails the call
+// (RS_EHIP); a failed record cannot change the return of the call it ends, so it is sticky: the next
+// call on the handle fails with RS_EHIP instead of running unordered.
+int order_begin(rs_model* m, hipStream_t st) {
+    if (m->order_lost) {
+        m->order_lost = false;
+        return fail(RS_EHIP, "the previous call on this handle could not record its end (hipEventRecord "
+                             "failed): cross-stream ordering was lost; synchronise the device and retry");
+    }
+    if (m->have_last && st != m->last_stream && m->call_done)
+        HIPTRY(hipStreamWaitEvent(st, m->call_done, 0));
+    return RS_OK;
+}
 struct CallOrder {
     rs_model* m;
     hipStream_t st;
-    CallOrder(rs_model* m_, hipStream_t st_) : m(m_), st(st_) {
-        if (m->have_last && st != m->last_stream && m->call_done) (void)hipStreamWaitEvent(st, m->call_done, 0);
-    }
+    CallOrder(rs_model* m_, hipStream_t st_) : m(m_), st(st_) {}
     ~CallOrder() {
-        if (!m->call_done && hipEventCreateWithFlags(&m->call_done, hipEventDisableTiming) != hipSuccess) return;
+        if (!m->call_done) return;                // not finalized: no call ran kernels
         if (hipEventRecord(m->call_done, st) == hipSuccess) {
             m->last_stream = st;
             m->have_last = true;
+        } else {
+            m->order_lost = true;
         }
     }
 };
+#define CALL_ORDER(m_, st_)                                   \
+    if (int r_ = order_begin((m_), (st_))) return r_;         \
+    CallOrder order_((m_), (st_))
 
 int reserve_impl(rs_model* m, int64_t max_rows) {
     const rs_bert_cfg& c = m->cfg;
@@ -971,6 +988,7 @@ int rs_model_finalize(rs_model* m) {
     }
 #undef UP32
 #undef UP16
+    if (!m->call_done) HIPTRY(hipEventCreateWithFlags(&m->call_done, hipEventDisableTiming));
     m->host.clear();
     m->finalized = true;
     return RS_OK;
@@ -986,8 +1004,9 @@ int rs_pll_score(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, in
                  double* d_pll, float* d_row_lp, void* stream) {
     if (!m || !h_hyp_off || n_hyp < 0 || (n_hyp > 0 && (!d_tok || !d_pll))) return fail(RS_EARG, "null argument");
     hipStream_t st = (hipStream_t)stream;
-    if (n_hyp > 0) HIPTRY(hipSetDevice(m->device));
-    CallOrder order(m, st);
+    if (n_hyp == 0) return RS_OK;
+    HIPTRY(hipSetDevice(m->device));
+    CALL_ORDER(m, st);
     SeqList sl;
     std::vector<int> hso(n_hyp + 1, 0);
     for (int h = 0; h < n_hyp; ++h) {
@@ -996,7 +1015,6 @@ int rs_pll_score(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, in
         for (int p = 1; p <= T - 2; ++p) sl.push(o, T, p, p, -1);   // do_job rows, p = mask_pos
         hso[h + 1] = (int)sl.size();
     }
-    if (n_hyp == 0) return RS_OK;
     float* rows = d_row_lp;
     if (!rows) {
         HIPTRY(m->rowlp_tmp.ensure(sl.size() * 4));
@@ -1018,7 +1036,7 @@ int rs_masked_logprob(rs_model* m, const int32_t* d_ids, const int32_t* h_seq_of
         return fail(RS_EARG, "null argument");
     if (n_seq == 0) return RS_OK;
     HIPTRY(hipSetDevice(m->device));
-    CallOrder order(m, (hipStream_t)stream);
+    CALL_ORDER(m, (hipStream_t)stream);
     SeqList sl;
     for (int s = 0; s < n_seq; ++s) {
         const int o = h_seq_off[s], T = h_seq_off[s + 1] - o;
@@ -1034,7 +1052,7 @@ int rs_cls_score(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, in
     if (!m || !h_hyp_off || n_hyp < 0 || (n_hyp > 0 && (!d_tok || !d_out))) return fail(RS_EARG, "null argument");
     if (n_hyp == 0) return RS_OK;
     HIPTRY(hipSetDevice(m->device));
-    CallOrder order(m, (hipStream_t)stream);
+    CALL_ORDER(m, (hipStream_t)stream);
     SeqList sl;
     for (int h = 0; h < n_hyp; ++h) {
         const int o = h_hyp_off[h], T = h_hyp_off[h + 1] - o;
@@ -1050,7 +1068,7 @@ int rs_token_embed(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_off, 
     if (!m || !h_hyp_off || n_hyp < 0 || (n_hyp > 0 && (!d_tok || !d_emb))) return fail(RS_EARG, "null argument");
     if (n_hyp == 0) return RS_OK;
     HIPTRY(hipSetDevice(m->device));
-    CallOrder order(m, (hipStream_t)stream);
+    CALL_ORDER(m, (hipStream_t)stream);
     SeqList sl;
     for (int h = 0; h < n_hyp; ++h) {
         const int o = h_hyp_off[h], T = h_hyp_off[h + 1] - o;
@@ -1082,7 +1100,7 @@ int rs_bertscore_recall(rs_model* m, const int32_t* d_tok, const int32_t* h_hyp_
             return fail(RS_EARG, "hypothesis " + std::to_string(h) + " has fewer than 2 tokens ([CLS] [SEP])");
     hipStream_t st = (hipStream_t)stream;
     HIPTRY(hipSetDevice(m->device));
-    CallOrder order(m, st);
+    CALL_ORDER(m, st);
     const int H = m->cfg.hidden;
     const size_t n_tok = (size_t)h_hyp_off[n_hyp];
     const bool two = m->kx == 3;                 // fp16x3: two-part embeddings, split-operand cosines
@@ -1142,7 +1160,7 @@ int rs_model_set_sync_check(rs_model* m, int on) {
 int rs_check(rs_model* m, void* stream) {
     if (!m) return fail(RS_EARG, "null model");
     HIPTRY(hipSetDevice(m->device));
-    CallOrder order(m, (hipStream_t)stream);
+    CALL_ORDER(m, (hipStream_t)stream);
     return report_flags(m, (hipStream_t)stream, "scores");
 }
 

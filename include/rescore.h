@@ -103,7 +103,10 @@ int rs_model_set_tensor(rs_model* m, const char* hf_key, const void* host_ptr, i
                         const int64_t* shape, int ndim);
 
 /* Packs the tensors into the kernel layouts (fp16 GEMM weights, fused QKV) on device.
- * Fails with RS_ESTATE naming the first missing key. */
+ * Fails with RS_ESTATE naming the first missing key, RS_EUNSUP for a weight outside the fp16 range.
+ * fp16x3: the split-operand GEMMs form 64 W_hi in fp16, so a model with a projection weight of
+ * |w| >= 1023.75 is packed without them and runs the K-concatenated fp16x3 form (same accuracy,
+ * slower); scores are never affected. */
 int rs_model_finalize(rs_model* m);
 
 /* Sizes the activation workspace for up to max_rows token rows per launch chunk
@@ -121,7 +124,10 @@ int rs_model_reserve(rs_model* m, int64_t max_rows);
  * rs_model_set_sync_check(m, 0) defers that report: the calls only enqueue the check (they stay
  * asynchronous on `stream`), the flags accumulate on the device, and rs_check(m, stream)
  * synchronises `stream`, reports (RS_EUNSUP / RS_EHIP) and clears them.  on = 1 restores the
- * default; call rs_check first so nothing pending is dropped.  No reference counterpart (the
+ * default; call rs_check first so nothing pending is dropped.  In deferred mode a statistics-wait
+ * timeout (RS_EHIP) is sticky on the device until rs_check: every fused-LayerNorm launch after it
+ * drains at once (fail-fast: no further waits), so EVERY result produced between the timeout and
+ * the rs_check that reports it is invalid and must be discarded — not only the timed-out call's.  No reference counterpart (the
  * reference's forward is synchronous PyTorch-CPU, MLM_PLL/main.py:83-107). */
 int rs_model_set_sync_check(rs_model* m, int on);
 int rs_check(rs_model* m, void* stream);

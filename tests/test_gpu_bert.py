@@ -347,3 +347,29 @@ def test_fp16_range_guard(w_tiny, precision):
                         s.score_nbest(nb.tokens, nb.hyp_off)
             finally:
                 s.close()
+
+
+def test_x3s_weight_range_falls_back_to_k_concatenated(w_tiny, monkeypatch):
+    """A projection weight in [1023.75, 65504] fits the fp16 images but not the split-operand K
+    loop's 64 W_hi (it became inf, and the call failed with a misleading range error).
+    rs_model_finalize then packs no split-operand weights and the model runs every fp16x3 layer in
+    the K-concatenated form: finite scores, bitwise equal to RS_X3S=0, within the north_star
+    tolerance of the fp32 oracle."""
+    from asr_rescoring_amd.scorer import PLLScorer
+    from oracle.bert_ref import TorchBert, pll_reference_pattern
+    nb = D.synthetic_nbest(2, 3, seed=5, vocab=BERT_TINY.vocab, len_lo=3, len_hi=12)
+    w = dict(w_tiny)
+    k = "bert.encoder.layer.1.intermediate.dense.weight"
+    w[k] = w[k].copy()
+    w[k][5, 7] = 2000.0
+    s = PLLScorer(w, BERT_TINY, device=0, max_rows=2048, precision="fp16x3")
+    try:
+        a = s.score_nbest(nb.tokens, nb.hyp_off).cpu().numpy()
+        monkeypatch.setenv("RS_X3S", "0")
+        b = s.score_nbest(nb.tokens, nb.hyp_off).cpu().numpy()
+    finally:
+        s.close()
+    assert np.isfinite(a).all()
+    assert np.array_equal(a, b)
+    _, ref = pll_reference_pattern(TorchBert(w, BERT_TINY), nb.tokens, nb.hyp_off, full_head=False)
+    assert rel_err(a, ref).max() < 1e-3

@@ -69,7 +69,8 @@ assert fn({blocks}, {usec}, out.data_ptr(), torch.cuda.current_stream().cuda_str
 time.sleep(0.05)
 print("ready", flush=True)
 torch.cuda.synchronize()
-print("done", int(out[:{blocks}].min().item()), flush=True)
+t_end = time.time()
+print("done", int(out[:{blocks}].min().item()), repr(t_end), flush=True)
 """
 
 
@@ -89,8 +90,10 @@ class _Occupier:
         assert line == "ready", line
 
     def wait(self):
+        """The occupier's output; ``self.t_end``: wall time (time.time()) its kernel was seen done."""
         out = self.p.stdout.read()
         assert self.p.wait(timeout=60) == 0, out
+        self.t_end = float(out.split()[-1])
         return out
 
 
@@ -113,10 +116,13 @@ def test_lnfuse_scores_beside_another_process(scorer, nb_mid, base_scores, monke
     occ = _Occupier(held, 3_000_000)
     t0 = time.perf_counter()
     got = scorer.score(nb_mid)
+    t_ret = time.time()
     dt = time.perf_counter() - t0
     occ.wait()
-    print(f"scored beside {held} held CUs in {dt:.2f} s ({gang})")
-    assert dt < 2.5, f"the call waited for the occupier ({dt:.2f} s)"
+    print(f"scored beside {held} held CUs in {dt:.2f} s ({gang}); occupier ended {occ.t_end - t_ret:.2f} s later")
+    # the call returned while the occupier still held its CUs (no wall-clock bound of our own: the
+    # occupier's end is the reference, whatever the box's speed)
+    assert t_ret < occ.t_end, f"the call waited for the occupier ({dt:.2f} s)"
     assert np.array_equal(got, base_scores)
 
 

@@ -12,6 +12,9 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# the timing-diagnostic build (build.py --diag): the wrong-results GEMM variants / the stamp build
+os.environ.setdefault("RS_LIBRESCORE", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                    "asr-rescoring_amd", "librescore_diag.so"))
 import __graft_entry__  # noqa: E402
 
 __graft_entry__._import_pkg()

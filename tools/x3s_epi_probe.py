@@ -6,8 +6,9 @@ Variants of gemm_x3s_kernel through rs_debug_gemm (cfg 32 fp32 out, cfg 31 GELU 
   alias    every tile stores onto row panel 0 (no HBM write burst; L2-resident lines)
   nw+al    both
   noepi    no stores (bias / GELU math kept)
-PROBE=scale: prod / noscale (no in-register operand scaling in the K loop: 64 W_hi since round 5,
-W_hi/64 and A_hi/64 before) / noepi / bare (no staging, no stores) / bare-noscale.
+(The round-5 PROBE=scale variants — no in-register operand scaling — were removed with their
+kernel bits; the numbers stay in profiles/r5t_x3s_scale.txt.)  Needs the RS_DIAG build
+(python asr-rescoring_amd/build.py --diag); operands are random interleaved images.
 Rounds interleaved in one process; medians.  TF/s of MFMA work (3 x 2MNK).
 Usage: python tools/x3s_epi_probe.py [M] [rounds]
 """
@@ -18,6 +19,9 @@ import sys
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# the timing-diagnostic build (build.py --diag): the wrong-results GEMM variants / the stamp build
+os.environ.setdefault("RS_LIBRESCORE", os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                    "asr-rescoring_amd", "librescore_diag.so"))
 import __graft_entry__  # noqa: E402
 
 __graft_entry__._import_pkg()
@@ -46,10 +50,8 @@ def main():
         fl = 3 * 2.0 * M * N * K
         var = {"f32": (32, out32, {"prod": 0, "nowait": 50, "alias": 51, "nw+al": 53, "noepi": 20}),
                "gelu2": (31, img, {"prod": 0, "nowait": 50, "alias": 51, "nw+al": 53, "noepi": 52})}
-        if os.environ.get("PROBE") == "scale":
-            # the K loop's in-register operand scaling: production, without it (dbg 4), and both
-            # against the bare loop (no staging, no stores: 3, 7)
-            var = {"f32": (32, out32, {"prod": 0, "noscale": 4, "noepi": 20, "bare": 3, "bare-noscale": 7})}
+        if os.environ.get("PROBE") == "bare":
+            var = {"f32": (32, out32, {"prod": 0, "noepi": 20, "bare": 3})}
         times = {}
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         for _ in range(rounds):
