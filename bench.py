@@ -182,12 +182,17 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: running {world} rank(s)", file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # RS_BENCH_DEVICE (rehearsal only): every rank on this one GPU (a multi-rank run on a 1-GPU box,
+    # with RS_DIST_BACKEND=gloo for the exchange); unset on a real node: rank r on GPU LOCAL_RANK
+    if os.environ.get("RS_BENCH_DEVICE") is not None:
+        local = int(os.environ["RS_BENCH_DEVICE"])
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     from asr_rescoring_amd import shard
     if world > 1 or args.force_gather:
         shard.init_from_env(local, force=args.force_gather)
     gather = dist.is_initialized()
+    xdev = shard.exchange_device(dist.get_backend() if gather else None, dev, dev)
 
     from asr_rescoring_amd.scorer import PLLScorer
     weights = weights0 = make_weights(BERT_BASE, seed=1234)
@@ -247,7 +252,10 @@ def main():
     def step():
         lm = scorer.score_nbest(d_tok, nb.hyp_off)               # float64 [H_local]
         pair = torch.stack([am_d, lm])                           # (am, lm) [2, H_local]
-        out = shard.gather_scores(pair, counts) if gather else pair
+        if gather and xdev.type == "cpu":                         # gloo rehearsal: host exchange
+            out = shard.gather_scores(pair.cpu(), counts).to(dev)
+        else:
+            out = shard.gather_scores(pair, counts) if gather else pair
         if rank == 0:
             rerank.fuse_rerank(out[0], out[1], hyp_len_all, nb_all.utt_off, grid, "norm", args.nbest, local)
         return out[1]
@@ -267,7 +275,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    t = torch.tensor([dt], dtype=torch.float64, device=xdev)
     if gather:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
@@ -465,7 +473,8 @@ def main():
                           "utts_total": nb_all.n_utt,
                           "forwards_per_step": n_fwd_all, "forwards_rank0_step": n_fwd,
                           "mean_T": round(mean_T, 2),
-                          "parallelism": f"dp{world} (cost-balanced utterance shards of one global set + one RCCL all_gather"
+                          "parallelism": f"dp{world} (cost-balanced utterance shards of one global set + one "
+                                         + ("gloo (host) " if gather and xdev.type == "cpu" else "RCCL ") + "all_gather"
                                          + (" in every step" if gather else "; none at one rank") + ")"},
                "achieved_tflops_canonical": round(flops_step * args.steps / dt / 1e12, 2),
                "achieved_tflops_basis": ("canonical algorithmic FLOPs of every masked forward (SURVEY 8d) net of "
