@@ -110,6 +110,7 @@ _DEBUG_SIGS = {
     "rs_debug_sgemm_cfg": (CI, [CI] * 4 + [P, CI, CI, P, CI, CI, P, CI, CI, P]),
     "rs_debug_sgemm": (CI, [CI] * 3 + [P, CI, CI, P, CI, CI, P, CI, CI, P]),
     "rs_debug_sgemm_pick": (CI, [CI] * 5),
+    "rs_debug_gelu": (CI, [P, P, CI, P]),
 }
 EXPORTED = tuple(_SIGS)          # the shipped library's entries (include/rescore.h)
 _SIGS.update(_DEBUG_SIGS)

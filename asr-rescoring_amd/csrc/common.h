@@ -85,7 +85,9 @@ inline size_t lnres_granules(int m_pad) { return (size_t)m_pad * 4 * 2 + (size_t
 constexpr float X3_UP = 64.f, X3_DOWN = 1.f / 64.f;
 __host__ __device__ __forceinline__ int il_hi(int c) { return ((c & ~31) << 1) | (c & 31); }
 __device__ __forceinline__ f16 x3_mid(f16 hi) { return (f16)((float)hi * X3_DOWN); }
-__device__ __forceinline__ f16 x3_lo(float v, f16 hi) { return (f16)((v - (float)hi) * X3_UP); }
+// lo = RNE(64 (v - hi)), formed as one fma of the fp16 hi with 64 v (v_fma_mix: 64 (v - hi) is
+// exact in fp32, so the single rounding to fp16 gives the same bits as (v - hi) * 64 rounded)
+__device__ __forceinline__ f16 x3_lo(float v, f16 hi) { return (f16)__builtin_fmaf((float)hi, -X3_UP, v * X3_UP); }
 __device__ __forceinline__ void put_split(f16* row, int c, int K, int kx, float v) {
     const f16 hi = (f16)v;
     if (kx == 2) {

@@ -1281,8 +1281,10 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         for (int j = 0; j < 4; ++j)
 #pragma unroll
                             for (int e = 0; e < 4; ++e)
+                                // h = hi + lo/64 as one v_fma_mix_f32 on the fp16 parts (lo/64 is exact:
+                                // the same single rounding as the add it replaces)
                                 acc16[RB2 * hh + ii][j][e] = __builtin_fmaf(acc16[RB2 * hh + ii][j][e], X3_DOWN, bq[j][e]) +
-                                                             ((float)rh0[ii][j][e] + (float)rl0[ii][j][e] * X3_DOWN);
+                                                             __builtin_fmaf((float)rl0[ii][j][e], X3_DOWN, (float)rh0[ii][j][e]);
                 }
                 stamp(2);                                         // residual read + add
                 // row partials over the wave's 64 columns (lanes l, l^16, l^32, l^48 share a row),
@@ -1843,6 +1845,27 @@ extern "C" int rs_debug_gemm(int cfg, int dbg, const void* A, const void* W, con
         default: return -1;
     }
     return e == hipSuccess ? 0 : -2;
+}
+
+// Test utility (not part of the scoring path): y[i] = gelu2(x[i]) — the epilogues' GELU evaluated
+// elementwise in fp32 (tests/test_gpu_gemm.py checks it against torch's exact-erf GELU).
+namespace {
+__global__ void __launch_bounds__(256) gelu_eval_kernel(const float* __restrict__ x, float* __restrict__ y, int n) {
+    const int i = 2 * (blockIdx.x * 256 + threadIdx.x);
+    if (i + 1 < n) {
+        const f32x2 v = gelu2((f32x2){x[i], x[i + 1]});
+        y[i] = v.x;
+        y[i + 1] = v.y;
+    } else if (i < n) {
+        y[i] = gelu2((f32x2){x[i], 0.f}).x;
+    }
+}
+}  // namespace
+
+extern "C" int rs_debug_gelu(const float* x, float* y, int n, void* stream) {
+    if (n <= 0) return n == 0 ? 0 : -1;
+    hipLaunchKernelGGL(gelu_eval_kernel, dim3((n + 511) / 512), dim3(256), 0, (hipStream_t)stream, x, y, n);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
 }
 
 // Test utility (not part of the scoring path): keeps `blocks` workgroups resident for `usec`
