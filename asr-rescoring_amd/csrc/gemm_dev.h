@@ -25,11 +25,35 @@ __device__ __forceinline__ f32x2 gelu2(f32x2 x) {
     q = __builtin_elementwise_fma(q, a, (f32x2)(-1.151201725e+00f));
     q = __builtin_elementwise_fma(q, a, (f32x2)(-9.999930859e-01f));
     const f32x2 e = {__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
-    const f32x2 r = __builtin_elementwise_max(x, (f32x2)(0.f));
-    // the unclamped |x| in the last product: beyond AMAX it only scales a term below fp32
-    // resolution, and it carries a NaN / inf of x into the result (v_min / v_max return the
-    // non-NaN operand), which the operand-range guard must see (rs_api.hip check_finite)
-    return __builtin_elementwise_fma(-__builtin_elementwise_abs(x), e, r);
+    // relu(x) as x - min(x, 0) (exact for every finite x), not max(x, 0): v_min / v_max return the
+    // non-NaN operand, so max would turn a NaN pre-activation into 0; this form carries a NaN (and
+    // the inf - inf of x = -inf) into the result, where the operand-range guard sees it
+    // (rs_api.hip check_finite)
+    const f32x2 r = x - __builtin_elementwise_min(x, (f32x2)(0.f));
+    return __builtin_elementwise_fma(-a, e, r);
+}
+
+// The two-part image's fp16 <-> fp32 steps as v_fma_mix (one instruction per value; hipcc forms
+// them only for some of the epilogue's values and otherwise converts with v_cvt_f32_f16 and a
+// separate multiply / subtract).  Both are exact rewrites, bitwise equal to the plain forms:
+//   mix_val<E>: hi + lo/64 of element E of a packed (hi, lo) fp16 pair — lo/64 is exact, so the
+//               fused form rounds once, as (float)hi + (float)lo * (1/64) does;
+//   mix_lo2:    RNE(64 x - 64 hi) of a pair into one packed register — 64 (x - hi) is exact in
+//               fp32, so the single rounding to fp16 equals x3_lo's.
+template <int E>
+__device__ __forceinline__ float mix_val(unsigned hi2, unsigned lo2, float inv64) {
+    float d;
+    if constexpr (E == 0)
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel_hi:[1,0,1]" : "=v"(d) : "v"(lo2), "s"(inv64), "v"(hi2));
+    else
+        asm("v_fma_mix_f32 %0, %1, %2, %3 op_sel:[1,0,1] op_sel_hi:[1,0,1]" : "=v"(d) : "v"(lo2), "s"(inv64), "v"(hi2));
+    return d;
+}
+__device__ __forceinline__ unsigned mix_lo2(unsigned hi2, float x0x64, float x1x64, float neg64) {
+    unsigned d;          // mixlo writes the low half (the high half is left for mixhi)
+    asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(hi2), "s"(neg64), "v"(x0x64));
+    asm("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "+v"(d) : "v"(hi2), "s"(neg64), "v"(x1x64));
+    return d;
 }
 
 // 16-byte epilogue store; VAR&64: non-temporal (streamed past L2, keeps the A panels there)

@@ -1278,13 +1278,15 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
 #pragma unroll
                     for (int ii = 0; ii < RB2; ++ii)
 #pragma unroll
-                        for (int j = 0; j < 4; ++j)
+                        for (int j = 0; j < 4; ++j) {
+                            // h = hi + lo/64 by v_fma_mix on the packed fp16 parts (gemm_dev.h mix_val)
+                            const uint2 hv = __builtin_bit_cast(uint2, rh0[ii][j]), lv = __builtin_bit_cast(uint2, rl0[ii][j]);
+                            const float hres[4] = {mix_val<0>(hv.x, lv.x, X3_DOWN), mix_val<1>(hv.x, lv.x, X3_DOWN),
+                                                   mix_val<0>(hv.y, lv.y, X3_DOWN), mix_val<1>(hv.y, lv.y, X3_DOWN)};
 #pragma unroll
                             for (int e = 0; e < 4; ++e)
-                                // h = hi + lo/64 as one v_fma_mix_f32 on the fp16 parts (lo/64 is exact:
-                                // the same single rounding as the add it replaces)
-                                acc16[RB2 * hh + ii][j][e] = __builtin_fmaf(acc16[RB2 * hh + ii][j][e], X3_DOWN, bq[j][e]) +
-                                                             __builtin_fmaf((float)rl0[ii][j][e], X3_DOWN, (float)rh0[ii][j][e]);
+                                acc16[RB2 * hh + ii][j][e] = __builtin_fmaf(acc16[RB2 * hh + ii][j][e], X3_DOWN, bq[j][e]) + hres[e];
+                        }
                 }
                 stamp(2);                                         // residual read + add
                 // row partials over the wave's 64 columns (lanes l, l^16, l^32, l^48 share a row),
@@ -1498,14 +1500,15 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         for (int a = 0; a < 2; ++a)
 #pragma unroll
                             for (int jj = 0; jj < 2; ++jj) {
+                                // hi = RNE(x) (v_cvt_pk_f16_f32), lo = RNE(64 x - 64 hi) (mix_lo2)
                                 half4 hh, hl;
+                                const f32x4 xv = acc16[2 * i2 + a][2 * g + jj];
 #pragma unroll
-                                for (int e = 0; e < 4; ++e) {
-                                    const float x = acc16[2 * i2 + a][2 * g + jj][e];
-                                    const f16 hi = (f16)x;
-                                    hh[e] = hi;
-                                    hl[e] = x3_lo(x, hi);
-                                }
+                                for (int e = 0; e < 4; ++e) hh[e] = (f16)xv[e];
+                                const uint2 hv = __builtin_bit_cast(uint2, hh);
+                                const f32x2 s01 = (f32x2){xv[0], xv[1]} * X3_UP, s23 = (f32x2){xv[2], xv[3]} * X3_UP;
+                                hl = __builtin_bit_cast(half4, (uint2){mix_lo2(hv.x, s01.x, s01.y, -X3_UP),
+                                                                       mix_lo2(hv.y, s23.x, s23.y, -X3_UP)});
                                 const int row = 16 * a + r16, byte = PERM ? 16 * q4 + 8 * jj : 32 * jj + 8 * q4;
                                 *(half4*)(slb + row * 128 + (((byte >> 4) ^ (row & 7)) << 4) + (byte & 8)) = hh;
                                 *(half4*)(slb + row * 128 + ((((byte >> 4) + 4) ^ (row & 7)) << 4) + (byte & 8)) = hl;
