@@ -803,9 +803,27 @@ attn16x3v2_kernel(const float* __restrict__ qkv, SeqMeta sm, int s0, int row0, i
 #pragma unroll
             for (int e = 0; e < 4; ++e) o[dt][e] = __builtin_fmaf(ol[e], LO_UNSCALE, oh[e]);
         }
-        if (t < T) {
-            const float il = 1.0f / ls;
-            f16* orow = ctx + (size_t)(rs + t) * kx * H;
+        const float il = 1.0f / ls;
+        f16* orow = ctx + (size_t)(rs + t) * kx * H;
+        if (kx == 2) {
+            // the interleaved image (common.h): lane (r16, g) holds columns 16 dt + 4 g .. + 3 of its
+            // query row; one v_permlane16_swap per dword trades the odd lane group's hi parts for the
+            // even group's lo parts (rows of 16 lanes: g <-> g ^ 1, the same query row), so every lane
+            // stores 8 consecutive halves with one 16-B store — even g: hi of columns 16 dt + 4 g ..
+            // + 7, odd g: lo of 16 dt + 4 (g - 1) .. + 7 — instead of two 8-B stores (T21)
+#pragma unroll
+            for (int dt = 0; dt < 4; ++dt) {
+                const float4 v = make_float4(o[dt][0] * il, o[dt][1] * il, o[dt][2] * il, o[dt][3] * il);
+                const half4 h = {(f16)v.x, (f16)v.y, (f16)v.z, (f16)v.w};
+                const half4 l = {x3_lo(v.x, h[0]), x3_lo(v.y, h[1]), x3_lo(v.z, h[2]), x3_lo(v.w, h[3])};
+                const uint2 a = __builtin_bit_cast(uint2, h), b = __builtin_bit_cast(uint2, l);
+                const auto r0 = __builtin_amdgcn_permlane16_swap(a.x, b.x, false, false);
+                const auto r1 = __builtin_amdgcn_permlane16_swap(a.y, b.y, false, false);
+                const int c = hd * 64 + dt * 16 + 4 * (g & ~1);
+                if (t < T)
+                    *(uint4*)(orow + il_hi(c) + ((g & 1) ? 32 : 0)) = (uint4){r0[0], r1[0], r0[1], r1[1]};
+            }
+        } else if (t < T) {
 #pragma unroll
             for (int dt = 0; dt < 4; ++dt)
                 put_split4(orow, hd * 64 + dt * 16 + 4 * g, H, kx,
