@@ -10,7 +10,7 @@ echo "[prof] bench"
 timeout -k 10 900 python bench.py > $O/bench.json 2> $O/bench.err
 echo "[prof] kernel trace"
 timeout -k 10 900 rocprofv3 --kernel-trace --stats -d $O/kt -o run --output-format csv -- \
-    python bench.py --cpu-seconds 0 > $O/bench_under_rocprof.json 2> $O/kt.err
+    python bench.py --cpu-seconds 0 --c4-secondary 0 --fp16-steps 0 > $O/bench_under_rocprof.json 2> $O/kt.err
 echo "[prof] pmc fetch"
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $O/fetch -o run --output-format csv -- \
     python bench.py --utts 20 --steps 1 --warmup 0 --cpu-seconds 0 --no-profile > /dev/null 2> $O/fetch.err
