@@ -1167,6 +1167,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             __builtin_amdgcn_sched_barrier(0);
             kstep16(par, BK);
             __builtin_amdgcn_sched_barrier(0);
+            stamp(9);                                             // (stamp build) K-step 0
             kt0 = 1;
         }
         for (int kt = kt0; kt < nk; ++kt) {
@@ -1178,6 +1179,9 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
             __builtin_amdgcn_sched_barrier(0);
             kstep16(cur, kt + 1 < nk ? (kt + 1) * BK : (1 << 29));
             __builtin_amdgcn_sched_barrier(0);
+            if constexpr (STAMP && !LNR) {
+                if (kt == 0) stamp(9);                            // (stamp build) K-step 0
+            }
         }
         stamp(0);                                                 // K loop
         // ---- transition

@@ -1,6 +1,7 @@
 """Phase shares of the split-operand GEMM tiles from the stamp build (rs_debug_stamps): one
 scoring pass of the C3 workload (U utterances x N=50) with every split-operand launch running its
-stamp build; prints, per kernel instance, the mean cycles per tile of each phase (wave 0 of each
+stamp build; prints, per kernel instance, the mean cycles per tile of each phase (kstep0: the tile's
+first K-step, from the end of the previous tile's stores; kloop: the rest) (wave 0 of each
 workgroup; s_memtime ticks) and its share.  The stamp build's fences forbid overlaps the production
 kernel has: read the SHARES, not the absolute time.
 Usage: python tools/stamps.py [U] [RS_LNGANG]"""
@@ -52,7 +53,10 @@ def main():
         per = st[i, :, :7].sum(axis=0) / tiles
         tot = per.sum()
         pro = st[i, :, 8].sum() / max((st[i, :, 7] > 0).sum(), 1)
-        print(f"{name:10s} tiles {int(tiles):7d}  cycles/tile {tot:9.0f}  prologue/workgroup {pro:8.0f}  " +
+        k0 = st[i, :, 9].sum() / tiles                  # K-step 0 (wait for the tile's stage 0 + first barrier)
+        tot += k0
+        print(f"{name:10s} tiles {int(tiles):7d}  cycles/tile {tot:9.0f}  prologue/workgroup {pro:8.0f}  "
+              f"kstep0 {k0:7.0f} ({k0 / tot * 100:4.1f}%)  " +
               "  ".join(f"{p} {v:7.0f} ({v / tot * 100:4.1f}%)" for p, v in zip(PHASES, per) if v > 0), flush=True)
     sc.close()
 
