@@ -1033,6 +1033,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
     // instead of two runs of 4: W image row 32 m + 16 jj + 4 q + e is W row 32 m + 8 q + 4 jj + e.
     // The epilogue's per-lane loads (bias, residual image, LayerNorm weights) become 16-B loads.
     constexpr bool PERM = (VAR & 16777216) != 0;
+    constexpr bool RESDMA = LNR && (VAR & 4) != 0;     // the LayerNorm epilogue's residual by LDS-DMA
     auto wperm = [](int L) {
         return PERM ? (L & ~31) | (((L >> 2) & 3) << 3) | (((L >> 4) & 1) << 2) | (L & 3) : L;
     };
@@ -1251,8 +1252,76 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                 // accumulators, and the spills that forced reloaded values whose waits drained the
                 // next tile's stage 0 inside the statistics publish)
                 constexpr int RB2 = 2;
+                // per row block: acc <- acc / 64 + bias + (hi + lo/64) from packed (hi, lo) fp16 pairs
+                auto add_res = [&](int rb, const half4 (&rh)[4], const half4 (&rl)[4]) __attribute__((always_inline)) {
 #pragma unroll
-                for (int hh = 0; hh < 8 / RB2; ++hh) {
+                    for (int j = 0; j < 4; ++j) {
+                        // h = hi + lo/64 by v_fma_mix on the packed fp16 parts (gemm_dev.h mix_val)
+                        const uint2 hv = __builtin_bit_cast(uint2, rh[j]), lv = __builtin_bit_cast(uint2, rl[j]);
+                        const float hres[4] = {mix_val<0>(hv.x, lv.x, X3_DOWN), mix_val<1>(hv.x, lv.x, X3_DOWN),
+                                               mix_val<0>(hv.y, lv.y, X3_DOWN), mix_val<1>(hv.y, lv.y, X3_DOWN)};
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            acc16[rb][j][e] = __builtin_fmaf(acc16[rb][j][e], X3_DOWN, bq[j][e]) + hres[e];
+                    }
+                };
+                if constexpr (RESDMA) {
+                    // VAR 4: the residual by whole-line LDS-DMA pieces (8 rows x 128 B, as the K loop
+                    // stages its operands) into this wave's 8 KiB of the NEXT tile's stage-0 buffer —
+                    // free here: its last reads (K-step nk - 2) are behind the last K-step's barrier, and
+                    // LATE0 issues stage 0 into it only after the statistics.  Two row blocks in
+                    // flight; the lane reads its (hi, lo) 16-B chunks back in the accumulator layout
+                    // (chunk c of LDS row n at c ^ ((n >> 1) & 7), as the K loop's images).
+                    static_assert(!RESDMA || (LATE0 && PERM), "the residual DMA needs the late stage 0");
+                    const int rbo = (last ^ 1) * STAGE + wave * 8192;
+                    const __amdgpu_buffer_rsrc_t rsR = __builtin_amdgcn_make_buffer_rsrc(
+                        (void*)(img + (size_t)cm0 * ldc), (short)0, 256 * ldc * 2, 0x00020000);
+                    int voR[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {            // q = 2 m + hf: 32-column group m, row half hf
+                        const int jr = 8 * (q & 1) + (lane >> 3);
+                        const int cc = (lane & 7) ^ ((jr >> 1) & 7);
+                        voR[q] = ((wm * WTM + jr) * ldc + 2 * (cn0 + wn * WTN) + 64 * (q >> 1) + 8 * cc) * 2;
+                    }
+                    auto issue = [&](int rb) __attribute__((always_inline)) {
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) {
+                            auto* dst = (__attribute__((address_space(3))) void*)(smem + rbo + (rb & 1) * 4096 + q * 1024);
+                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsR, dst, 16, voR[q], rb * 16 * ldc * 2, 0, 0);
+                        }
+                    };
+                    const uint32_t lrow = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem + rbo +
+                                          r16 * 128;
+                    const uint32_t lh = lrow + ((q4 ^ ((r16 >> 1) & 7)) << 4), ll = lrow + (((q4 + 4) ^ ((r16 >> 1) & 7)) << 4);
+                    issue(0);
+                    issue(1);
+#pragma unroll
+                    for (int rb = 0; rb < 8; ++rb) {
+                        if (rb < 7) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+                        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                        uint4 h0, h1, l0, l1;                 // (hi, lo) of groups m = 0, 1
+                        const int so = (rb & 1) * 4096;
+                        asm volatile(
+                            "ds_read_b128 %0, %4 offset:%6\n\t"
+                            "ds_read_b128 %1, %4 offset:%7\n\t"
+                            "ds_read_b128 %2, %5 offset:%6\n\t"
+                            "ds_read_b128 %3, %5 offset:%7\n\t"
+                            "s_waitcnt lgkmcnt(0)"
+                            : "=&v"(h0), "=&v"(h1), "=&v"(l0), "=&v"(l1)
+                            : "v"(lh), "v"(ll), "i"(so), "i"(so + 2048)
+                            : "memory");
+                        if (rb + 2 < 8) issue(rb + 2);
+                        const half8 vh0 = __builtin_bit_cast(half8, h0), vh1 = __builtin_bit_cast(half8, h1);
+                        const half8 vl0 = __builtin_bit_cast(half8, l0), vl1 = __builtin_bit_cast(half8, l1);
+                        const half4 rh[4] = {(half4){vh0[0], vh0[1], vh0[2], vh0[3]}, (half4){vh0[4], vh0[5], vh0[6], vh0[7]},
+                                             (half4){vh1[0], vh1[1], vh1[2], vh1[3]}, (half4){vh1[4], vh1[5], vh1[6], vh1[7]}};
+                        const half4 rl[4] = {(half4){vl0[0], vl0[1], vl0[2], vl0[3]}, (half4){vl0[4], vl0[5], vl0[6], vl0[7]},
+                                             (half4){vl1[0], vl1[1], vl1[2], vl1[3]}, (half4){vl1[4], vl1[5], vl1[6], vl1[7]}};
+                        add_res(rb, rh, rl);
+                    }
+                }
+#pragma unroll
+                for (int hh = 0; hh < (RESDMA ? 0 : 8 / RB2); ++hh) {
                     half4 rh0[RB2][4], rl0[RB2][4];
 #pragma unroll
                     for (int ii = 0; ii < RB2; ++ii) {
@@ -1280,17 +1349,7 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                         }
                     }
 #pragma unroll
-                    for (int ii = 0; ii < RB2; ++ii)
-#pragma unroll
-                        for (int j = 0; j < 4; ++j) {
-                            // h = hi + lo/64 by v_fma_mix on the packed fp16 parts (gemm_dev.h mix_val)
-                            const uint2 hv = __builtin_bit_cast(uint2, rh0[ii][j]), lv = __builtin_bit_cast(uint2, rl0[ii][j]);
-                            const float hres[4] = {mix_val<0>(hv.x, lv.x, X3_DOWN), mix_val<1>(hv.x, lv.x, X3_DOWN),
-                                                   mix_val<0>(hv.y, lv.y, X3_DOWN), mix_val<1>(hv.y, lv.y, X3_DOWN)};
-#pragma unroll
-                            for (int e = 0; e < 4; ++e)
-                                acc16[RB2 * hh + ii][j][e] = __builtin_fmaf(acc16[RB2 * hh + ii][j][e], X3_DOWN, bq[j][e]) + hres[e];
-                        }
+                    for (int ii = 0; ii < RB2; ++ii) add_res(RB2 * hh + ii, rh0[ii], rl0[ii]);
                 }
                 stamp(2);                                         // residual read + add
                 // row partials over the wave's 64 columns (lanes l, l^16, l^32, l^48 share a row),
@@ -1741,7 +1800,9 @@ hipError_t launch_gemm_x3s_v(int epi, const f16* A, const f16* W, int ldw, int M
             const bool xcd = !(g && !strcmp(g, "ticket"));
             // VAR 1073741824: the next tile's stage 0 issued after the row statistics (O-projection
             // -1.1 %, BertOutput -0.7 %, profiles/r5late0_stage0_after_stats.txt)
-            constexpr int VL = 16777216 | 1073741824 | STV;
+            // VAR 4: the residual by whole-line LDS-DMA (round 6: O-projection -1.9 %, BertOutput -1.0 %,
+            // C3 +0.4 %, bitwise; profiles/r6o_lnres_residual_dma.txt)
+            constexpr int VL = 16777216 | 1073741824 | 4 | STV;
             if (xcd) {
                 if (K > 1024) return launch_x3s<EPI_LNRES_IMG, VL | 67108864 | 134217728>(A, W, M_pad, N_pad, K, ep, st, ldw);
                 return launch_x3s<EPI_LNRES_IMG, VL | 134217728>(A, W, M_pad, N_pad, K, ep, st, ldw);

@@ -1,6 +1,7 @@
 """Scores of two library builds compared BITWISE on the same inputs (one process per build:
 RS_LIBRESCORE selects the library).  Usage:
-    bitwise_ab.py LIB_A LIB_B OUTDIR     (parent: runs both, compares, prints one JSON line)
+    bitwise_ab.py LIB_A LIB_B OUTDIR     (parent: runs both, compares, prints one JSON line;
+                                          LIB@VAR=VALUE,...: that library under env switches)
 Inputs: the fp16x3 golden tokens (F1), 40 C3 utterances x N=50, 150 C4 utterances x N=100 at the
 alfred real lengths; bert-base random init seed 1234, fp16x3, default kernels."""
 import json
@@ -45,9 +46,12 @@ if __name__ == "__main__":
     la, lb, od = sys.argv[1:4]
     os.makedirs(od, exist_ok=True)
     outs = []
-    for tag, lib in (("a", la), ("b", lb)):
+    for tag, spec in (("a", la), ("b", lb)):
+        # LIB or LIB@VAR=VALUE,...: the same library under other environment switches
+        lib, _, envs = spec.partition("@")
         o = os.path.join(od, f"scores_{tag}.npz")
         env = dict(os.environ, RS_LIBRESCORE=os.path.abspath(lib))
+        env.update(dict(kv.split("=", 1) for kv in envs.split(",") if kv))
         subprocess.run([sys.executable, os.path.abspath(__file__), "--one", o], env=env, check=True, timeout=600)
         outs.append(np.load(o))
     rec = {"lib_a": la, "lib_b": lb}
