@@ -1189,9 +1189,32 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
         const int last = (par + nk - 1) & 1;                      // buffer of the last K-step
         const int cm0 = m0, cn0 = n0;
         // bias of this tile (16-B quads of the lane's 4 consecutive columns, 16 j + 4 (l >> 4) of
-        // the wave's 64): only the bias loads are outstanding here (the last K-step issued no
-        // DMA), so one vmcnt(0) waits for exactly them; inline asm keeps the compiler from placing
-        // its own wait
+        // the wave's 64): only the bias loads (and, LayerNorm build, the residual's first pieces)
+        // are outstanding here (the last K-step issued no DMA), so one vmcnt(0) waits for exactly
+        // them; inline asm keeps the compiler from placing its own wait
+        // LayerNorm build (VAR 4): the residual's first two row blocks go out as LDS-DMA before the
+        // bias loads, so their latency and the bias loads' overlap (lnres_epilogue streams the rest)
+        const int rbo = (last ^ 1) * STAGE + wave * 8192;
+        const __amdgpu_buffer_rsrc_t rsR = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)((const f16*)ep.out + (size_t)cm0 * ep.ldc), (short)0, 256 * ep.ldc * 2, 0x00020000);
+        int voR[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {            // q = 2 m + hf: 32-column group m, row half hf
+            const int jr = 8 * (q & 1) + (lane >> 3);
+            const int cc = (lane & 7) ^ ((jr >> 1) & 7);
+            voR[q] = ((wm * WTM + jr) * ep.ldc + 2 * (cn0 + wn * WTN) + 64 * (q >> 1) + 8 * cc) * 2;
+        }
+        auto issue = [&](int rb) __attribute__((always_inline)) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                auto* dst = (__attribute__((address_space(3))) void*)(smem + rbo + (rb & 1) * 4096 + q * 1024);
+                __builtin_amdgcn_raw_ptr_buffer_load_lds(rsR, dst, 16, voR[q], rb * 16 * ep.ldc * 2, 0, 0);
+            }
+        };
+        if constexpr (RESDMA) {
+            issue(0);
+            issue(1);
+        }
         f32x4 bq[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -1272,29 +1295,11 @@ gemm_x3s_kernel(const f16* __restrict__ A, const f16* __restrict__ W, int K, int
                     // LATE0 issues stage 0 into it only after the statistics.  Two row blocks in
                     // flight; the lane reads its (hi, lo) 16-B chunks back in the accumulator layout
                     // (chunk c of LDS row n at c ^ ((n >> 1) & 7), as the K loop's images).
+                    // (pieces of row blocks 0 and 1 issued at the transition, before the bias loads)
                     static_assert(!RESDMA || (LATE0 && PERM), "the residual DMA needs the late stage 0");
-                    const int rbo = (last ^ 1) * STAGE + wave * 8192;
-                    const __amdgpu_buffer_rsrc_t rsR = __builtin_amdgcn_make_buffer_rsrc(
-                        (void*)(img + (size_t)cm0 * ldc), (short)0, 256 * ldc * 2, 0x00020000);
-                    int voR[4];
-#pragma unroll
-                    for (int q = 0; q < 4; ++q) {            // q = 2 m + hf: 32-column group m, row half hf
-                        const int jr = 8 * (q & 1) + (lane >> 3);
-                        const int cc = (lane & 7) ^ ((jr >> 1) & 7);
-                        voR[q] = ((wm * WTM + jr) * ldc + 2 * (cn0 + wn * WTN) + 64 * (q >> 1) + 8 * cc) * 2;
-                    }
-                    auto issue = [&](int rb) __attribute__((always_inline)) {
-#pragma unroll
-                        for (int q = 0; q < 4; ++q) {
-                            auto* dst = (__attribute__((address_space(3))) void*)(smem + rbo + (rb & 1) * 4096 + q * 1024);
-                            __builtin_amdgcn_raw_ptr_buffer_load_lds(rsR, dst, 16, voR[q], rb * 16 * ldc * 2, 0, 0);
-                        }
-                    };
                     const uint32_t lrow = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)smem + rbo +
                                           r16 * 128;
                     const uint32_t lh = lrow + ((q4 ^ ((r16 >> 1) & 7)) << 4), ll = lrow + (((q4 + 4) ^ ((r16 >> 1) & 7)) << 4);
-                    issue(0);
-                    issue(1);
 #pragma unroll
                     for (int rb = 0; rb < 8; ++rb) {
                         if (rb < 7) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
