@@ -129,6 +129,31 @@ struct SgOperand {
             }
         }
     }
+    // piece i of stage() without the wave-uniform branch: masked by its own k (only a tail K-step
+    // has masked lanes), so the DMA pieces can sit inside a straight-line MFMA stream
+    __device__ __forceinline__ void stage_piece(char* lds, int wave, int k0, int ke, int i) const {
+        const int so = KC ? k0 * 4 : k0 * ld * 4;
+        const bool in = k0 + krow[i] < ke;
+        const unsigned vo = in ? voff[i] : oob;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rs, (__attribute__((address_space(3))) void*)(lds + (NW * i + wave) * 1024), 16, vo, so, 0, 0);
+    }
+    // The fragment reads of T 32-row tiles (rows r0 + 32 t) cut into units the software-pipelined
+    // kernel spreads over its MFMA stream: KC, unit u = one ds_read_b128 (tile u / 4, 16-B chunk
+    // u % 4); MC, unit u = k-row u of every tile (adjacent tiles pair into ds_read2_b32).
+    static constexpr int units(int tiles) { return KC ? 4 * tiles : BK / 2; }
+    template <int T>
+    __device__ __forceinline__ static void frag_unit(const char* img, int r0, int h, int u, float (&f)[T][BK / 2]) {
+        if (KC) {
+            const int t = u / 4, q = u % 4, r = r0 + 32 * t;
+            const int pc = ((BK / 8) * h + q) ^ ((r >> SH) & (NCH - 1));
+            const float4 v = *(const float4*)(img + r * BK * 4 + pc * 16);
+            f[t][4 * q] = v.x; f[t][4 * q + 1] = v.y; f[t][4 * q + 2] = v.z; f[t][4 * q + 3] = v.w;
+        } else {
+#pragma unroll
+            for (int t = 0; t < T; ++t) f[t][u] = *(const float*)(img + ((BK / 2) * h + u) * R * 4 + (r0 + 32 * t) * 4);
+        }
+    }
     // fragments of one 32-row MFMA tile for a K-step: f[kk] = operand(row r, k = (BK/2) h + kk)
     __device__ __forceinline__ static void frag(const char* img, int r, int h, float (&f)[BK / 2]) {
         if (KC) {
@@ -317,6 +342,154 @@ sgemm_pipe_kernel(const float* __restrict__ A, int lda, const float* __restrict_
         if (t + 1 < nt) step(t + 1, ga, gb, fa, fb);
     }
 
+    float* P = ws ? ws + (size_t)z * M * N : nullptr;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int col = n0 + wn + 32 * j + c;
+            if (col >= N) continue;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
+                if (row >= M) continue;
+                if (P) {
+                    P[(size_t)row * N + col] = acc[i][j][r];
+                } else {
+                    float* o = C + (size_t)row * ldc + col;
+                    *o = accum ? acc[i][j][r] + *o : acc[i][j][r];
+                }
+            }
+        }
+}
+
+// Software-pipelined form with a straight-line K loop (cfg 12-16).  The forms above read a
+// K-step's fragments between the barrier and its MFMAs, so every wave of a CU reads its 16 KiB
+// from LDS at the same moment while its MFMA pipe idles: at one workgroup per CU (a 5.3k-token
+// GEMM with N = 768 has 252 tiles of 128×128) that is ≈ 20 % of each K-step.  Here the
+// fragments of step t + 1 are read during step t's MFMAs, spread over its first 12 kk groups,
+// the DMA pieces of step t + NS over its first 8, and the only gap left between two MFMA
+// streams is the barrier.  NS LDS stages in NS distinct __shared__ objects (the compiler then
+// sees that the DMA into one does not alias the fragment reads from another and puts no
+// vmcnt(0) in front of them), step s in stage s % NS: step t, from the barrier on, issues the
+// DMA of step t + NS into the stage step t came from (its fragments are in registers, every
+// wave's reads completed before the barrier), so each DMA has NS - 1 K-steps to land.  Two
+// register sets of fragments swap roles from step to step; a loop trip is lcm(2, NS) steps so
+// every stage and register role is a compile-time constant, and nothing in a trip branches (a
+// DMA past the last K-step re-loads the last one), which keeps the accumulators in place.
+template <bool AKC, bool BKC, int BM, int BN, int TM, int NS, int OCC>
+__global__ void __launch_bounds__((BM / TM) * (BN / 64) * 64, OCC * (BM / TM) * (BN / 64) / 4)
+sgemm_sp_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb, float* __restrict__ C,
+                int ldc, int M, int N, int K, int kc, int accum, float* __restrict__ ws) {
+    constexpr int BK = 32, WM = BM / TM, WN = BN / 64, NW = WM * WN, MT = TM / 32, HK = BK / 2;
+    constexpr int IMG_A = BM * BK * 4, STAGE = (BM + BN) * BK * 4;
+    using OA = SgOperand<AKC, BM, NW, BK>;
+    using OB = SgOperand<BKC, BN, NW, BK>;
+    constexpr int UA = OA::units(MT), UB = OB::units(2), RG = 12;   // read units over RG kk groups,
+    constexpr int NPC = OA::NP + OB::NP < 8 ? OA::NP + OB::NP : 8;  // DMA pieces over NPC kk groups
+    static_assert(NS >= 2 && NS <= 4, "stages");
+    constexpr int TRIP = NS == 3 ? 6 : NS;                          // steps per loop trip: even, NS | TRIP
+    constexpr int NPW = OA::NP + OB::NP;                            // DMA pieces per wave per K-step
+    __shared__ __attribute__((aligned(16))) char s0[STAGE];
+    __shared__ __attribute__((aligned(16))) char s1[STAGE];
+    __shared__ __attribute__((aligned(16))) char s2[NS > 2 ? STAGE : 16];
+    __shared__ __attribute__((aligned(16))) char s3[NS > 3 ? STAGE : 16];
+    auto stg = [&](int i) -> char* { return i == 0 ? s0 : i == 1 ? s1 : i == 2 ? s2 : s3; };   // i constant
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    int tm, tn, z;
+    sg_tile((M + BM - 1) / BM, (N + BN - 1) / BN, tm, tn, z);
+    const int m0 = tm * BM, n0 = tn * BN;
+    const int kb = z * kc, ke = min(K, kb + kc);
+    const int nt = (ke - kb + BK - 1) / BK;
+    const int wm = (wave % WM) * TM, wn = (wave / WM) * 64;
+    const int h = lane >> 5, c = lane & 31;
+
+    OA oa;
+    OB ob;
+    oa.init(A, lda, M, m0, wave, lane);
+    ob.init(B, ldb, N, n0, wave, lane);
+
+    f32x16_t acc[MT][2];
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    // DMA piece p (A's, then B's) of K-step s (past the last: the last again)
+    auto dma_piece = [&](char* dst, int s, int p) {
+        const int k0 = kb + min(s, nt - 1) * BK;
+        if (p < OA::NP) oa.stage_piece(dst, wave, k0, ke, p);
+        else ob.stage_piece(dst + IMG_A, wave, k0, ke, p - OA::NP);
+    };
+    auto dma = [&](char* dst, int s) {
+#pragma unroll
+        for (int p = 0; p < OA::NP + OB::NP; ++p) dma_piece(dst, s, p);
+    };
+    auto mfmas = [&](int kk, const float (&xa)[MT][HK], const float (&xb)[2][HK]) {
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[i][kk], xb[j][kk], acc[i][j], 0, 0, 0);
+    };
+    // step t: MFMAs on (xa, xb) = its fragments; (ya, yb) <- step t + 1's from src; DMA of step
+    // t + 2 into dst (= the stage step t was read from)
+    auto step = [&](int t, char* dst, const char* src, const float (&xa)[MT][HK], const float (&xb)[2][HK],
+                    float (&ya)[MT][HK], float (&yb)[2][HK]) {
+        // step t + 1's DMA landed (the NS - 2 later ones may still fly); step t's reads done
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NS - 2) * NPW) : "memory");
+        __builtin_amdgcn_s_barrier();                  // (not __syncthreads: its fence waits vmcnt(0))
+        asm volatile("" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int kk = 0; kk < HK; ++kk) {
+            if (kk < NPC)
+#pragma unroll
+                for (int p = kk * NPW / NPC; p < (kk + 1) * NPW / NPC; ++p) dma_piece(dst, t + NS, p);
+            if (kk < RG) {
+#pragma unroll
+                for (int u = kk * UA / RG; u < (kk + 1) * UA / RG; ++u) OA::frag_unit(src, wm + c, h, u, ya);
+#pragma unroll
+                for (int u = kk * UB / RG; u < (kk + 1) * UB / RG; ++u) OB::frag_unit(src + IMG_A, wn + c, h, u, yb);
+            }
+            mfmas(kk, xa, xb);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+
+    float fa[MT][HK], fb[2][HK], ga[MT][HK], gb[2][HK];
+#pragma unroll
+    for (int i = 0; i < NS; ++i) dma(stg(i), i);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NS - 1) * NPW) : "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < UA; ++u) OA::frag_unit(s0, wm + c, h, u, fa);
+#pragma unroll
+    for (int u = 0; u < UB; ++u) OB::frag_unit(s0 + IMG_A, wn + c, h, u, fb);
+    // step t + i of a trip (t a multiple of TRIP): its stage i % NS, the next one's (i + 1) % NS
+    int t = 0;
+    for (; t + TRIP <= nt; t += TRIP) {
+#pragma unroll
+        for (int i = 0; i < TRIP; i += 2) {
+            step(t + i, stg(i % NS), stg((i + 1) % NS), fa, fb, ga, gb);
+            step(t + i + 1, stg((i + 1) % NS), stg((i + 2) % NS), ga, gb, fa, fb);
+        }
+    }
+    // the last nt - t < TRIP steps (a step's read of K-step nt and DMA past it are harmless); a
+    // chain of exits, so no register set stays live across a join
+#pragma unroll
+    for (int i = 0; i < TRIP - 1; ++i) {
+        if (t + i >= nt) break;
+        if (i % 2 == 0) step(t + i, stg(i % NS), stg((i + 1) % NS), fa, fb, ga, gb);
+        else step(t + i, stg(i % NS), stg((i + 1) % NS), ga, gb, fa, fb);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no LDS-DMA outlives the workgroup
+
+    // D map of the 32x32 forms: column = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
     float* P = ws ? ws + (size_t)z * M * N : nullptr;
 #pragma unroll
     for (int i = 0; i < MT; ++i)
@@ -729,14 +902,19 @@ sgemm_splitk_sum_kernel(const float* __restrict__ ws, int splits, int M, int N, 
 // resident at once), 2 = 256×128×32 (8 waves of 64×64, 1 per CU; half the operand bytes per
 // FLOP of a 128×128 tile on the A side).
 struct SgCfg { int bm, bn, bk, occ; };
-constexpr int kSgNCfg = 12;
+constexpr int kSgNCfg = 17;
 constexpr SgCfg kSgCfg[kSgNCfg] = {{128, 128, 32, 2}, {128, 128, 16, 4}, {256, 128, 32, 1},
                                    {128, 128, 16, 3}, {128, 128, 32, 1},    // 3, 4: sgemm_pipe_kernel
                                    {128, 64, 32, 2},  {128, 64, 32, 3},     // 5, 6: 4 waves of 32×64
                                    {64, 64, 32, 4},   {64, 64, 32, 6},      // 7, 8: 2 waves of 32×64
                                    {192, 128, 32, 2},                       // 9: 4 waves of 96×64
                                    {256, 256, 32, 1},                       // 10: 8 waves of 128×64
-                                   {64, 64, 32, 2}};                        // 11: sgemm_d64_kernel
+                                   {64, 64, 32, 2},                         // 11: sgemm_d64_kernel
+                                   {128, 128, 32, 2},                       // 12-16: sgemm_sp_kernel: 2 stages,
+                                   {192, 128, 32, 1},                       //   3 (4 waves of 96×64),
+                                   {256, 128, 32, 1},                       //   3 (8 waves of 64×64),
+                                   {128, 128, 32, 1},                       //   3,
+                                   {128, 128, 32, 1}};                      //   4 stages
 
 // Modelled time (µs) of one configuration at a split count: dispatch rounds × (K-steps per
 // workgroup × the time a CU takes per K-step with its resident workgroups + a per-round
@@ -760,6 +938,18 @@ double sg_model(int cfg, int M, int N, int K, int sp, bool mcmc, int cus_) {
     double t_one = 2.14 * vol, t_full = 3.74 * vol * g.occ / 2.0;
     const long long wgs = tiles * spr, cus = cus_;
     double t;
+    if (cfg >= 12) {
+        // software-pipelined tiles: a CU retires a workgroup's K-step in the same time alone as
+        // beside a second one (the LDS reads and the barrier no longer idle the MFMA pipe), so
+        // the time is the K-steps of the most loaded CU, ceil(wgs / CUs) workgroups.  Fitted to
+        // the split sweep of the 27 training shapes (profiles/r6y_sgemm_split_sweep.txt, 135
+        // points, 3.4 % rms): 1.745 µs per 128×128 K-step, 1.94 µs per workgroup, 8.0 µs, and for
+        // a split 0.52 µs + 0.121 µs per MB of partials written and read
+        const long long rounds = (wgs + cus - 1) / cus;
+        t = 1.745 * vol * rounds * per + 1.94 * rounds + 8.0;
+        if (spr > 1) t += 0.52 + 0.121e-6 * (2.0 * spr + 1.0) * M * N * 4.0;
+        return t;
+    }
     if (cfg == 11) {
         // 64×64 direct-to-register tiles: a wave runs every fourth K-step; small workgroups are
         // dispatched as slots free up, so the load is continuous in the grid size rather than in
@@ -790,7 +980,12 @@ int sg_splits(int cfg, int M, int N, int K, int* kc, bool mcmc, int cus) {
         splits = std::min(forced, std::max(1, steps));
     } else {
         double best = 1e30;
+        const long long tiles = (long long)((M + g.bm - 1) / g.bm) * ((N + g.bn - 1) / g.bn);
         for (int sp = 1; sp <= 16 && sp <= std::max(1, steps / 4); ++sp) {
+            // software-pipelined tiles: no split past two workgroups per CU (a third round of
+            // short splits measured well above the model: profiles/r6y_sgemm_split_sweep.txt)
+            const int per_ = (steps + sp - 1) / sp;
+            if (cfg >= 12 && sp > 1 && tiles * ((steps + per_ - 1) / per_) > 2LL * cus) break;
             const double t = sg_model(cfg, M, N, K, sp, mcmc, cus);
             if (t < best) {
                 best = t;
@@ -803,34 +998,23 @@ int sg_splits(int cfg, int M, int N, int K, int* kc, bool mcmc, int cus) {
     return (steps + per - 1) / per;
 }
 
-// The tile configuration: 128×128 (cfg 0), 192×128 (cfg 9) or 64×64 direct (cfg 11), whichever
-// the model times lower at its best split (192×128 wins where the 128×128 grid leaves a half-empty last round, e.g.
-// 5300 × 2304).  RS_SGEMM_CFG=0..11 forces a configuration (A/B knob).  The choice depends on
-// the shape and the device's CU count only, so a shape's results stay bitwise reproducible on a
-// given device model.
+// The tile configuration: the software-pipelined 128×128 tile (cfg 12) at its best split, or
+// the 64×64 direct-to-register form (cfg 11) where its (coarser) model wins by 10 %: the ~1k-token
+// GEMMs whose 128×128 grid leaves most of the chip idle (1100 × 768 × 768: one pass of 216
+// tiles).  Against rocBLAS / hipBLASLt at the 27 training shapes: profiles/r6*_sgemm_all.jsonl.
+// RS_SGEMM_CFG=0..16 forces a configuration (A/B knob).  The choice depends on the shape and the
+// device's CU count only, so a shape's results stay bitwise reproducible on a given device model.
 int sg_pick(int M, int N, int K, bool mcmc, int cus) {
     static const int forced = [] {
         const char* v = getenv("RS_SGEMM_CFG");
         return v ? atoi(v) : -1;
     }();
     if (forced >= 0 && forced < kSgNCfg) return forced;
-    int best = 0;
-    double tb = 1e30;
-    for (int cfg : {0, 9}) {
-        int kc = 0;
-        const int sp = sg_splits(cfg, M, N, K, &kc, mcmc, cus);
-        const double t = sg_model(cfg, M, N, K, sp, mcmc, cus);
-        if (t < 0.97 * tb) {
-            tb = t;
-            best = cfg;
-        }
-    }
-    // the 64×64 direct-to-register form where its (coarser) model wins by 10 %: the ~1k-token
-    // GEMMs whose 128×128 grid needs split-K (1100 × 768 × 768: 27.5 -> 18.7 µs)
     int kc = 0;
+    const int sp12 = sg_splits(12, M, N, K, &kc, mcmc, cus);
+    const double t12 = sg_model(12, M, N, K, sp12, mcmc, cus);
     const int sp11 = sg_splits(11, M, N, K, &kc, mcmc, cus);
-    if (sg_model(11, M, N, K, sp11, mcmc, cus) < 0.9 * tb) best = 11;
-    return best;
+    return sg_model(11, M, N, K, sp11, mcmc, cus) < 0.9 * t12 ? 11 : 12;
 }
 
 bool sk_enabled() {                                 // read per call (tests flip it in-process)
@@ -959,6 +1143,16 @@ static hipError_t sg_run(int cfg, int M, int N, int K, const float* A, int lda, 
         else if (b_kc) SG_LAUNCH(KER, false, true, BM_, BN_, TM_, KB_, OCC_);     \
         else SG_LAUNCH(KER, false, false, BM_, BN_, TM_, KB_, OCC_);              \
     } while (0)
+#define SP_LAUNCH(AK, BK_, BM_, BN_, TM_, NS_, OCC_)                                                          \
+    hipLaunchKernelGGL((sgemm_sp_kernel<AK, BK_, BM_, BN_, TM_, NS_, OCC_>), grid, dim3((BM_ / TM_) * (BN_ / 64) * 64), \
+                       0, s, A, lda, B, ldb, C, ldc, M, N, K, kc, accum, P)
+#define SP_FORMS(BM_, BN_, TM_, NS_, OCC_)                                     \
+    do {                                                                       \
+        if (a_kc && b_kc) SP_LAUNCH(true, true, BM_, BN_, TM_, NS_, OCC_);     \
+        else if (a_kc) SP_LAUNCH(true, false, BM_, BN_, TM_, NS_, OCC_);       \
+        else if (b_kc) SP_LAUNCH(false, true, BM_, BN_, TM_, NS_, OCC_);       \
+        else SP_LAUNCH(false, false, BM_, BN_, TM_, NS_, OCC_);                \
+    } while (0)
     if (cfg == 0) SG_FORMS(sgemm_dma_kernel, 128, 128, 64, 32, 2);
     else if (cfg == 1) SG_FORMS(sgemm_dma_kernel, 128, 128, 64, 16, 4);
     else if (cfg == 2) SG_FORMS(sgemm_dma_kernel, 256, 128, 64, 32, 1);
@@ -970,6 +1164,11 @@ static hipError_t sg_run(int cfg, int M, int N, int K, const float* A, int lda, 
     else if (cfg == 8) SG_FORMS(sgemm_dma_kernel, 64, 64, 32, 32, 6);
     else if (cfg == 9) SG_FORMS(sgemm_dma_kernel, 192, 128, 96, 32, 2);
     else if (cfg == 10) SG_FORMS(sgemm_dma_kernel, 256, 256, 128, 32, 1);
+    else if (cfg == 12) SP_FORMS(128, 128, 64, 2, 2);
+    else if (cfg == 13) SP_FORMS(192, 128, 96, 3, 1);
+    else if (cfg == 14) SP_FORMS(256, 128, 64, 3, 1);
+    else if (cfg == 15) SP_FORMS(128, 128, 64, 3, 1);
+    else if (cfg == 16) SP_FORMS(128, 128, 64, 4, 1);
     else {
         static const hipError_t attr = [] {
             for (const void* f : {(const void*)sgemm_d64_kernel<true, true>, (const void*)sgemm_d64_kernel<true, false>,
@@ -987,6 +1186,8 @@ static hipError_t sg_run(int cfg, int M, int N, int K, const float* A, int lda, 
         else D64_LAUNCH(false, false);
 #undef D64_LAUNCH
     }
+#undef SP_FORMS
+#undef SP_LAUNCH
 #undef SG_FORMS
 #undef SG_LAUNCH
     hipError_t e = hipGetLastError();

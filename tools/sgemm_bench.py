@@ -1,7 +1,8 @@
 """Trainer fp32 GEMM (k_sgemm.hip, rs_debug_sgemm_cfg) vs torch fp32 matmul (rocBLAS / hipBLASLt)
 at the bert-base training shapes: forward / dgrad / wgrad of each Linear and the tied MLM
 decoder, for a 1.1k-token MLM batch and a 5.3k-token RescoreBert batch; every tile
-configuration named in SG_CFGS (default 0: 128x128, 9: 192x128, 11: 64x64 direct-to-register)
+configuration named in SG_CFGS (default 0: 128x128, 11: 64x64 direct-to-register, 12: 128x128
+software-pipelined)
 and the shape's pick (-1), interleaved in
 one process.  Usage: python tools/sgemm_bench.py"""
 import ctypes
@@ -36,7 +37,7 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         return e0.elapsed_time(e1) / reps
-    CFGS = (-1,) + tuple(int(c) for c in os.environ.get("SG_CFGS", "0,9,11").split(","))
+    CFGS = (-1,) + tuple(int(c) for c in os.environ.get("SG_CFGS", "0,11,12").split(","))
     tot = {c: 0.0 for c in CFGS}
     tot_ref = 0.0
     for T in (1100, 5300):
