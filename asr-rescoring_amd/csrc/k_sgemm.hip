@@ -902,7 +902,7 @@ sgemm_splitk_sum_kernel(const float* __restrict__ ws, int splits, int M, int N, 
 // resident at once), 2 = 256×128×32 (8 waves of 64×64, 1 per CU; half the operand bytes per
 // FLOP of a 128×128 tile on the A side).
 struct SgCfg { int bm, bn, bk, occ; };
-constexpr int kSgNCfg = 17;
+constexpr int kSgNCfg = 20;
 constexpr SgCfg kSgCfg[kSgNCfg] = {{128, 128, 32, 2}, {128, 128, 16, 4}, {256, 128, 32, 1},
                                    {128, 128, 16, 3}, {128, 128, 32, 1},    // 3, 4: sgemm_pipe_kernel
                                    {128, 64, 32, 2},  {128, 64, 32, 3},     // 5, 6: 4 waves of 32×64
@@ -914,7 +914,10 @@ constexpr SgCfg kSgCfg[kSgNCfg] = {{128, 128, 32, 2}, {128, 128, 16, 4}, {256, 1
                                    {192, 128, 32, 1},                       //   3 (4 waves of 96×64),
                                    {256, 128, 32, 1},                       //   3 (8 waves of 64×64),
                                    {128, 128, 32, 1},                       //   3,
-                                   {128, 128, 32, 1}};                      //   4 stages
+                                   {128, 128, 32, 1},                       //   4 stages;
+                                   {64, 128, 32, 2},                        // 17-19: 2 stages, 4 waves of
+                                   {128, 64, 32, 2},                        //   32×64 / 2 waves of 32×64
+                                   {64, 64, 32, 4}};
 
 // Modelled time (µs) of one configuration at a split count: dispatch rounds × (K-steps per
 // workgroup × the time a CU takes per K-step with its resident workgroups + a per-round
@@ -945,16 +948,21 @@ double sg_model(int cfg, int M, int N, int K, int sp, bool mcmc, int cus_) {
         // the split sweep of the 27 training shapes (profiles/r6y_sgemm_split_sweep.txt, 135
         // points, 3.4 % rms): 1.745 µs per 128×128 K-step, 1.94 µs per workgroup, 8.0 µs, and for
         // a split 0.52 µs + 0.121 µs per MB of partials written and read
+        // (per workgroup 0.66 + 1.28 vol, fixed 5.4 + 2.6 vol: the 64×128 / 128×64 tiles' 1.27 and
+        // 6.7 fitted to their 1100-token sweep, profiles/r6aa_sgemm_small_tiles.txt, 2.9 % rms)
         const long long rounds = (wgs + cus - 1) / cus;
-        t = 1.745 * vol * rounds * per + 1.94 * rounds + 8.0;
+        t = 1.745 * vol * rounds * per + (0.66 + 1.28 * vol) * rounds + 5.4 + 2.6 * vol;
         if (spr > 1) t += 0.52 + 0.121e-6 * (2.0 * spr + 1.0) * M * N * 4.0;
         return t;
     }
     if (cfg == 11) {
-        // 64×64 direct-to-register tiles: a wave runs every fourth K-step; small workgroups are
-        // dispatched as slots free up, so the load is continuous in the grid size rather than in
-        // whole rounds.  Fitted to the 27 training shapes (profiles/r4f_sgemm_cfg11.txt, 9 % rms):
-        // 1.55 µs per wave K-step alone, 4.5 µs per K-step-round at two workgroups per CU, 10 µs
+        // 64×64 direct-to-register tiles: a wave runs every fourth K-step.  One pass (at most one
+        // workgroup per CU): 2.1 µs per wave K-step + 8 µs (profiles/r6y_sgemm_split_sweep.txt,
+        // split 1, 8 shapes, 0.85-1.2x); otherwise small workgroups are dispatched as slots free
+        // up, so the load is continuous in the grid size rather than in whole rounds, fitted to
+        // the 27 training shapes (profiles/r4f_sgemm_cfg11.txt, 9 % rms): 1.55 µs per wave K-step
+        // alone, 4.5 µs per K-step-round at two workgroups per CU, 10 µs
+        if (wgs <= cus) return 8.0 + 2.1 * ((per + 3) / 4) + (spr > 1 ? 4.24 + (2.0 * spr + 1.0) * M * N * 4.0 * 0.127e-6 : 0.0);
         t = 10.0 + (per + 3) / 4 * std::max(1.55, (double)wgs / (cus * g.occ) * 4.5);
     } else {
         if (cfg == 9) { t_one = 3.43; t_full = 6.4; }
@@ -998,10 +1006,10 @@ int sg_splits(int cfg, int M, int N, int K, int* kc, bool mcmc, int cus) {
     return (steps + per - 1) / per;
 }
 
-// The tile configuration: the software-pipelined 128×128 tile (cfg 12) at its best split, or
-// the 64×64 direct-to-register form (cfg 11) where its (coarser) model wins by 10 %: the ~1k-token
-// GEMMs whose 128×128 grid leaves most of the chip idle (1100 × 768 × 768: one pass of 216
-// tiles).  Against rocBLAS / hipBLASLt at the 27 training shapes: profiles/r6*_sgemm_all.jsonl.
+// The tile configuration: the software-pipelined 128×128 tile (cfg 12) at its best split, a
+// software-pipelined 64×128 / 128×64 tile (cfg 17 / 18) where it wins by 3 % (the ~1k-token
+// GEMMs: twice the tiles for the same rounds), or the 64×64 direct-to-register form (cfg 11)
+// where its grid is one pass and it times lower (1100 × 768 × 768: 216 tiles).  Against rocBLAS / hipBLASLt at the 27 training shapes: profiles/r6*_sgemm_all.jsonl.
 // RS_SGEMM_CFG=0..16 forces a configuration (A/B knob).  The choice depends on the shape and the
 // device's CU count only, so a shape's results stay bitwise reproducible on a given device model.
 int sg_pick(int M, int N, int K, bool mcmc, int cus) {
@@ -1010,11 +1018,18 @@ int sg_pick(int M, int N, int K, bool mcmc, int cus) {
         return v ? atoi(v) : -1;
     }();
     if (forced >= 0 && forced < kSgNCfg) return forced;
-    int kc = 0;
-    const int sp12 = sg_splits(12, M, N, K, &kc, mcmc, cus);
-    const double t12 = sg_model(12, M, N, K, sp12, mcmc, cus);
-    const int sp11 = sg_splits(11, M, N, K, &kc, mcmc, cus);
-    return sg_model(11, M, N, K, sp11, mcmc, cus) < 0.9 * t12 ? 11 : 12;
+    int kc = 0, best = 12;
+    double tb = sg_model(12, M, N, K, sg_splits(12, M, N, K, &kc, mcmc, cus), mcmc, cus);
+    for (int cfg : {17, 18}) {                    // a half tile where it wins by 3 %
+        const double t = sg_model(cfg, M, N, K, sg_splits(cfg, M, N, K, &kc, mcmc, cus), mcmc, cus);
+        if (t < 0.97 * tb) {
+            tb = t;
+            best = cfg;
+        }
+    }
+    // the 64×64 direct form where its grid is one pass (no split) and it times lower
+    const long long tiles64 = (long long)((M + 63) / 64) * ((N + 63) / 64);
+    return tiles64 <= cus && sg_model(11, M, N, K, 1, mcmc, cus) < tb ? 11 : best;
 }
 
 bool sk_enabled() {                                 // read per call (tests flip it in-process)
@@ -1169,6 +1184,9 @@ static hipError_t sg_run(int cfg, int M, int N, int K, const float* A, int lda, 
     else if (cfg == 14) SP_FORMS(256, 128, 64, 3, 1);
     else if (cfg == 15) SP_FORMS(128, 128, 64, 3, 1);
     else if (cfg == 16) SP_FORMS(128, 128, 64, 4, 1);
+    else if (cfg == 17) SP_FORMS(64, 128, 32, 2, 2);
+    else if (cfg == 18) SP_FORMS(128, 64, 32, 2, 2);
+    else if (cfg == 19) SP_FORMS(64, 64, 32, 2, 4);
     else {
         static const hipError_t attr = [] {
             for (const void* f : {(const void*)sgemm_d64_kernel<true, true>, (const void*)sgemm_d64_kernel<true, false>,

@@ -75,7 +75,7 @@ CASES = [("nt", 1037, 2304, 768), ("nt", 1037, 768, 3072), ("nt", 301, 21128, 76
 
 @pytest.mark.parametrize("form,M,N,K", CASES)
 @pytest.mark.parametrize("accum", [0, 1])
-@pytest.mark.parametrize("cfg", [0, "streamk", 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16])
+@pytest.mark.parametrize("cfg", [0, "streamk", 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19])
 def test_sgemm_forms_vs_float64(sgemm, form, M, N, K, accum, cfg, monkeypatch):
     """Every tile configuration (k_sgemm.hip kSgCfg) on every form and edge, and the opt-in
     stream-K form of cfg 0 (RS_SGEMM_SK=1: partial tiles handed between workgroups)."""

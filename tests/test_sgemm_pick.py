@@ -28,11 +28,13 @@ def test_software_pipelined_tile_without_split_at_5k_tokens(pick):
     assert pick(5300, 768, 3072) == (12, 1)
 
 
-def test_small_batches_64x64_direct_or_split_k(pick):
+def test_small_batches_64x64_direct_half_tiles_or_split_k(pick):
     # 1100 x 768 x 768: 54 tiles of 128x128; 216 tiles of the 64x64 direct form fill the chip in
-    # one pass (19.4 us against 26.7 us for the 128x128 tile split 4 ways)
+    # one pass (18.7 us against 26.3 us for the 128x128 tile split 4 ways, 21.5 for 64x128 split 2)
     assert pick(1100, 768, 768) == (11, 1)
-    assert pick(2304, 768, 1100, 1) == (12, 2)  # a ~1k-token weight gradient: 216 workgroups
+    # a ~1k-token weight gradient: 216 software-pipelined 64x128 tiles, one pass, no split
+    # (40.8 us against 48.0 for the 128x128 tile split 2 ways, profiles/r6ab_sgemm_all.jsonl)
+    assert pick(2304, 768, 1100, 1) == (17, 1)
     cfg, sp = pick(768, 768, 5300, 1)           # weight gradient over 5.3k tokens
     assert cfg == 12 and sp > 1
     # splits stop at two workgroups per CU (a third short round measured well above the model)
@@ -45,8 +47,8 @@ def test_choice_is_a_function_of_shape_and_cus(pick):
     a = [pick(m, n, k, f) for m, n, k, f in shapes]
     b = [pick(m, n, k, f) for m, n, k, f in shapes]
     assert a == b
-    # a device with fewer CUs rounds differently: on 128 CUs the 128x128 tile split 2 ways fills
-    # the chip where the 64x64 direct form needs two passes
+    # a device with fewer CUs rounds differently: on 128 CUs the 64x64 direct form's 216 tiles
+    # need two passes and the 108 software-pipelined 64x128 tiles fill the chip in one
     assert pick(1100, 768, 768, 0, 256) == (11, 1)
-    assert pick(1100, 768, 768, 0, 128) == (12, 2)
+    assert pick(1100, 768, 768, 0, 128) == (17, 1)
     assert pick(5300, 2304, 768, 0, 0) == (-1, 99)        # rejected

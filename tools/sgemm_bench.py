@@ -4,7 +4,7 @@ decoder, for a 1.1k-token MLM batch and a 5.3k-token RescoreBert batch; every ti
 configuration named in SG_CFGS (default 0: 128x128, 11: 64x64 direct-to-register, 12: 128x128
 software-pipelined)
 and the shape's pick (-1), interleaved in
-one process.  Usage: python tools/sgemm_bench.py"""
+one process; SG_TOKENS picks the token counts (default 1100,5300).  Usage: python tools/sgemm_bench.py"""
 import ctypes
 import json
 import os
@@ -40,7 +40,7 @@ def main():
     CFGS = (-1,) + tuple(int(c) for c in os.environ.get("SG_CFGS", "0,11,12").split(","))
     tot = {c: 0.0 for c in CFGS}
     tot_ref = 0.0
-    for T in (1100, 5300):
+    for T in [int(x) for x in os.environ.get("SG_TOKENS", "1100,5300").split(",")]:
         for (O, I) in [(2304, 768), (768, 768), (3072, 768), (768, 3072), (21128, 768)]:
             if O == 21128 and T > 2000:
                 continue
