@@ -341,6 +341,78 @@ __global__ void tr_colsum_partial_kernel(const float* __restrict__ dy, const flo
     part[(size_t)rb * N + c] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
 }
 
+// Wide form (N % 4 == 0, every training shape): a block of CL column lanes (float4 each, 4 CL
+// columns) x 256 / CL row lanes over a row block, row lane l summing rows r0 + l, r0 + l + RL, ...
+// in order, the row lanes then combined through LDS in a fixed order (groups of 8 lanes, then the
+// groups): 4x the blocks of the form above at a ~1k-token batch, and every lane's loads
+// independent.  Rows <= kOnePass: one row block over all rows (CL = 4: 16 columns a block), written
+// straight to the output (accumulate: added to it), no second launch; otherwise kRB4-row blocks
+// (CL = 16) and the ordered stage 2 below.  MODE 0: part0 = sum dy; 1: part0 = sum dy * xhat; 2:
+// both from one read of dy (LayerNorm gamma into part0, beta into part1).
+constexpr int kRB4 = 128, kOnePass = 2048;
+template <int MODE, bool ONE>
+__global__ void __launch_bounds__(256)
+tr_colsum4_partial_kernel(const float* __restrict__ dy, const float* __restrict__ x, const float2* __restrict__ st,
+                          int M, int N, float* __restrict__ part0, float* __restrict__ part1, int accumulate) {
+    constexpr int CL = ONE ? 4 : 16, RL = 256 / CL, NQ = MODE == 2 ? 2 : 1;
+    __shared__ float4 red[NQ][RL][CL];
+    __shared__ float4 red8[NQ][RL / 8][CL];
+    const int cl = threadIdx.x % CL, rl = threadIdx.x / CL;
+    const int c = blockIdx.x * 4 * CL + cl * 4, rb = blockIdx.y;
+    const int r0 = ONE ? 0 : rb * kRB4, r1 = ONE ? M : min(M, r0 + kRB4);
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+    if (c < N) {
+#pragma unroll 4
+        for (int r = r0 + rl; r < r1; r += RL) {
+            const float4 d = *(const float4*)(dy + (size_t)r * N + c);
+            if (MODE != 1) {
+                b.x += d.x; b.y += d.y; b.z += d.z; b.w += d.w;
+            }
+            if (MODE != 0) {
+                const float2 sr = st[r];
+                const float4 xv = *(const float4*)(x + (size_t)r * N + c);
+                a.x += d.x * ((xv.x - sr.x) * sr.y);
+                a.y += d.y * ((xv.y - sr.x) * sr.y);
+                a.z += d.z * ((xv.z - sr.x) * sr.y);
+                a.w += d.w * ((xv.w - sr.x) * sr.y);
+            }
+        }
+    }
+    red[0][rl][cl] = MODE == 0 ? b : a;
+    if (MODE == 2) red[NQ - 1][rl][cl] = b;
+    __syncthreads();
+    auto add8 = [](const float4* v, int stride) {
+        float4 t = v[0];
+#pragma unroll
+        for (int k = 1; k < 8; ++k) {
+            const float4 u = v[k * stride];
+            t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+        }
+        return t;
+    };
+    if (rl < RL / 8)
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) red8[q][rl][cl] = add8(&red[q][8 * rl][cl], CL);
+    __syncthreads();
+    if (rl == 0 && c < N) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            float4 t = red8[q][0][cl];
+#pragma unroll
+            for (int k = 1; k < RL / 8; ++k) {
+                const float4 v = red8[q][k][cl];
+                t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+            }
+            float4* o = (float4*)((q == 0 ? part0 : part1) + (size_t)rb * N + c);
+            if (ONE && accumulate) {
+                const float4 v = *o;
+                t.x = v.x + t.x; t.y = v.y + t.y; t.z = v.z + t.z; t.w = v.w + t.w;
+            }
+            *o = t;
+        }
+    }
+}
+
 // stage 2: out[c] (+)= sum over row blocks in order
 __global__ void tr_colsum_final_kernel(const float* __restrict__ part, int nrb, int N, float* __restrict__ out,
                                        int accumulate) {
@@ -641,14 +713,57 @@ hipError_t tr_ln_bwd(const float* dy, const float* x, const float2* st, const fl
     return hipGetLastError();
 }
 
-size_t tr_colsum_scratch(int M, int N) { return (size_t)((M + kRB - 1) / kRB) * N * 4; }
+// floats: the kRB-row partials of tr_colsum's narrow form, or two arrays of kRB4-row partials
+size_t tr_colsum_scratch(int M, int N) {
+    return std::max((size_t)((M + kRB - 1) / kRB), (size_t)2 * ((M + kRB4 - 1) / kRB4)) * N * 4;
+}
 
 hipError_t tr_colsum(const float* dy, const float* x, const float2* st, int M, int N, int mode, float* part,
                      float* out, int accumulate, hipStream_t s) {
     if (M <= 0 || N <= 0) return hipSuccess;
+    if (N % 4 == 0) {
+        const dim3 g1((N + 63) / 64), g16((N + 15) / 16);
+        if (M <= kOnePass) {
+            if (mode == 0)
+                hipLaunchKernelGGL((tr_colsum4_partial_kernel<0, true>), g16, dim3(256), 0, s, dy, x, st, M, N, out, out, accumulate);
+            else
+                hipLaunchKernelGGL((tr_colsum4_partial_kernel<1, true>), g16, dim3(256), 0, s, dy, x, st, M, N, out, out, accumulate);
+            return hipGetLastError();
+        }
+        const int nrb = (M + kRB4 - 1) / kRB4;
+        if (mode == 0)
+            hipLaunchKernelGGL((tr_colsum4_partial_kernel<0, false>), dim3(g1.x, nrb), dim3(256), 0, s, dy, x, st, M, N, part, part, 0);
+        else
+            hipLaunchKernelGGL((tr_colsum4_partial_kernel<1, false>), dim3(g1.x, nrb), dim3(256), 0, s, dy, x, st, M, N, part, part, 0);
+        hipLaunchKernelGGL(tr_colsum_final_kernel, g1, dim3(64), 0, s, part, nrb, N, out, accumulate);
+        return hipGetLastError();
+    }
     const int nrb = (M + kRB - 1) / kRB;
     hipLaunchKernelGGL(tr_colsum_partial_kernel, dim3((N + 255) / 256, nrb), dim3(256), 0, s, dy, x, st, M, N, mode, part);
     hipLaunchKernelGGL(tr_colsum_final_kernel, dim3((N + 63) / 64), dim3(64), 0, s, part, nrb, N, out, accumulate);
+    return hipGetLastError();
+}
+
+// LayerNorm gamma (sum dy * xhat) and beta (sum dy) gradients from one read of dy: the two
+// tr_colsum calls' results bit for bit (the same per-column order), half the dy reads and launches
+hipError_t tr_colsum_ln(const float* dy, const float* x, const float2* st, int M, int N, float* part, float* out_g,
+                        float* out_b, hipStream_t s) {
+    if (M <= 0 || N <= 0) return hipSuccess;
+    if (N % 4) {
+        if (hipError_t e = tr_colsum(dy, x, st, M, N, 1, part, out_g, 0, s)) return e;
+        return tr_colsum(dy, nullptr, nullptr, M, N, 0, part, out_b, 0, s);
+    }
+    if (M <= kOnePass) {
+        hipLaunchKernelGGL((tr_colsum4_partial_kernel<2, true>), dim3((N + 15) / 16), dim3(256), 0, s, dy, x, st, M, N, out_g,
+                           out_b, 0);
+        return hipGetLastError();
+    }
+    const int nrb = (M + kRB4 - 1) / kRB4;
+    float* part_b = part + (size_t)nrb * N;         // tr_colsum_scratch: room for two
+    hipLaunchKernelGGL((tr_colsum4_partial_kernel<2, false>), dim3((N + 63) / 64, nrb), dim3(256), 0, s, dy, x, st, M, N, part,
+                       part_b, 0);
+    hipLaunchKernelGGL(tr_colsum_final_kernel, dim3((N + 63) / 64), dim3(64), 0, s, part, nrb, N, out_g, 0);
+    hipLaunchKernelGGL(tr_colsum_final_kernel, dim3((N + 63) / 64), dim3(64), 0, s, part_b, nrb, N, out_b, 0);
     return hipGetLastError();
 }
 

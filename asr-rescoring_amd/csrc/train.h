@@ -82,6 +82,8 @@ hipError_t tr_ln_bwd(const float* dy, const float* x, const float2* st, const fl
 size_t tr_colsum_scratch(int M, int N);
 hipError_t tr_colsum(const float* dy, const float* x, const float2* st, int M, int N, int mode, float* part,
                      float* out, int accumulate, hipStream_t s);
+hipError_t tr_colsum_ln(const float* dy, const float* x, const float2* st, int M, int N, float* part, float* out_g,
+                        float* out_b, hipStream_t s);
 hipError_t tr_word_grad(const float* dx0, const int* utok, const int* toff, const int* rows, int n_uniq, int H,
                         float* dword, hipStream_t s);
 hipError_t tr_pos_grad(const float* dx0, const int* seq_off, int S, int tmax, int H, float* dpos, hipStream_t s);

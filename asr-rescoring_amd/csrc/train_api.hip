@@ -523,8 +523,7 @@ int encoder_backward(StepCtx& c) {
     for (int l = cf.layers - 1; l >= 0; --l) {
         const TLayer& L = t->lay[l];
         StepCtx::LA& a = c.la[l];
-        TRY_HIP(tr_colsum(dA, a.x2, a.st2, M, H, 1, part, Gm + L.g2, 0, st));
-        TRY_HIP(tr_colsum(dA, nullptr, nullptr, M, H, 0, part, Gm + L.be2, 0, st));
+        TRY_HIP(tr_colsum_ln(dA, a.x2, a.st2, M, H, part, Gm + L.g2, Gm + L.be2, st));
         TRY_HIP(tr_ln_bwd(dA, a.x2, a.st2, Pm + L.g2, dB, M, H, st));              // dB = dx2
         // BertOutput dropout: the dense branch sees dx2 * mask * scale (in the free dQKV
         // buffer), the residual branch dx2 itself (dB, copied into dA below)
@@ -541,8 +540,7 @@ int encoder_backward(StepCtx& c) {
         RS_TRY(gemm_tn(t, st, M, F, H, dF, a.h1, Gm + L.w1, 0.f));
         TRY_HIP(hipMemcpyAsync(dA, dB, MH * 4, hipMemcpyDeviceToDevice, st));      // residual
         RS_TRY(gemm_nn(t, st, M, F, H, dF, Pm + L.w1, dA, 1.f));                     // dA = d h1
-        TRY_HIP(tr_colsum(dA, a.x1, a.st1, M, H, 1, part, Gm + L.g1, 0, st));
-        TRY_HIP(tr_colsum(dA, nullptr, nullptr, M, H, 0, part, Gm + L.be1, 0, st));
+        TRY_HIP(tr_colsum_ln(dA, a.x1, a.st1, M, H, part, Gm + L.g1, Gm + L.be1, st));
         TRY_HIP(tr_ln_bwd(dA, a.x1, a.st1, Pm + L.g1, dB, M, H, st));              // dB = dx1
         // BertSelfOutput dropout: masked copy for the dense branch in the free dF buffer
         const float* dBs = dB;
@@ -561,8 +559,7 @@ int encoder_backward(StepCtx& c) {
     }
     // embedding dropout: d(LN output) = d h0 * mask * scale
     if (c.th_hidden) TRY_HIP(tr_dropout(dA, dA, (long long)MH, c.drop(0, false), st));
-    TRY_HIP(tr_colsum(dA, c.x0, c.st0, M, H, 1, part, Gm + t->o_eg, 0, st));
-    TRY_HIP(tr_colsum(dA, nullptr, nullptr, M, H, 0, part, Gm + t->o_eb, 0, st));
+    TRY_HIP(tr_colsum_ln(dA, c.x0, c.st0, M, H, part, Gm + t->o_eg, Gm + t->o_eb, st));
     TRY_HIP(tr_ln_bwd(dA, c.x0, c.st0, Pm + t->o_eg, dB, M, H, st));                // dB = dx0
     // word embeddings: += (the tied MLM decoder already wrote its part)
     TRY_HIP(tr_word_grad(dB, c.dm + c.i_utok, c.dm + c.i_toff, c.dm + c.i_ord, c.n_uniq, H, Gm + t->o_word, st));
@@ -667,8 +664,7 @@ int rs_train_step_mlm(rs_trainer* t, const int32_t* d_ids, const int32_t* h_seq_
     TRY_HIP(tr_colsum(c.logits, nullptr, nullptr, M, V, 0, c.part, Gm + t->o_db, 0, st));
     RS_TRY(gemm_tn(t, st, M, V, H, c.logits, c.th, Gm + t->o_word, 0.f));          // tied decoder part
     RS_TRY(gemm_nn(t, st, M, V, H, c.logits, Pm + t->o_word, dT, 0.f));
-    TRY_HIP(tr_colsum(dT, c.tx, c.tst, M, H, 1, c.part, Gm + t->o_tg, 0, st));
-    TRY_HIP(tr_colsum(dT, nullptr, nullptr, M, H, 0, c.part, Gm + t->o_tb, 0, st));
+    TRY_HIP(tr_colsum_ln(dT, c.tx, c.tst, M, H, c.part, Gm + t->o_tg, Gm + t->o_tb, st));
     TRY_HIP(tr_ln_bwd(dT, c.tx, c.tst, Pm + t->o_tg, dT2, M, H, st));
     TRY_HIP(tr_gelu_bwd(dT2, c.tpre, (long long)M * H, st));
     TRY_HIP(tr_colsum(dT2, nullptr, nullptr, M, H, 0, c.part, Gm + t->o_bt, 0, st));
