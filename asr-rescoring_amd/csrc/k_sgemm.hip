@@ -259,111 +259,7 @@ sgemm_dma_kernel(const float* __restrict__ A, int lda, const float* __restrict__
         }
 }
 
-// Software-pipelined form: a 3-stage LDS ring, the DMA two K-steps ahead, and the next
-// K-step's fragments read from LDS while this K-step's MFMAs run (two fragment sets in
-// registers).  The plain form above runs barrier -> fragment reads -> DMA issue -> MFMAs in
-// every wave, so the two workgroups sharing a SIMD fall into lockstep and the MFMA pipe idles
-// through both waves' read / issue / barrier phases; here those phases of step t+1 hide under
-// step t's MFMAs.  Per iteration t: vmcnt(0) (step t+1's DMA, issued one iteration ago, landed
-// for this wave), barrier (landed for every wave; every wave finished reading buffer (t-1)%3),
-// fragment reads of step t+1 (issued first: an LDS read placed after an LDS-DMA issue would get
-// a compiler vmcnt(0) in front of it), DMA of step t+2 into buffer (t+2)%3 = (t-1)%3, MFMAs of
-// step t.
-template <bool AKC, bool BKC, int BM, int BN, int TM, int BK, int OCC>
-__global__ void __launch_bounds__((BM / TM) * (BN / 64) * 64, OCC * (BM / TM) * (BN / 64) / 4)
-sgemm_pipe_kernel(const float* __restrict__ A, int lda, const float* __restrict__ B, int ldb, float* __restrict__ C,
-                  int ldc, int M, int N, int K, int kc, int accum, float* __restrict__ ws) {
-    constexpr int WM = BM / TM, WN = BN / 64, NW = WM * WN, MT = TM / 32, HK = BK / 2;
-    constexpr int IMG_A = BM * BK * 4, STAGE = (BM + BN) * BK * 4;
-    using OA = SgOperand<AKC, BM, NW, BK>;
-    using OB = SgOperand<BKC, BN, NW, BK>;
-    __shared__ __attribute__((aligned(16))) char smem[3 * STAGE];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    int tm, tn, z;
-    sg_tile((M + BM - 1) / BM, (N + BN - 1) / BN, tm, tn, z);
-    const int m0 = tm * BM, n0 = tn * BN;
-    const int kb = z * kc, ke = min(K, kb + kc);
-    const int nt = (ke - kb + BK - 1) / BK;
-    const int wm = (wave % WM) * TM, wn = (wave / WM) * 64;
-    const int h = lane >> 5, c = lane & 31;
-
-    OA oa;
-    OB ob;
-    oa.init(A, lda, M, m0, wave, lane);
-    ob.init(B, ldb, N, n0, wave, lane);
-
-    f32x16_t acc[MT][2];
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-    auto stage = [&](int t) {
-        char* dst = smem + (t % 3) * STAGE;
-        oa.stage(dst, wave, kb + t * BK, ke);
-        ob.stage(dst + IMG_A, wave, kb + t * BK, ke);
-    };
-    float fa[MT][HK], fb[2][HK], ga[MT][HK], gb[2][HK];
-    auto frags = [&](int t, float (&xa)[MT][HK], float (&xb)[2][HK]) {
-        const char* st = smem + (t % 3) * STAGE;
-#pragma unroll
-        for (int i = 0; i < MT; ++i) OA::frag(st, wm + 32 * i + c, h, xa[i]);
-#pragma unroll
-        for (int j = 0; j < 2; ++j) OB::frag(st + IMG_A, wn + 32 * j + c, h, xb[j]);
-    };
-    stage(0);
-    if (nt > 1) stage(1);
-    if (nt > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OA::NP + OB::NP) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    frags(0, fa, fb);
-    // one K-step: MFMAs on (xa, xb) = step t's fragments while step t+1's are read into (ya, yb);
-    // the loop runs two steps per trip with the register sets swapping roles (no copies)
-    auto step = [&](int t, float (&xa)[MT][HK], float (&xb)[2][HK], float (&ya)[MT][HK], float (&yb)[2][HK]) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (t + 1 < nt) frags(t + 1, ya, yb);
-        __builtin_amdgcn_sched_barrier(0);
-        if (t + 2 < nt) stage(t + 2);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int kk = 0; kk < HK; ++kk)
-#pragma unroll
-            for (int i = 0; i < MT; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(xa[i][kk], xb[j][kk], acc[i][j], 0, 0, 0);
-    };
-    for (int t = 0; t < nt; t += 2) {
-        step(t, fa, fb, ga, gb);
-        if (t + 1 < nt) step(t + 1, ga, gb, fa, fb);
-    }
-
-    float* P = ws ? ws + (size_t)z * M * N : nullptr;
-#pragma unroll
-    for (int i = 0; i < MT; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int col = n0 + wn + 32 * j + c;
-            if (col >= N) continue;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * h;
-                if (row >= M) continue;
-                if (P) {
-                    P[(size_t)row * N + col] = acc[i][j][r];
-                } else {
-                    float* o = C + (size_t)row * ldc + col;
-                    *o = accum ? acc[i][j][r] + *o : acc[i][j][r];
-                }
-            }
-        }
-}
-
-// Software-pipelined form with a straight-line K loop (cfg 12-16).  The forms above read a
+// Software-pipelined form with a straight-line K loop (cfg 12, 17, 18).  The form above reads a
 // K-step's fragments between the barrier and its MFMAs, so every wave of a CU reads its 16 KiB
 // from LDS at the same moment while its MFMA pipe idles: at one workgroup per CU (a 5.3k-token
 // GEMM with N = 768 has 252 tiles of 128×128) that is ≈ 20 % of each K-step.  Here the
@@ -897,27 +793,25 @@ sgemm_splitk_sum_kernel(const float* __restrict__ ws, int splits, int M, int N, 
     *o = s;
 }
 
-// Tile configurations: 0 = 128×128×32 (4 waves of 64×64, 2 workgroups per CU, 64 KiB LDS),
-// 1 = 128×128×16 (the same waves, 4 workgroups per CU, 32 KiB LDS: a mid-size GEMM's tiles all
-// resident at once), 2 = 256×128×32 (8 waves of 64×64, 1 per CU; half the operand bytes per
-// FLOP of a 128×128 tile on the A side).
-struct SgCfg { int bm, bn, bk, occ; };
+// Tile configurations (RS_SGEMM_CFG indices; the retired ones — measured, never picked, their
+// instantiations removed — keep their index and fail with hipErrorInvalidValue):
+//   0  128×128×32 sgemm_dma_kernel, 4 waves of 64×64, 2 workgroups per CU (the round-3 default)
+//   9  192×128×32 sgemm_dma_kernel, 4 waves of 96×64
+//   11 64×64 sgemm_d64_kernel (direct to registers)
+//   12 128×128 sgemm_sp_kernel (software-pipelined; the round-6 default), 17 / 18 its 64×128 /
+//      128×64 half tiles (4 waves of 32×64)
+//   retired: 1-8 and 10 (sgemm_dma_kernel at BK 16, 128×64, 64×64, 256×128, 256×256; the round-2
+//   3-stage sgemm_pipe_kernel; profiles/r5e_sgemm_all.jsonl), 13-16 and 19 (sgemm_sp_kernel at
+//   3 / 4 stages, 192×128, 256×128, 64×64; profiles/r6y_sgemm_split_sweep.txt, r6aa_*)
+struct SgCfg { int bm, bn, bk, occ, live; };
 constexpr int kSgNCfg = 20;
-constexpr SgCfg kSgCfg[kSgNCfg] = {{128, 128, 32, 2}, {128, 128, 16, 4}, {256, 128, 32, 1},
-                                   {128, 128, 16, 3}, {128, 128, 32, 1},    // 3, 4: sgemm_pipe_kernel
-                                   {128, 64, 32, 2},  {128, 64, 32, 3},     // 5, 6: 4 waves of 32×64
-                                   {64, 64, 32, 4},   {64, 64, 32, 6},      // 7, 8: 2 waves of 32×64
-                                   {192, 128, 32, 2},                       // 9: 4 waves of 96×64
-                                   {256, 256, 32, 1},                       // 10: 8 waves of 128×64
-                                   {64, 64, 32, 2},                         // 11: sgemm_d64_kernel
-                                   {128, 128, 32, 2},                       // 12-16: sgemm_sp_kernel: 2 stages,
-                                   {192, 128, 32, 1},                       //   3 (4 waves of 96×64),
-                                   {256, 128, 32, 1},                       //   3 (8 waves of 64×64),
-                                   {128, 128, 32, 1},                       //   3,
-                                   {128, 128, 32, 1},                       //   4 stages;
-                                   {64, 128, 32, 2},                        // 17-19: 2 stages, 4 waves of
-                                   {128, 64, 32, 2},                        //   32×64 / 2 waves of 32×64
-                                   {64, 64, 32, 4}};
+constexpr SgCfg kSgCfg[kSgNCfg] = {{128, 128, 32, 2, 1}, {128, 128, 16, 4, 0}, {256, 128, 32, 1, 0},
+                                   {128, 128, 16, 3, 0}, {128, 128, 32, 1, 0}, {128, 64, 32, 2, 0},
+                                   {128, 64, 32, 3, 0},  {64, 64, 32, 4, 0},   {64, 64, 32, 6, 0},
+                                   {192, 128, 32, 2, 1}, {256, 256, 32, 1, 0}, {64, 64, 32, 2, 1},
+                                   {128, 128, 32, 2, 1}, {192, 128, 32, 1, 0}, {256, 128, 32, 1, 0},
+                                   {128, 128, 32, 1, 0}, {128, 128, 32, 1, 0}, {64, 128, 32, 2, 1},
+                                   {128, 64, 32, 2, 1},  {64, 64, 32, 4, 0}};
 
 // Modelled time (µs) of one configuration at a split count: dispatch rounds × (K-steps per
 // workgroup × the time a CU takes per K-step with its resident workgroups + a per-round
@@ -1010,14 +904,14 @@ int sg_splits(int cfg, int M, int N, int K, int* kc, bool mcmc, int cus) {
 // software-pipelined 64×128 / 128×64 tile (cfg 17 / 18) where it wins by 3 % (the ~1k-token
 // GEMMs: twice the tiles for the same rounds), or the 64×64 direct-to-register form (cfg 11)
 // where its grid is one pass and it times lower (1100 × 768 × 768: 216 tiles).  Against rocBLAS / hipBLASLt at the 27 training shapes: profiles/r6*_sgemm_all.jsonl.
-// RS_SGEMM_CFG=0..16 forces a configuration (A/B knob).  The choice depends on the shape and the
+// RS_SGEMM_CFG forces a live configuration (A/B knob).  The choice depends on the shape and the
 // device's CU count only, so a shape's results stay bitwise reproducible on a given device model.
 int sg_pick(int M, int N, int K, bool mcmc, int cus) {
     static const int forced = [] {
         const char* v = getenv("RS_SGEMM_CFG");
         return v ? atoi(v) : -1;
     }();
-    if (forced >= 0 && forced < kSgNCfg) return forced;
+    if (forced >= 0 && forced < kSgNCfg && kSgCfg[forced].live) return forced;
     int kc = 0, best = 12;
     double tb = sg_model(12, M, N, K, sg_splits(12, M, N, K, &kc, mcmc, cus), mcmc, cus);
     for (int cfg : {17, 18}) {                    // a half tile where it wins by 3 %
@@ -1087,6 +981,7 @@ int tr_sgemm_failed() {
 size_t tr_sgemm_ws_floats(int M, int N, int K) {
     size_t w = sk_enabled() ? (size_t)kSkMaxG * 16384 : 0;   // stream-K partial slots (128×128 each)
     for (int cfg = 0; cfg < kSgNCfg; ++cfg) {  // any configuration the picker or the knob may choose
+        if (!kSgCfg[cfg].live) continue;
         int kc = 0;
         for (int mc = 0; mc < 2; ++mc) {
             const int s = sg_splits(cfg, M, N, K, &kc, mc != 0, n_cus_sg());
@@ -1101,7 +996,7 @@ static hipError_t sg_run(int cfg, int M, int N, int K, const float* A, int lda, 
     if (M <= 0 || N <= 0) return hipSuccess;
     // 16-B DMA pieces along each operand's contiguous dimension, float4 rows of C (split-K sum)
     if (N % 4 || lda % 4 || ldb % 4 || ldc % 4 || (a_kc ? K % 4 : M % 4) || (b_kc ? K % 4 : N % 4) ||
-        ((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 || cfg < 0 || cfg >= kSgNCfg)
+        ((uintptr_t)A | (uintptr_t)B | (uintptr_t)C) % 16 || cfg < 0 || cfg >= kSgNCfg || !kSgCfg[cfg].live)
         return hipErrorInvalidValue;
     // 32-bit byte offsets into each operand (buffer descriptors)
     const long long ea = (long long)(a_kc ? M : K) * lda * 4, eb = (long long)(b_kc ? N : K) * ldb * 4;
@@ -1169,24 +1064,10 @@ static hipError_t sg_run(int cfg, int M, int N, int K, const float* A, int lda, 
         else SP_LAUNCH(false, false, BM_, BN_, TM_, NS_, OCC_);                \
     } while (0)
     if (cfg == 0) SG_FORMS(sgemm_dma_kernel, 128, 128, 64, 32, 2);
-    else if (cfg == 1) SG_FORMS(sgemm_dma_kernel, 128, 128, 64, 16, 4);
-    else if (cfg == 2) SG_FORMS(sgemm_dma_kernel, 256, 128, 64, 32, 1);
-    else if (cfg == 3) SG_FORMS(sgemm_pipe_kernel, 128, 128, 64, 16, 3);
-    else if (cfg == 4) SG_FORMS(sgemm_pipe_kernel, 128, 128, 64, 32, 1);
-    else if (cfg == 5) SG_FORMS(sgemm_dma_kernel, 128, 64, 32, 32, 2);
-    else if (cfg == 6) SG_FORMS(sgemm_dma_kernel, 128, 64, 32, 32, 3);
-    else if (cfg == 7) SG_FORMS(sgemm_dma_kernel, 64, 64, 32, 32, 4);
-    else if (cfg == 8) SG_FORMS(sgemm_dma_kernel, 64, 64, 32, 32, 6);
     else if (cfg == 9) SG_FORMS(sgemm_dma_kernel, 192, 128, 96, 32, 2);
-    else if (cfg == 10) SG_FORMS(sgemm_dma_kernel, 256, 256, 128, 32, 1);
     else if (cfg == 12) SP_FORMS(128, 128, 64, 2, 2);
-    else if (cfg == 13) SP_FORMS(192, 128, 96, 3, 1);
-    else if (cfg == 14) SP_FORMS(256, 128, 64, 3, 1);
-    else if (cfg == 15) SP_FORMS(128, 128, 64, 3, 1);
-    else if (cfg == 16) SP_FORMS(128, 128, 64, 4, 1);
     else if (cfg == 17) SP_FORMS(64, 128, 32, 2, 2);
     else if (cfg == 18) SP_FORMS(128, 64, 32, 2, 2);
-    else if (cfg == 19) SP_FORMS(64, 64, 32, 2, 4);
     else {
         static const hipError_t attr = [] {
             for (const void* f : {(const void*)sgemm_d64_kernel<true, true>, (const void*)sgemm_d64_kernel<true, false>,
