@@ -182,6 +182,12 @@ def main():
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: running {world} rank(s)", file=sys.stderr)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one JSON line on stdout from the whole job (the torch.distributed.run form prints every rank's
+    # stdout): ranks > 0 write stdout to stderr from here on, native libraries included (gloo's
+    # connection messages go to fd 1)
+    if world > 1 and rank != 0:
+        sys.stdout.flush()
+        os.dup2(2, 1)
     # RS_BENCH_DEVICE (rehearsal only): every rank on this one GPU (a multi-rank run on a 1-GPU box,
     # with RS_DIST_BACKEND=gloo for the exchange); unset on a real node: rank r on GPU LOCAL_RANK
     if os.environ.get("RS_BENCH_DEVICE") is not None:
@@ -190,7 +196,15 @@ def main():
     dev = torch.device("cuda", local)
     from asr_rescoring_amd import shard
     if world > 1 or args.force_gather:
-        shard.init_from_env(local, force=args.force_gather)
+        sys.stdout.flush()
+        fd1 = os.dup(1)
+        os.dup2(2, 1)                             # (rank 0 too, while the group forms)
+        try:
+            shard.init_from_env(local, force=args.force_gather)
+        finally:
+            sys.stdout.flush()
+            os.dup2(fd1, 1)
+            os.close(fd1)
     gather = dist.is_initialized()
     xdev = shard.exchange_device(dist.get_backend() if gather else None, dev, dev)
 
