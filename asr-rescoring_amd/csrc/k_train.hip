@@ -624,6 +624,34 @@ __global__ void tr_adamw_kernel(float* __restrict__ p, const float* __restrict__
     }
 }
 
+// The same update on float4 quads (16-B aligned arrays, n4 = n / 4 quads; the host runs the
+// scalar kernel over the n % 4 tail): every element's arithmetic is the scalar kernel's, bit for
+// bit, at 16-B accesses (the scalar form moved its 28 B per parameter at ≈ 63 % of HBM peak)
+__device__ __forceinline__ float adamw1(float& pi, float gi, float& mi, float& vi, float decay, float b1w, float b2,
+                                        float b2w, float step_size, float bc2_sqrt, float eps) {
+    pi *= decay;
+    mi = mi + b1w * (gi - mi);
+    vi = vi * b2 + b2w * gi * gi;
+    const float denom = sqrtf(vi) / bc2_sqrt + eps;
+    pi = pi - step_size * (mi / denom);
+    return pi;
+}
+__global__ void tr_adamw4_kernel(float4* __restrict__ p, const float4* __restrict__ g, float4* __restrict__ m,
+                                 float4* __restrict__ v, long long n4, float decay, float b1w, float b2, float b2w,
+                                 float step_size, float bc2_sqrt, float eps) {
+    for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+        float4 pi = p[i], mi = m[i], vi = v[i];
+        const float4 gi = g[i];
+        adamw1(pi.x, gi.x, mi.x, vi.x, decay, b1w, b2, b2w, step_size, bc2_sqrt, eps);
+        adamw1(pi.y, gi.y, mi.y, vi.y, decay, b1w, b2, b2w, step_size, bc2_sqrt, eps);
+        adamw1(pi.z, gi.z, mi.z, vi.z, decay, b1w, b2, b2w, step_size, bc2_sqrt, eps);
+        adamw1(pi.w, gi.w, mi.w, vi.w, decay, b1w, b2, b2w, step_size, bc2_sqrt, eps);
+        m[i] = mi;
+        v[i] = vi;
+        p[i] = pi;
+    }
+}
+
 __global__ void tr_dropout_kernel(float* dst, const float* src, long long n, TrDrop dr) {
     for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
         dst[i] = tr_drop(dr, (unsigned long long)i, src[i]);
@@ -810,6 +838,15 @@ hipError_t tr_ce(float* logits, const int* labels, int M, int V, float* row_loss
 hipError_t tr_adamw(float* p, const float* g, float* m, float* v, long long n, float decay, float b1w, float b2,
                     float b2w, float step_size, float bc2_sqrt, float eps, hipStream_t s) {
     if (n <= 0) return hipSuccess;
+    if ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0 && n >= 4) {
+        const long long n4 = n / 4, done = n4 * 4;
+        hipLaunchKernelGGL(tr_adamw4_kernel, dim3(grid_for(n4, 256)), dim3(256), 0, s, (float4*)p, (const float4*)g,
+                           (float4*)m, (float4*)v, n4, decay, b1w, b2, b2w, step_size, bc2_sqrt, eps);
+        if (done < n)
+            hipLaunchKernelGGL(tr_adamw_kernel, dim3(1), dim3(64), 0, s, p + done, g + done, m + done, v + done, n - done,
+                               decay, b1w, b2, b2w, step_size, bc2_sqrt, eps);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(tr_adamw_kernel, dim3(grid_for(n, 256)), dim3(256), 0, s, p, g, m, v, n, decay, b1w, b2, b2w,
                        step_size, bc2_sqrt, eps);
     return hipGetLastError();
