@@ -65,6 +65,31 @@ def test_gradients_match_autograd(method):
         tr.close()
 
 
+def test_gradients_match_autograd_past_the_one_pass_column_sums():
+    """A batch of more than 2048 token rows: the trainer's bias / LayerNorm column sums take their
+    two-stage form (k_train.hip tr_colsum, kOnePass) and the GEMM picker other tiles — gradients
+    against torch autograd as above."""
+    from asr_rescoring_amd.train import RescoreBertTrainer
+    from oracle.train_ref import TorchTrainer
+    w = _weights()
+    nb, seqs, target, am, cer = _batch(5, n_utt=12, n_best=16, len_hi=30)
+    assert int(nb.hyp_off[-1]) > 2048
+    tr = RescoreBertTrainer(w, BERT_TINY, method="MD_MWER", md_loss_weight=0.5, **NO_DROP)
+    ref = TorchTrainer(w, BERT_TINY)
+    try:
+        loss, sc = tr.step(nb.tokens, nb.hyp_off, nb.utt_off, target, am, cer, update=False)
+        rloss, rsc = ref.step(seqs, target, am, cer, n_best=16, method="MD_MWER", md_loss_weight=0.5, update=False)
+        assert abs(loss - rloss) <= 1e-4 * abs(rloss)
+        assert np.abs(sc - rsc).max() <= 1e-4 * np.abs(rsc).max()
+        gnorm = np.sqrt(sum(float(np.sum(ref.grad(k).astype(np.float64) ** 2)) for k in tr.shapes))
+        for k in tr.shapes:
+            g, rg = tr.grad(k), ref.grad(k)
+            rel = np.linalg.norm(g - rg) / max(np.linalg.norm(rg), 1e-4 * gnorm)
+            assert rel < 2e-4, (k, rel, np.linalg.norm(rg))
+    finally:
+        tr.close()
+
+
 @pytest.mark.parametrize("method", ["MD", "MD_MWER", "MD_MWED"])
 def test_rescorebert_training_matches_reference_run(method):
     """Two epochs of the reference's RescoreBert/main.py training loop (F6): epoch losses, dev
